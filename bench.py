@@ -1,0 +1,306 @@
+"""Benchmark: stereo pairs/sec of the ESMStereo hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one pass of the hot path (models/ESMStereo.py:700-745: cost volume -> 3-D stems ->
+3-D hourglass -> regression -> ESM/ShuffleMixer upsampler -> x4) over one batch of synthetic
+input that is already resident in HBM: the workload is BASELINE.json configs[1], ESMStereo-S
+(mobilenetv2_100 channel ladder, cv_scale 16, gwc volume) at KITTI 384x1248, maxdisp 192,
+batch 1 per GPU.  The backbone side that produces the matching features is out of scope
+ and runs once, before timing.  Each rank processes its own batch (weak
+scaling); with N > 1 the disparity maps are all-gathered over RCCL every step.
+
+Printed (rank 0, one JSON line): the contract fields, plus
+  roofline      dominant kernel of the step (longest hipEvent-probed launch), its algorithmic
+                FLOPs or bytes / its live average duration (hipEvent pair around that launch
+                on every timed replay), against the fp32 MFMA or HBM peak;
+  roofline_cost_volume  the gwc cost-volume kernel at KITTI full res for ESMStereo-L
+                (the north_star headline: HBM fraction of the volume kernel);
+  cpu_baseline  the CPU oracle (oracle/esm_oracle.py, PyTorch fp32 on the host cores) timed
+                on a bounded sample of the same workload, rank 0 at N = 1 only;
+  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import esmstereo_amd as E  # noqa: E402
+
+VARIANTS = {"S": ("mobilenetv2_100", 16), "M": ("efficientnet_b2", 8), "L": ("efficientnet_b2", 4)}
+METRIC = "stereo pairs/sec at 384×1248 maxdisp=192; EPE vs reference"
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F32_MFMA_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_16x16x4_f32), spec
+
+
+def seeded_init(model: torch.nn.Module, seed: int) -> None:
+    """Random-init weights of the architecture (no checkpoints offline): He-normal convs,
+    randomised eval BatchNorm statistics."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (torch.nn.Conv2d, torch.nn.Conv3d, torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d)):
+                w = m.weight
+                fan = w[0].numel() if not isinstance(m, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d)) \
+                    else max(1, w.shape[0] * w[0, 0].numel() // (2 ** (w.dim() - 2)))
+                w.copy_(torch.randn(w.shape, generator=g) * math.sqrt(2.0 / fan))
+                if m.bias is not None:
+                    m.bias.copy_(torch.rand(m.bias.shape, generator=g) * 0.2 - 0.1)
+            elif isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
+                m.weight.copy_(torch.rand(m.weight.shape, generator=g) * 0.4 + 0.8)
+                m.bias.copy_(torch.rand(m.bias.shape, generator=g) * 0.2 - 0.1)
+                m.running_mean.copy_(torch.rand(m.running_mean.shape, generator=g) * 0.2 - 0.1)
+                m.running_var.copy_(torch.rand(m.running_var.shape, generator=g) + 0.5)
+
+
+def synthetic_pair(B: int, H: int, W: int, maxdisp: int, seed: int, device) -> tuple:
+    """Smooth sinusoid texture (ImageNet-normalised range) + right view shifted by a planar
+    disparity field."""
+    g = torch.Generator().manual_seed(seed)
+    yy, xx = torch.meshgrid(torch.arange(H, dtype=torch.float32), torch.arange(W + maxdisp, dtype=torch.float32),
+                            indexing="ij")
+    full = torch.zeros(B, 3, H, W + maxdisp)
+    for b in range(B):
+        for c in range(3):
+            for _ in range(8):
+                fx, fy, ph = (torch.rand(3, generator=g) * torch.tensor([0.33, 0.33, 6.28]) + 0.02).tolist()
+                full[b, c] += torch.sin(fx * xx + fy * yy + ph) / 2
+    left = full[..., maxdisp:]
+    right = torch.empty_like(left)
+    for y in range(H):
+        d = int((0.1 + 0.8 * y / max(1, H - 1)) * (maxdisp - 1))
+        right[:, :, y] = full[:, :, y, maxdisp - d: maxdisp - d + W]
+    return left.to(device), right.to(device)
+
+
+def kernel_roofline(meta: dict, avg_ms: float) -> dict:
+    sec = avg_ms * 1e-3
+    if meta["kind"] == "conv":
+        ach = meta["flops"] / sec / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_F32_MFMA_TFS, 4)}
+    ach = meta["bytes"] / sec / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4)}
+
+
+def pmc_traffic(name: str, workload: str):
+    """HBM bytes per launch of `name` from the committed rocprofv3 PMC summary, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tab = json.load(f)
+    e = tab.get(workload, {}).get(name)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def find_dominant(hp: E.HotPath, reps: int = 3) -> tuple:
+    graph = hp.graph
+    hp.graph = False
+    times = []
+    for i in range(hp.num_ops):
+        hp.set_probe(i, reps + 1)
+        for _ in range(reps + 1):
+            hp.launch()
+        torch.cuda.synchronize()
+        t = sorted(hp.probe_read()[1:])
+        times.append(t[len(t) // 2])
+    hp.set_probe(-1, 1)
+    hp.graph = graph
+    dom = max(range(len(times)), key=lambda i: times[i])
+    return dom, times
+
+
+def cost_volume_roofline(device, reps: int = 20) -> dict:
+    """gwc kernel alone at ESMStereo-L KITTI full res (B=1, C=64, 96x312, D=48, G=32)."""
+    B, C, H, W, D, G = 1, 64, 96, 312, 48, 32
+    L = torch.randn(B, C, H, W, device=device)
+    R = torch.randn(B, C, H, W, device=device)
+    V = torch.empty(B, G, D, H, W, device=device)
+    ctx = E.engine.Ctx(device)
+    for _ in range(3):
+        ctx.gwc(L, R, None, V, B, C, H, W, D, G)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record()
+        ctx.gwc(L, R, None, V, B, C, H, W, D, G)
+        b.record()
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)
+    avg = sum(ms) / len(ms)
+    byts = 4 * B * (2 * C * H * W + G * D * H * W)
+    ach = byts / (avg * 1e-3) / 1e9
+    return {"kernel": "gwc_volume", "config": "ESMStereo-L KITTI 384x1248 md192: B=1 C=64 96x312 D=48 G=32",
+            "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2),
+            "min_us": round(ms[0] * 1e3, 2)}
+
+
+def cpu_baseline(model, ml, mr, att, up, args, budget_s: float) -> tuple:
+    from oracle import esm_oracle as O
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    ins = (ml.cpu(), mr.cpu(), None if att is None else att.cpu(), [u.cpu() for u in up])
+    backbone, cvs = VARIANTS[args.variant]
+    reps, t0, out = 0, time.perf_counter(), None
+    with torch.no_grad():
+        while True:
+            out = O.hot_path(sd, cvs, args.maxdisp, args.cv == "gwc", *ins)
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s and reps >= 2:
+                break
+    el = time.perf_counter() - t0
+    B = ml.shape[0]
+    return ({"value": round(B * reps / el, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+             "sample": f"{reps} hot-path forwards of the same {B}x{args.height}x{args.width} md{args.maxdisp} "
+                       f"ESMStereo-{args.variant} {args.cv} input, oracle/esm_oracle.py (PyTorch fp32 CPU), "
+                       f"{el:.1f} s"}, out["disp_0"])
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--variant", default="S", choices=sorted(VARIANTS))
+    ap.add_argument("--cv", default="gwc", choices=["gwc", "nc"])
+    ap.add_argument("--batch", type=int, default=1, help="pairs per GPU per step")
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--width", type=int, default=1248)
+    ap.add_argument("--maxdisp", type=int, default=192)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cost-volume roofline side measurement")
+    ap.add_argument("--kernel-table", default="", help="write the per-op probe table (json) here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    backbone, cvs = VARIANTS[args.variant]
+    model = E.ESMStereo(args.maxdisp, args.cv == "gwc", args.cv == "nc", backbone, cvs)
+    seeded_init(model, 1234)
+    model = model.eval().to(dev)
+    left, right = synthetic_pair(args.batch, args.height, args.width, args.maxdisp, 100 + rank, dev)
+    with torch.no_grad():
+        ml, mr, att, up = model.prefix(left, right)
+    B, C, h, w = (int(v) for v in ml.shape)
+    hp = E.HotPath(model, B, h, w, 0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], dev,
+                   graph=not args.no_graph, channels=C)
+    hp.load_inputs(ml, mr, att, up)
+    meta = hp.ctx.meta
+    assert len(meta) == hp.num_ops, (len(meta), hp.num_ops)
+
+    dom, op_ms = find_dominant(hp)
+    if args.kernel_table and rank == 0:
+        with open(args.kernel_table, "w") as f:
+            json.dump([dict(m, median_ms=t) for m, t in zip(meta, op_ms)], f, indent=1)
+    probe_mode = "graph" if hp.graph else "eager"
+    hp.set_probe(dom, args.steps + args.warmup + 8)
+    try:
+        hp.launch()
+    except E.EsmError:  # event nodes not capturable: time the step as a graph, the kernel eagerly
+        hp.set_probe(-1, 1)
+        probe_mode = "eager-sidecar"
+    gbuf = None
+    if world > 1 and not args.no_gather:
+        gbuf = torch.empty((world,) + tuple(hp.outputs[0].shape), device=dev)
+    for _ in range(args.warmup):
+        hp.launch()
+        if gbuf is not None:
+            dist.all_gather_into_tensor(gbuf, hp.outputs[0])
+    torch.cuda.synchronize()
+    if probe_mode != "eager-sidecar":
+        hp.probe_read()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hp.launch()
+        if gbuf is not None:
+            dist.all_gather_into_tensor(gbuf, hp.outputs[0])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if probe_mode == "eager-sidecar":
+        hp.graph = False
+        hp.set_probe(dom, args.steps + 8)
+        for _ in range(args.steps):
+            hp.launch()
+        torch.cuda.synchronize()
+    ktimes = hp.probe_read()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        avg_kms = sum(ktimes) / max(1, len(ktimes))
+        roof = kernel_roofline(meta[dom], avg_kms)
+        workload = f"ESMStereo-{args.variant} {args.cv} {args.height}x{args.width} md{args.maxdisp} B{args.batch}"
+        roof.update({"traffic": pmc_traffic(meta[dom]["name"], workload), "kernel": meta[dom]["name"],
+                     "kernel_shape": meta[dom].get("shape", ""), "avg_us": round(avg_kms * 1e3, 2),
+                     "launches_timed": len(ktimes), "probe": probe_mode,
+                     "algorithmic_per_launch": meta[dom]["flops"] if meta[dom]["kind"] == "conv" else meta[dom]["bytes"]})
+        total = args.batch * world * args.steps
+        line = {
+            "metric": METRIC,
+            "value": round(total / elapsed, 2),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (sinusoid-texture stereo pair, planar disparity; random-init weights)",
+            "config": {"workload": "hot path: cost volume -> 3D stems -> 3D hourglass -> regression -> "
+                                   "ESM upsampler (models/ESMStereo.py:700-745), " + workload,
+                       "variant": args.variant, "cv": args.cv, "global_batch": args.batch * world,
+                       "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
+                       "parallelism": f"dp{world}", "graph": hp.graph or probe_mode == "eager-sidecar",
+                       "launches_per_step": hp.num_ops},
+            "roofline": roof,
+        }
+        if not args.no_extra:
+            line["roofline_cost_volume"] = cost_volume_roofline(dev)
+        if world == 1 and not args.no_cpu_baseline:
+            cb, ref = cpu_baseline(model, ml, mr, att, up, args, args.cpu_seconds)
+            line["cpu_baseline"] = cb
+            got = hp.outputs[0].detach().cpu()
+            line["epe_vs_oracle"] = float((got - ref).abs().mean())
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

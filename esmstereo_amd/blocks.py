@@ -1,0 +1,299 @@
+"""Hot-path modules of ESMStereo, re-expressed for the HIP engine.
+
+Class names, constructor arguments and state-dict keys follow the reference
+(``models/submodule.py:12-103``, ``models/ESMStereo.py:129-509``) so checkpoints load
+unchanged; every forward is a sequence of ``libesmstereo_amd`` launches described once in
+an ``emit(ctx, ...)`` method (used both by the eager nn.Module forward and by the compiled
+whole-hot-path plan).  Fusions relative to the reference op graph:
+
+* ``torch.cat`` (+ the crops of ESMStereo.py:172,177,230) become extra K sources of the
+  next conv; nothing is materialised;
+* BatchNorm (eval) and conv biases fold into a per-channel scale/shift epilogue, GELU /
+  SiLU run in the same epilogue;
+* ``Conv2d(1x1) -> PixelShuffle -> SiLU`` is one conv with a shuffled store;
+* ``F.interpolate(prev, bilinear) + refinement`` is the epilogue of the refinement's last
+  transposed conv, and the final ``* 4`` (ESMStereo.py:737-745) folds into its store.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .engine import ACT_GELU, ACT_NONE, ACT_SILU, Ctx, PackedConv, pack_conv, param_token, run_conv
+from .mixer import FMBlock
+
+__all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
+
+
+class BasicConv(nn.Module):
+    """conv (bias=False) -> BatchNorm -> exact GELU, 2-D or 3-D, normal or transposed
+    (reference models/submodule.py:12-38); one fused HIP launch."""
+
+    def __init__(self, in_channels: int, out_channels: int, deconv: bool = False, is_3d: bool = False,
+                 bn: bool = True, gelu: bool = True, **kwargs) -> None:
+        super().__init__()
+        self.gelu = gelu
+        self.use_bn = bn
+        kinds = {(False, False): nn.Conv2d, (False, True): nn.ConvTranspose2d,
+                 (True, False): nn.Conv3d, (True, True): nn.ConvTranspose3d}
+        self.conv = kinds[(bool(is_3d), bool(deconv))](in_channels, out_channels, bias=False, **kwargs)
+        self.bn = (nn.BatchNorm3d if is_3d else nn.BatchNorm2d)(out_channels)
+        self._esm = None
+
+    def packed(self) -> PackedConv:
+        tok = param_token(self.conv, self.bn) + (self.use_bn, self.gelu)
+        if self._esm is None or self._esm[0] != tok:
+            self._esm = (tok, pack_conv(self.conv, self.bn if self.use_bn else None,
+                                        ACT_GELU if self.gelu else ACT_NONE))
+        return self._esm[1]
+
+    def emit(self, ctx: Ctx, srcs: Sequence[torch.Tensor], **epi) -> torch.Tensor:
+        return run_conv(ctx, self.packed(), srcs, tag=getattr(self, "_esm_name", "BasicConv"), **epi)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.emit(Ctx(x.device), [x])
+
+
+class Conv2x(nn.Module):
+    """Decoder step of the backbone neck (reference models/submodule.py:64-103).  Out of the
+    hot path (FeatUp); kept for checkpoint compatibility, convs run through BasicConv."""
+
+    def __init__(self, in_channels: int, out_channels: int, deconv: bool = False, is_3d: bool = False,
+                 concat: bool = True, keep_concat: bool = True, bn: bool = True, gelu: bool = True,
+                 keep_dispc: bool = False) -> None:
+        super().__init__()
+        self.concat = concat
+        self.is_3d = is_3d
+        if deconv and is_3d and keep_dispc:
+            self.conv1 = BasicConv(in_channels, out_channels, deconv, is_3d, bn=True, gelu=True,
+                                   kernel_size=(1, 4, 4), stride=(1, 2, 2), padding=(0, 1, 1))
+        else:
+            k = (4 if not is_3d else (4, 4, 4)) if deconv else 3
+            self.conv1 = BasicConv(in_channels, out_channels, deconv, is_3d, bn=True, gelu=True, kernel_size=k,
+                                   stride=2, padding=1)
+        mul = (2 if keep_concat else 1) if concat else 1
+        cin2 = out_channels * 2 if concat else out_channels
+        self.conv2 = BasicConv(cin2, out_channels * mul, False, is_3d, bn, gelu, kernel_size=3, stride=1, padding=1)
+
+    def forward(self, x: torch.Tensor, rem: torch.Tensor) -> torch.Tensor:
+        x = self.conv1(x)
+        if x.shape != rem.shape:
+            x = F.interpolate(x, size=(rem.shape[-2], rem.shape[-1]), mode="nearest")
+        if self.concat:
+            return self.conv2.emit(Ctx(x.device), [x, rem]) if x.shape[1] % 4 == 0 and rem.shape[1] % 4 == 0 \
+                else self.conv2(torch.cat((x, rem), 1))
+        return self.conv2(x + rem)
+
+
+def _bc(cin: int, cout: int, is_3d: bool, k: int = 3, s: int = 1, p: int = 1, **kw) -> BasicConv:
+    return BasicConv(cin, cout, is_3d=is_3d, kernel_size=k, stride=s, padding=p, **kw)
+
+
+def _up(cin: int, cout: int, is_3d: bool, last: bool = False) -> BasicConv:
+    return BasicConv(cin, cout, deconv=True, is_3d=is_3d, bn=not last, gelu=not last, kernel_size=4, padding=1,
+                     stride=2)
+
+
+def _crop_like(t: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """``t[..., :ref.D, :ref.H, :ref.W]`` (ESMStereo.py:172,177,230) as a strided view."""
+    idx = (slice(None), slice(None)) + tuple(slice(0, n) for n in ref.shape[2:])
+    return t[idx]
+
+
+class _Hourglass(nn.Module):
+    """Shared 3-level encoder/decoder of ``aggregation`` (3-D) and ``up_refinement`` (2-D)."""
+
+    is_3d = False
+
+    def _build(self, c_in: int, c1: int, c2: int, c3: int, cat0: int, cat1: int) -> None:
+        d3 = self.is_3d
+        self.conv1 = nn.Sequential(_bc(c_in, c1, d3, s=2), _bc(c1, c1, d3))
+        self.conv2 = nn.Sequential(_bc(c1, c2, d3, s=2), _bc(c2, c2, d3))
+        self.conv3 = nn.Sequential(_bc(c2, c3, d3, s=2), _bc(c3, c3, d3))
+        self.conv3_up = _up(c3, c2, d3)
+        self.conv2_up = _up(c2, c1, d3)
+        self.conv1_up = _up(c1, 1, d3, last=True)
+        self.agg_0 = nn.Sequential(_bc(cat0, c2, d3, k=1, p=0), _bc(c2, c2, d3))
+        self.agg_1 = nn.Sequential(_bc(cat1, c1, d3, k=1, p=0), _bc(c1, c1, d3))
+
+    def _emit(self, ctx: Ctx, x: torch.Tensor, extra0: Sequence[torch.Tensor] = (),
+              extra1: Sequence[torch.Tensor] = (), crop1: bool = True, **last) -> torch.Tensor:
+        c1 = self.conv1[1].emit(ctx, [self.conv1[0].emit(ctx, [x])])
+        c2 = self.conv2[1].emit(ctx, [self.conv2[0].emit(ctx, [c1])])
+        c3 = self.conv3[1].emit(ctx, [self.conv3[0].emit(ctx, [c2])])
+        u3 = self.conv3_up.emit(ctx, [c3])
+        a0 = self.agg_0[0].emit(ctx, [_crop_like(u3, c2), c2, *extra0])
+        a0 = self.agg_0[1].emit(ctx, [a0])
+        u2 = self.conv2_up.emit(ctx, [a0])
+        if crop1:
+            u2 = _crop_like(u2, c1)
+        elif u2.shape[2:] != c1.shape[2:]:
+            # the reference concat at ESMStereo.py:234 does not crop and raises here
+            raise RuntimeError(f"Sizes of tensors must match except in dimension 1. Expected size "
+                               f"{u2.shape[2]} but got size {c1.shape[2]} for tensor number 1 in the list.")
+        a1 = self.agg_1[0].emit(ctx, [u2, c1, *extra1])
+        a1 = self.agg_1[1].emit(ctx, [a1])
+        return self.conv1_up.emit(ctx, [a1], **last)
+
+
+class aggregation(_Hourglass):
+    """3-D cost aggregation hourglass (reference models/ESMStereo.py:129-182).
+
+    Channel ladder c, c+a, c+2a, c+4a (L: 8 -> 24 -> 40 -> 72).  Output depth is 2*ceil(D/2).
+    """
+
+    is_3d = True
+
+    def __init__(self, in_channels: int, add_channel: int) -> None:
+        super().__init__()
+        c0, a = in_channels, add_channel
+        self._build(c0, c0 + a, c0 + 2 * a, c0 + 4 * a, 2 * (c0 + 2 * a), 2 * (c0 + a))
+
+    def emit(self, ctx: Ctx, x: torch.Tensor, **last) -> torch.Tensor:
+        return self._emit(ctx, x, crop1=True, **last)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.emit(Ctx(x.device), x)
+
+
+class up_refinement(_Hourglass):
+    """2-D disparity refinement hourglass (reference models/ESMStereo.py:185-239)."""
+
+    is_3d = False
+
+    def __init__(self, C: int, cf1: int, cf2: int) -> None:
+        super().__init__()
+        self._build(1, C, C, C, 2 * C + cf1, 2 * C + cf2)
+
+    def emit(self, ctx: Ctx, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor,
+             **last) -> torch.Tensor:
+        return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, **last)
+
+    def forward(self, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor) -> torch.Tensor:
+        return self.emit(Ctx(disp.device), disp, left_f1x, left_f2x)
+
+
+# ----------------------------------------------------------------------------- ESM upsampler
+
+
+def _dm(c: int) -> nn.Sequential:
+    """Disparity-feature stack: k5 p1, k3 p1, k3 p1, k1 p1 (reference ESMStereo.py:250-253)."""
+    return nn.Sequential(_bc(1, c, False, k=5), _bc(c, c, False), _bc(c, c, False), _bc(c, c, False, k=1, p=1))
+
+
+def _spx(cin: int, c: int, cout: int) -> nn.Sequential:
+    return nn.Sequential(_bc(cin, c, False), nn.Conv2d(c, cout, 3, 1, 1, bias=False), nn.BatchNorm2d(cout), nn.GELU())
+
+
+def _shuffle_up(nf: int, r: int) -> nn.Sequential:
+    return nn.Sequential(nn.Conv2d(nf, nf * r * r, 1, 1, 0), nn.PixelShuffle(r), nn.SiLU(inplace=True))
+
+
+class _ESMUpsampler(nn.Module):
+    """Generic ESM cascade: each stage refines the previous disparity by a factor r.
+
+    ``STAGES`` rows: (tag, C, cat_channels, spx_out, r, cf1, cf2, cat_src, ref_src_a, ref_src_b) where
+    the *_src entries index the forward()'s feature arguments.
+    """
+
+    STAGES: Tuple = ()
+    N_FEATS = 8
+
+    def __init__(self) -> None:
+        super().__init__()
+        nf = self.N_FEATS
+        for i, (tag, C, catc, spx_out, r, cf1, cf2, *_src) in enumerate(self.STAGES):
+            setattr(self, f"dm{tag}", _dm(C))
+            setattr(self, f"spx_{tag}", _spx(C + catc, C, spx_out))
+            if i == 0:
+                self.to_feat = nn.Conv2d(C, nf, 3, 1, 1, bias=False)
+                self.blocks = nn.Sequential(*[FMBlock(nf, 7, 2) for _ in range(2)])
+            setattr(self, f"upsampling{tag[:-1]}", _shuffle_up(nf, r))
+            setattr(self, f"tail{tag}", nn.Conv2d(nf, 1, 3, 1, 1))
+            setattr(self, f"ref{tag}", up_refinement(C, cf1, cf2))
+        self._esm = None
+
+    def _packed(self):
+        tok = param_token(*self.modules())
+        if self._esm is None or self._esm[0] != tok:
+            p = {"to_feat": pack_conv(self.to_feat)}
+            for (tag, *_r) in self.STAGES:
+                spx = getattr(self, f"spx_{tag}")
+                p[f"spx1_{tag}"] = pack_conv(spx[1], spx[2], ACT_GELU)
+                p[f"up_{tag}"] = pack_conv(getattr(self, f"upsampling{tag[:-1]}")[0], act=ACT_SILU)
+                p[f"tail_{tag}"] = pack_conv(getattr(self, f"tail{tag}"))
+            self._esm = (tok, p)
+        return self._esm[1]
+
+    def emit(self, ctx: Ctx, feats: Sequence[torch.Tensor], init_disp: torch.Tensor, final_scale: float = 1.0,
+             scaled_copies: Optional[float] = None) -> List[torch.Tensor]:
+        """Returns [finest, ..., coarsest] like the reference forward.  ``final_scale`` scales the
+        finest output in its store; with ``scaled_copies`` every coarser output also gets a
+        scaled second copy (returned second): ([outputs], [scaled copies])."""
+        p = self._packed()
+        me = getattr(self, "_esm_name", "upsample")
+        prev = init_disp
+        outs, copies = [], []
+        n = len(self.STAGES)
+        for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
+            dm = getattr(self, f"dm{tag}")
+            d = prev
+            for layer in dm:
+                d = layer.emit(ctx, [d])
+            spx = getattr(self, f"spx_{tag}")
+            c = spx[0].emit(ctx, [d, feats[cat_i]])
+            c = run_conv(ctx, p[f"spx1_{tag}"], [c], tag=f"{me}.spx_{tag}.1")
+            x = c
+            if i == 0:
+                x = run_conv(ctx, p["to_feat"], [x], tag=f"{me}.to_feat")
+                for blk in self.blocks:
+                    x = blk.emit(ctx, x)
+            x = run_conv(ctx, p[f"up_{tag}"], [x], shuffle=r, tag=f"{me}.upsampling{tag[:-1]}.0")
+            x = run_conv(ctx, p[f"tail_{tag}"], [x], tag=f"{me}.tail{tag}")
+            last = i == n - 1
+            epi = dict(up=prev, up_f=r, post_scale=final_scale if last else 1.0)
+            if scaled_copies is not None and not last:
+                B, _, H, W = x.shape
+                cp = ctx.empty(B, 1, H, W)
+                epi.update(out2=cp, post_scale2=scaled_copies)
+                copies.append(cp)
+            prev = getattr(self, f"ref{tag}").emit(ctx, x, feats[ra], feats[rb], **epi)
+            outs.append(prev)
+        outs.reverse()
+        copies.reverse()
+        return (outs, copies) if scaled_copies is not None else outs
+
+    def forward(self, *args: torch.Tensor) -> Tuple[torch.Tensor, ...]:
+        *feats, init = args
+        return tuple(self.emit(Ctx(init.device), feats, init))
+
+
+class upsample4(_ESMUpsampler):
+    """ESMStereo-L upsampler, two x2 stages (reference models/ESMStereo.py:242-318).
+    forward(left_f1x, left_f2x, left_f4x, init_disp) -> (x4 disparity, x2 disparity)."""
+
+    N_FEATS = 16
+    STAGES = (("2x", 32, 48, 32, 2, 96, 48, 1, 0, 1),
+              ("4x", 32, 32, 16, 2, 48, 32, 2, 1, 2))
+
+
+class upsample8(_ESMUpsampler):
+    """ESMStereo-M upsampler, three x2 stages (reference models/ESMStereo.py:320-428).
+    forward(left_f2x, left_f4x, left_f8x, stem_f2, init_disp) -> (x8, x4, x2)."""
+
+    N_FEATS = 8
+    STAGES = (("2x", 16, 96, 16, 2, 240, 96, 1, 0, 1),
+              ("4x", 16, 24, 8, 2, 96, 24, 2, 1, 2),
+              ("8x", 16, 32, 8, 2, 24, 32, 3, 2, 3))
+
+
+class upsample16(_ESMUpsampler):
+    """ESMStereo-S upsampler, two x4 stages (reference models/ESMStereo.py:430-509).
+    forward(left_f1x, left_f2x, left_f4x, left_f8x, init_disp) -> (x16, x4)."""
+
+    N_FEATS = 8
+    STAGES = (("2x", 16, 32, 16, 4, 32, 32, 1, 1, 0),
+              ("4x", 16, 24, 8, 4, 24, 24, 2, 2, 3))

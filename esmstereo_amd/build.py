@@ -1,0 +1,83 @@
+"""Build the gfx950 shared library ``esmstereo_amd/libesmstereo_amd.so`` in-tree.
+
+``python -m esmstereo_amd.build`` (or ``__graft_entry__.build()``) compiles every
+``csrc/*.hip`` with ``hipcc --offload-arch=gfx950`` into objects (in parallel, skipping
+up-to-date ones) and links one C-ABI shared library.  No torch headers are involved: the
+library's interface is ``include/esmstereo_amd.h``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "libesmstereo_amd.so")
+HEADER = os.path.join(ROOT, "include", "esmstereo_amd.h")
+ARCH = os.environ.get("ESM_OFFLOAD_ARCH", "gfx950")
+CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+
+
+def _hipcc() -> str:
+    h = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(h):
+        raise RuntimeError("hipcc not found: the esmstereo_amd HIP library cannot be built")
+    return h
+
+
+def _deps():
+    return [os.path.join(CSRC, "common.h"), HEADER]
+
+
+def _stale(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(p) > t for p in [src] + _deps())
+
+
+def _compile(src: str, obj: str) -> str:
+    cmd = [_hipcc()] + CXXFLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+    objs = []
+    todo = []
+    for f in srcs:
+        src = os.path.join(CSRC, f)
+        obj = os.path.join(BUILD, f[:-4] + ".o")
+        objs.append(obj)
+        if _stale(obj, src):
+            todo.append((src, obj))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            for fut in [ex.submit(_compile, s, o) for s, o in todo]:
+                o = fut.result()
+                if verbose:
+                    print("compiled", os.path.relpath(o, ROOT))
+    if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        tmp = LIB + ".tmp"
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print("linked", os.path.relpath(LIB, ROOT))
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

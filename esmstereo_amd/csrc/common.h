@@ -1,0 +1,70 @@
+// Shared helpers for the gfx950 kernels of esmstereo_amd.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/esmstereo_amd.h"
+
+namespace esm {
+
+void set_error(const std::string& msg);
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        return ESM_ERR_LAUNCH;
+    }
+    return ESM_OK;
+}
+
+inline int arg_error(const std::string& msg) {
+    set_error(msg);
+    return ESM_ERR_ARG;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned>((a + b - 1) / b); }
+
+// exact-erf GELU as nn.GELU() (models/submodule.py:37): x * 0.5 * (1 + erf(x / sqrt 2))
+__device__ __forceinline__ float gelu_erf(float x) {
+    return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+// SiLU as nn.SiLU: x / (1 + exp(-x))
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+    switch (act) {
+        case ESM_ACT_GELU: return gelu_erf(v);
+        case ESM_ACT_SILU: return silu(v);
+        case ESM_ACT_RELU: return v > 0.f ? v : 0.f;
+        default: return v;
+    }
+}
+
+// F.interpolate(mode='bilinear', align_corners=False, scale_factor=f) at output (y, x):
+// src = (dst + 0.5) / f - 0.5 clamped at 0; neighbour index clamped at the last row/col.
+__device__ __forceinline__ float bilinear_at(const float* __restrict__ img, int H, int W, long long sh, int f, int y,
+                                             int x) {
+    const float sc = 1.0f / static_cast<float>(f);
+    float sy = sc * (static_cast<float>(y) + 0.5f) - 0.5f;
+    float sx = sc * (static_cast<float>(x) + 0.5f) - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    sx = sx < 0.f ? 0.f : sx;
+    const int y0 = static_cast<int>(sy);
+    const int x0 = static_cast<int>(sx);
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    const int x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly1 = sy - static_cast<float>(y0), ly0 = 1.0f - ly1;
+    const float lx1 = sx - static_cast<float>(x0), lx0 = 1.0f - lx1;
+    const float a = img[y0 * sh + x0], b = img[y0 * sh + x1];
+    const float c = img[y1 * sh + x0], d = img[y1 * sh + x1];
+    return ly0 * (lx0 * a + lx1 * b) + ly1 * (lx0 * c + lx1 * d);
+}
+
+}  // namespace esm

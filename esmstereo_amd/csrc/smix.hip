@@ -1,0 +1,155 @@
+// ShuffleMixer per-pixel chain (models/shufflemixer.py):
+//   [optional] depthwise KxK `spatial` conv with bias            (SMLayer :103, :110)
+//   per stage: t = shuffle(cat(fc2(silu(fc0(LN(t)[:C/2]))), LN(t)[C/2:])) + t
+//              LN = BiasFree_LayerNorm over C (mean IS subtracted) :47-62
+//              SplitPointMlp :23-37, channel shuffle 'b (g d) -> b (d g)', g = 8
+//   [optional] + res                                              (FMBlock `net(x) + x` :130)
+// One thread owns one pixel and keeps its C (8 or 16) channels in registers; the tiny
+// weights are wave-uniform (scalar loads).  With the depthwise conv, a 16x16 pixel tile and
+// its (K-1)/2 halo are staged in LDS once per channel group.
+#include "common.h"
+
+namespace esm {
+namespace {
+
+constexpr int kTileH = 16;
+constexpr int kTileW = 16;
+constexpr int kThreads = kTileH * kTileW;
+
+template <int C>
+__device__ __forceinline__ void mix_stage(float (&t)[C], const esm_smix_stage& st) {
+    constexpr int H2 = C / 2;
+    constexpr int DD = C / 8;
+    float mu = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) mu += t[c];
+    mu = mu / static_cast<float>(C);
+    float var = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const float dv = t[c] - mu;
+        var += dv * dv;
+    }
+    var = var / static_cast<float>(C);
+    const float den = sqrtf(var + 1e-5f);
+    float n[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) / den * st.ln_w[c];
+    float h[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        float s = st.fc0_b[j];
+#pragma unroll
+        for (int i = 0; i < H2; ++i) s += st.fc0_w[j * H2 + i] * n[i];
+        h[j] = silu(s);
+    }
+    float cat[C];
+#pragma unroll
+    for (int i = 0; i < H2; ++i) {
+        float s = st.fc2_b[i];
+#pragma unroll
+        for (int j = 0; j < C; ++j) s += st.fc2_w[i * C + j] * h[j];
+        cat[i] = s;
+    }
+#pragma unroll
+    for (int i = H2; i < C; ++i) cat[i] = n[i];
+    // out[d*8 + g] = cat[g*DD + d]
+    float o[C];
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int d = 0; d < DD; ++d) o[d * 8 + g] = cat[g * DD + d] + t[d * 8 + g];
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[c] = o[c];
+}
+
+template <int C, int K>
+__global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
+    constexpr int R = K / 2;
+    constexpr int LH = kTileH + 2 * R;
+    constexpr int LW = kTileW + 2 * R;
+    __shared__ float tile[(K > 1) ? C : 1][(K > 1) ? LH : 1][(K > 1) ? LW + 1 : 1];
+    const int H = a.H, W = a.W;
+    const int b = blockIdx.z;
+    const int y0 = blockIdx.y * kTileH, x0 = blockIdx.x * kTileW;
+    const int ty = threadIdx.x / kTileW, tx = threadIdx.x - (threadIdx.x / kTileW) * kTileW;
+    const int y = y0 + ty, x = x0 + tx;
+    const long long plane = static_cast<long long>(H) * W;
+    const float* xb = a.x + static_cast<long long>(b) * C * plane;
+    float t[C];
+    if (K > 1) {
+        for (int i = threadIdx.x; i < C * LH * LW; i += kThreads) {
+            const int c = i / (LH * LW);
+            const int rem = i - c * LH * LW;
+            const int ly = rem / LW, lx = rem - (rem / LW) * LW;
+            const int gy = y0 + ly - R, gx = x0 + lx - R;
+            tile[c][ly][lx] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? xb[c * plane + gy * W + gx] : 0.f;
+        }
+        __syncthreads();
+        if (y >= H || x >= W) return;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            float s = 0.f;
+            const float* wc = a.dw_w + c * K * K;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) s += wc[ky * K + kx] * tile[c][ty + ky][tx + kx];
+            t[c] = s + a.dw_b[c];
+        }
+    } else {
+        if (y >= H || x >= W) return;
+#pragma unroll
+        for (int c = 0; c < C; ++c) t[c] = xb[c * plane + y * W + x];
+    }
+    for (int s = 0; s < a.nstages; ++s) mix_stage<C>(t, a.stage[s]);
+    const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
+    if (a.res) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) t[c] += a.res[pix + c * plane];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) a.out[pix + c * plane] = t[c];
+}
+
+template <int C>
+int launch_c(const esm_smix_desc& a, hipStream_t s) {
+    dim3 grid(ceil_div(a.W, kTileW), ceil_div(a.H, kTileH), a.B);
+    if (!a.dw_w) {
+        hipLaunchKernelGGL((smix_kernel<C, 1>), grid, dim3(kThreads), 0, s, a);
+    } else if (a.dw_k == 7) {
+        hipLaunchKernelGGL((smix_kernel<C, 7>), grid, dim3(kThreads), 0, s, a);
+    } else if (a.dw_k == 3) {
+        hipLaunchKernelGGL((smix_kernel<C, 3>), grid, dim3(kThreads), 0, s, a);
+    } else {
+        set_error("smix: depthwise kernel must be 3 or 7");
+        return ESM_ERR_UNSUPPORTED;
+    }
+    return check_launch("smix");
+}
+
+}  // namespace
+
+int launch_smix(const esm_smix_desc* d, hipStream_t s) {
+    if (!d) return arg_error("smix: null descriptor");
+    const esm_smix_desc& a = *d;
+    if (!a.x || !a.out) return arg_error("smix: null pointer");
+    if (a.B <= 0 || a.H <= 0 || a.W <= 0) return arg_error("smix: bad size");
+    if (a.nstages < 0 || a.nstages > ESM_SMIX_MAX_STAGES) return arg_error("smix: nstages must be 0..2");
+    if (a.dw_w && !a.dw_b) return arg_error("smix: depthwise conv needs a bias");
+    if (a.x == a.out && a.dw_w) return arg_error("smix: depthwise conv cannot run in place");
+    for (int i = 0; i < a.nstages; ++i) {
+        const esm_smix_stage& st = a.stage[i];
+        if (!st.ln_w || !st.fc0_w || !st.fc0_b || !st.fc2_w || !st.fc2_b) return arg_error("smix: null stage weights");
+    }
+    if (a.C == 8) return launch_c<8>(a, s);
+    if (a.C == 16) return launch_c<16>(a, s);
+    set_error("smix: C must be 8 or 16");
+    return ESM_ERR_UNSUPPORTED;
+}
+
+}  // namespace esm
+
+extern "C" int esm_smix_f32(const esm_smix_desc* desc, void* stream) {
+    return esm::launch_smix(desc, esm::as_stream(stream));
+}

@@ -1,0 +1,405 @@
+"""Host side of the HIP hot path: weight packing, launch descriptors, eager/plan contexts.
+
+Every op here goes to ``libesmstereo_amd.so`` through ``_lib`` (ctypes over the C ABI of
+``include/esmstereo_amd.h``).  Nothing computes on the CPU and there is no PyTorch
+fallback: CPU tensors, non-fp32 tensors or a missing library raise.
+
+A :class:`Ctx` either launches each op immediately on the current torch stream (``eager``)
+or appends it to a native ``esm_plan`` (``plan``) whose launch list is later replayed —
+eagerly or as one hipGraph.  The module classes (blocks.py, mixer.py, model.py) describe the
+reference's forward passes once, against a Ctx, so the eager nn.Module forward and the
+compiled whole-hot-path plan run the very same kernels with the very same fusions.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, ACT_SILU, EsmConvDesc, EsmSmixDesc, check, lib
+
+__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
+
+
+def _rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{what}: esmstereo_amd runs on ROCm devices only (got a {t.device.type} tensor); "
+                           "there is no CPU path")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32, got {t.dtype}")
+    if t.dim() > 0 and t.stride(-1) != 1:
+        raise ValueError(f"{what}: innermost dimension must be contiguous")
+
+
+# ----------------------------------------------------------------------------- packing
+
+
+@dataclass
+class PackedConv:
+    """A conv layer ready for ``esm_conv_f32``: packed weights + folded BN/bias epilogue."""
+
+    w: torch.Tensor
+    scale: Optional[torch.Tensor]
+    shift: Optional[torch.Tensor]
+    act: int
+    nd: int
+    k: int
+    stride: int
+    pad: int
+    transposed: bool
+    cin: int
+    cout: int
+    cin_pad: int
+    cout_pad: int
+
+
+def _bits(v: int, n: int) -> Tuple[int, ...]:
+    return tuple((v >> (n - 1 - i)) & 1 for i in range(n))
+
+
+def pack_weight(W: torch.Tensor, transposed: bool) -> Tuple[torch.Tensor, int, int]:
+    """Pack a Conv/ConvTranspose weight for the implicit-GEMM kernel.
+
+    normal      W[cout][cin][k..]  -> P[tap][cin_pad][cout_pad]
+    transposed  W[cin][cout][4..]  -> P[cls][tap][cin_pad][cout_pad]; for output parity q and
+                tap t of a dim the kernel index is 1 - q + 2t (input index m + q - t).
+    """
+    W = W.detach().to(torch.float32)
+    nd = W.dim() - 2
+    if not transposed:
+        cout, cin = W.shape[:2]
+        taps = int(W[0, 0].numel())
+        cin_pad, cout_pad = _rup(cin, 4), _rup(cout, 32)
+        P = W.new_zeros(taps, cin_pad, cout_pad)
+        P[:, :cin, :cout] = W.reshape(cout, cin, taps).permute(2, 1, 0)
+        return P.contiguous(), cin_pad, cout_pad
+    cin, cout = W.shape[:2]
+    if any(s != 4 for s in W.shape[2:]):
+        raise ValueError("transposed conv: only kernel 4 is supported")
+    cin_pad, cout_pad = _rup(cin, 4), _rup(cout, 32)
+    n = 2 ** nd
+    P = W.new_zeros(n, n, cin_pad, cout_pad)
+    for cls in range(n):
+        q = _bits(cls, nd)
+        for tap in range(n):
+            t = _bits(tap, nd)
+            k = tuple(1 - qi + 2 * ti for qi, ti in zip(q, t))
+            P[cls, tap, :cin, :cout] = W[(slice(None), slice(None)) + k]
+    return P.contiguous(), cin_pad, cout_pad
+
+
+def bn_affine(bn: torch.nn.Module) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Eval BatchNorm as y = x*alpha + beta with alpha = w/sqrt(var+eps), beta = b - mean*alpha."""
+    invstd = 1.0 / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+    alpha = invstd * bn.weight.detach().float()
+    beta = bn.bias.detach().float() - bn.running_mean.detach().float() * alpha
+    return alpha.contiguous(), beta.contiguous()
+
+
+def pack_conv(conv: torch.nn.Module, bn: Optional[torch.nn.Module] = None, act: int = ACT_NONE) -> PackedConv:
+    transposed = isinstance(conv, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d))
+    W = conv.weight
+    nd = W.dim() - 2
+    ks = set(conv.kernel_size)
+    ss = set(conv.stride)
+    ps = set(conv.padding) if not isinstance(conv.padding, str) else {-1}
+    if len(ks) != 1 or len(ss) != 1 or len(ps) != 1 or set(conv.dilation) != {1} or conv.groups != 1:
+        raise ValueError(f"unsupported conv geometry {conv}")
+    P, cin_pad, cout_pad = pack_weight(W, transposed)
+    scale = shift = None
+    if bn is not None:
+        scale, shift = bn_affine(bn)
+        if conv.bias is not None:  # conv bias feeds BN: (x + cb)*a + b = x*a + (cb*a + b)
+            shift = (conv.bias.detach().float() * scale + shift).contiguous()
+    elif conv.bias is not None:
+        shift = conv.bias.detach().float().contiguous()
+    cin, cout = (W.shape[0], W.shape[1]) if transposed else (W.shape[1], W.shape[0])
+    return PackedConv(P, scale, shift, act, nd, ks.pop(), ss.pop(), ps.pop(), transposed, int(cin), int(cout),
+                      cin_pad, cout_pad)
+
+
+def param_token(*mods: torch.nn.Module) -> Tuple:
+    """Cheap identity of a module's own tensors (storage + in-place version)."""
+    tok = []
+    for m in mods:
+        if m is None:
+            continue
+        for t in list(m.parameters(recurse=False)) + list(m.buffers(recurse=False)):
+            tok.append((t.data_ptr(), t._version, t.device.index))
+    return tuple(tok)
+
+
+# ----------------------------------------------------------------------------- context
+
+
+class Ctx:
+    """Where ops go: launched now (``plan=False``) or appended to a native plan."""
+
+    def __init__(self, device: torch.device, plan: bool = False):
+        self.device = torch.device(device)
+        self.plan = lib.esm_plan_create() if plan else None
+        if plan and not self.plan:
+            raise RuntimeError("esm_plan_create failed")
+        self.keep: List[object] = []  # tensors (and ctypes descs) that must outlive the plan
+        # one entry per launch-list op: name, kernel family, algorithmic flops / HBM bytes
+        self.meta: List[dict] = []
+        self.stream = None if plan else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self) -> None:
+        if self.plan:
+            lib.esm_plan_destroy(self.plan)
+            self.plan = None
+        self.keep.clear()
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def empty(self, *shape: int) -> torch.Tensor:
+        t = torch.empty(shape, device=self.device, dtype=torch.float32)
+        if self.plan:
+            self.keep.append(t)
+        return t
+
+    def hold(self, *objs) -> None:
+        if self.plan:
+            self.keep.extend(o for o in objs if o is not None)
+
+    # --- op submission
+    def conv(self, d: EsmConvDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_conv(self.plan, ctypes.byref(d)), "plan_add_conv")
+        else:
+            check(lib.esm_conv_f32(ctypes.byref(d), self.stream), "conv")
+
+    def smix(self, d: EsmSmixDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_smix(self.plan, ctypes.byref(d)), "plan_add_smix")
+        else:
+            check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
+
+    def gwc(self, L, R, att, V, B, C, H, W, D, G) -> None:
+        self.meta.append(dict(name="gwc_volume", kind="gwc", flops=2 * B * C * D * H * W,
+                              bytes=4 * B * (2 * C * H * W + G * D * H * W + (G * H * W if att is not None else 0))))
+        a = att.data_ptr() if att is not None else None
+        if self.plan:
+            self.hold(L, R, att, V)
+            check(lib.esm_plan_add_gwc(self.plan, L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G), "gwc")
+        else:
+            check(lib.esm_gwc_volume_f32(L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G, self.stream),
+                  "gwc")
+
+    def concat(self, L, R, V, B, C, H, W, D) -> None:
+        self.meta.append(dict(name="concat_volume", kind="concat", flops=0,
+                              bytes=4 * B * (2 * C * H * W + 2 * C * D * H * W)))
+        if self.plan:
+            self.hold(L, R, V)
+            check(lib.esm_plan_add_concat(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D), "concat")
+        else:
+            check(lib.esm_concat_volume_f32(L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D, self.stream),
+                  "concat")
+
+    def normcorr(self, L, R, V, work, B, C, H, W, D) -> None:
+        self.meta.append(dict(name="normcorr_volume", kind="normcorr", flops=2 * B * C * D * H * W,
+                              bytes=4 * B * (2 * C * H * W + D * H * W)))
+        if self.plan:
+            self.hold(L, R, V, work)
+            check(lib.esm_plan_add_normcorr(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C,
+                                            H, W, D), "normcorr")
+        else:
+            check(lib.esm_normcorr_volume_f32(L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C, H, W, D,
+                                              self.stream), "normcorr")
+
+    def regression(self, kind, cost, out, B, D, H, W, samples=None) -> None:
+        self.meta.append(dict(name="regression_topk2" if kind else "disparity_regression", kind="regression",
+                              flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W))
+        if self.plan:
+            if samples is not None:
+                raise ValueError("plan regression: disparity samples are arange(D)")
+            self.hold(cost, out)
+            check(lib.esm_plan_add_regression(self.plan, kind, cost.data_ptr(), out.data_ptr(), B, D, H, W),
+                  "regression")
+        elif kind == 0:
+            check(lib.esm_disp_regression_f32(cost.data_ptr(), out.data_ptr(), B, D, H, W, self.stream), "regression")
+        else:
+            s = samples.data_ptr() if samples is not None else None
+            check(lib.esm_topk2_regression_f32(cost.data_ptr(), s, out.data_ptr(), B, D, H, W, self.stream),
+                  "regression_topk")
+
+
+# ----------------------------------------------------------------------------- ops
+
+
+def _spatial(t: torch.Tensor, nd: int) -> Tuple[int, int, int]:
+    if nd == 3:
+        return int(t.shape[2]), int(t.shape[3]), int(t.shape[4])
+    return 1, int(t.shape[2]), int(t.shape[3])
+
+
+def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, *,
+             mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
+             up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
+             out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv") -> torch.Tensor:
+    """One implicit-GEMM conv launch; ``srcs`` are concatenated along channels (each may be a
+    cropped view), the epilogue applies BN/bias, activation, ``*mul``, ``+res``,
+    ``+bilinear(up)``, ``*post_scale`` and an optional PixelShuffle(``shuffle``)."""
+    nd = pc.nd
+    if not srcs or len(srcs) > _lib.MAX_SRC:
+        raise ValueError("conv: 1..3 sources")
+    x0 = srcs[0]
+    if x0.dim() != nd + 2:
+        raise ValueError(f"conv: expected a {nd + 2}-D input, got shape {tuple(x0.shape)}")
+    B = int(x0.shape[0])
+    Di, Hi, Wi = _spatial(x0, nd)
+    d = EsmConvDesc()
+    cin = 0
+    for i, s in enumerate(srcs):
+        require_device(s, "conv input")
+        if s.dim() != nd + 2 or int(s.shape[0]) != B or _spatial(s, nd) != (Di, Hi, Wi):
+            # torch.cat of mismatching tensors raises RuntimeError in the reference
+            raise RuntimeError(f"Sizes of tensors must match except in dimension 1 (conv sources "
+                               f"{[tuple(t.shape) for t in srcs]})")
+        st = s.stride()
+        d.src[i].ptr = s.data_ptr()
+        d.src[i].C = int(s.shape[1])
+        d.src[i].sb, d.src[i].sc = st[0], st[1]
+        d.src[i].sd = st[2] if nd == 3 else 0
+        d.src[i].sh = st[-2]
+        cin += int(s.shape[1])
+    if cin != pc.cin:
+        raise RuntimeError(f"conv: input has {cin} channels, layer expects {pc.cin}")
+    d.nsrc = len(srcs)
+    d.B, d.Cin = B, cin
+    d.Di, d.Hi, d.Wi = Di, Hi, Wi
+    k, s, p = pc.k, pc.stride, pc.pad
+    if pc.transposed:
+        if (k, s, p) != (4, 2, 1):
+            raise ValueError("transposed conv: only k=4 s=2 p=1")
+        Do, Ho, Wo = (2 * Di if nd == 3 else 1), 2 * Hi, 2 * Wi
+    else:
+        Ho, Wo = (Hi + 2 * p - k) // s + 1, (Wi + 2 * p - k) // s + 1
+        Do = (Di + 2 * p - k) // s + 1 if nd == 3 else 1
+    if min(Do, Ho, Wo) <= 0:
+        raise RuntimeError(f"conv: empty output for input {tuple(x0.shape)}")
+    d.Do, d.Ho, d.Wo = Do, Ho, Wo
+    d.kd = k if nd == 3 else 1
+    d.kh = d.kw = k
+    d.stride, d.transposed = s, int(pc.transposed)
+    d.pd = p if nd == 3 else 0
+    d.ph = d.pw = p
+    d.Cout, d.cin_pad, d.cout_pad = pc.cout, pc.cin_pad, pc.cout_pad
+    d.w = pc.w.data_ptr()
+    d.scale = pc.scale.data_ptr() if pc.scale is not None else None
+    d.shift = pc.shift.data_ptr() if pc.shift is not None else None
+    d.act = pc.act
+    r = int(shuffle)
+    d.shuffle = r
+    if out is None:
+        if r > 1:
+            if pc.cout % (r * r):
+                raise ValueError("pixel shuffle: Cout not divisible by r^2")
+            out = ctx.empty(B, pc.cout // (r * r), Ho * r, Wo * r)
+        else:
+            out = ctx.empty(B, pc.cout, Do, Ho, Wo) if nd == 3 else ctx.empty(B, pc.cout, Ho, Wo)
+    require_device(out, "conv output")
+    ost = out.stride()
+    d.out = out.data_ptr()
+    d.ob, d.oc = ost[0], ost[1]
+    d.od = ost[2] if nd == 3 else 0
+    d.oh = ost[-2]
+    if mul is not None:
+        require_device(mul, "conv mul")
+        d.mul = mul.data_ptr()
+        d.mb, d.mc, d.mh = mul.stride(0), mul.stride(1), mul.stride(-2)
+    if res is not None:
+        require_device(res, "conv residual")
+        if tuple(res.shape) != tuple(out.shape):
+            raise ValueError("conv: residual shape must match the output")
+        rs = res.stride()
+        d.res = res.data_ptr()
+        d.rb, d.rc = rs[0], rs[1]
+        d.rd = rs[2] if nd == 3 else 0
+        d.rh = rs[-2]
+    if up is not None:
+        require_device(up, "conv bilinear source")
+        d.up = up.data_ptr()
+        d.up_h, d.up_w, d.up_f = int(up.shape[-2]), int(up.shape[-1]), int(up_f)
+        d.ub, d.uh = up.stride(0), up.stride(-2)
+        if d.up_h * up_f != Ho or d.up_w * up_f != Wo:
+            raise ValueError("conv: bilinear source extent x factor must equal the output extent")
+    d.post_scale = float(post_scale)
+    if out2 is not None:
+        require_device(out2, "conv out2")
+        if out2.stride() != out.stride() or out2.shape != out.shape:
+            raise ValueError("conv: out2 must have the output's shape and strides")
+        d.out2 = out2.data_ptr()
+        d.post_scale2 = float(post_scale2)
+    ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
+    taps = pc.k ** nd
+    if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap
+        macs = B * Di * Hi * Wi * pc.cin * pc.cout * taps
+    else:
+        macs = B * Do * Ho * Wo * pc.cin * pc.cout * taps
+    in_bytes = 4 * B * cin * Di * Hi * Wi
+    out_bytes = 4 * B * pc.cout * Do * Ho * Wo * (2 if out2 is not None else 1)
+    extra = 4 * (res.numel() if res is not None else 0) + 4 * (mul.numel() if mul is not None else 0)
+    ctx.meta.append(dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
+                         shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
+                               f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}"))
+    ctx.conv(d)
+    return out
+
+
+@dataclass
+class SmixStage:
+    ln_w: torch.Tensor
+    fc0_w: torch.Tensor
+    fc0_b: torch.Tensor
+    fc2_w: torch.Tensor
+    fc2_b: torch.Tensor
+
+
+def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, tag: str = "smix") -> torch.Tensor:
+    require_device(x, "smix input")
+    if not x.is_contiguous():
+        raise ValueError("smix: input must be contiguous")
+    B, C, H, W = (int(v) for v in x.shape)
+    if out is None:
+        out = ctx.empty(B, C, H, W)
+    d = EsmSmixDesc()
+    d.x, d.out = x.data_ptr(), out.data_ptr()
+    if res is not None:
+        require_device(res, "smix residual")
+        if not res.is_contiguous() or res.shape != x.shape:
+            raise ValueError("smix: residual must be contiguous and shaped like the input")
+        d.res = res.data_ptr()
+    if dw is not None:
+        d.dw_w, d.dw_b = dw[0].data_ptr(), dw[1].data_ptr()
+        d.dw_k = int(dw[0].shape[-1])
+    if len(stages) > _lib.SMIX_MAX_STAGES:
+        raise ValueError("smix: at most 2 stages per launch")
+    d.nstages = len(stages)
+    for i, st in enumerate(stages):
+        d.stage[i].ln_w = st.ln_w.data_ptr()
+        d.stage[i].fc0_w, d.stage[i].fc0_b = st.fc0_w.data_ptr(), st.fc0_b.data_ptr()
+        d.stage[i].fc2_w, d.stage[i].fc2_b = st.fc2_w.data_ptr(), st.fc2_b.data_ptr()
+        ctx.hold(st.ln_w, st.fc0_w, st.fc0_b, st.fc2_w, st.fc2_b)
+    d.B, d.C, d.H, d.W = B, C, H, W
+    ctx.hold(x, out, res, *(dw or ()))
+    npix = B * H * W
+    ctx.meta.append(dict(name=tag, kind="smix", flops=npix * (2 * C * C * len(stages) + (2 * C * d.dw_k ** 2 if dw else 0)),
+                         bytes=4 * npix * C * (3 if res is not None else 2), shape=f"C{C} {H}x{W} dw{d.dw_k}"))
+    ctx.smix(d)
+    return out

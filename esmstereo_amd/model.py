@@ -1,0 +1,301 @@
+"""Drop-in ``ESMStereo`` module (reference ``models/ESMStereo.py:511-745``).
+
+Same constructor ``ESMStereo(maxdisp, gwc=False, norm_correlation=True,
+backbone="efficientnet_b2", cv_scale=4)``, same ``forward(left, right, train_status)``
+returning ``[disp]`` in eval (``[disp_1, disp_2(, disp_4)]`` with ``train_status``), same
+state-dict keys for every hot-path module, so ``test_kitti.py`` / ``save_disp.py`` run
+unchanged with ``from esmstereo_amd import __models__``.
+
+Split of the forward:
+
+* backbone side (``:640-697``: feature pyramid, FeatUp, stems, matching descriptor,
+  ``semantic``, ``conv_f2/f0``) - OUT of the hot path; PyTorch modules on the device, with
+  every ``BasicConv`` among them running through the HIP conv kernel;
+* hot path (``:700-745``: cost volume -> 3-D stems -> hourglass -> regression -> ESM
+  upsampler -> ``*4``) - compiled once per input shape into a native ``esm_plan`` of ~70
+  HIP launches and replayed as one hipGraph (:class:`HotPath`).
+"""
+from __future__ import annotations
+
+import collections
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import check, lib
+from .backbone import StubFeature
+from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
+from .engine import Ctx, require_device
+
+__all__ = ["ESMStereo", "FeatUp", "HotPath"]
+
+Feature = StubFeature  # placeholder backbone with the reference interface (see backbone.py)
+
+
+class FeatUp(nn.Module):
+    """Backbone neck (reference models/ESMStereo.py:79-125); out of the hot path."""
+
+    def __init__(self, chans: List[int], vol_size: int) -> None:
+        super().__init__()
+        self.v = vol_size
+        self.deconv32_16 = Conv2x(chans[4], chans[3], deconv=True, concat=True)
+        if self.v == 16:
+            self.conv16 = BasicConv(chans[3] * 2, chans[2] * 2, kernel_size=3, stride=1, padding=1)
+        if self.v in (8, 4):
+            self.deconv16_8 = Conv2x(chans[3] * 2, chans[2], deconv=True, concat=True)
+        if self.v == 8:
+            self.conv8 = BasicConv(chans[2] * 2, chans[2] * 2, kernel_size=3, stride=1, padding=1)
+        if self.v == 4:
+            self.deconv8_4 = Conv2x(chans[2] * 2, chans[1], deconv=True, concat=True)
+            self.conv4 = BasicConv(chans[1] * 2, chans[1] * 2, kernel_size=3, stride=1, padding=1)
+        for m in self.modules():  # He-normal init as the reference SubModule.weight_init (:25-38)
+            if isinstance(m, (nn.Conv2d, nn.Conv3d)):
+                n = math.prod(m.kernel_size) * m.out_channels
+                m.weight.data.normal_(0, math.sqrt(2.0 / n))
+            elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm3d)):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+
+    def forward(self, featL, featR):
+        outs = []
+        for feats in (featL, featR):
+            x2, x4, x8, x16, x32 = feats
+            x16 = self.deconv32_16(x32, x16)
+            if self.v == 16:
+                x16 = self.conv16(x16)
+            if self.v in (8, 4):
+                x8 = self.deconv16_8(x16, x8)
+            if self.v == 8:
+                x8 = self.conv8(x8)
+            if self.v == 4:
+                x4 = self.conv4(self.deconv8_4(x8, x4))
+            outs.append([x4, x8, x16, x32])
+        return outs[0], outs[1]
+
+
+def _stem(cin: int, c: int) -> nn.Sequential:
+    return nn.Sequential(BasicConv(cin, c, kernel_size=3, stride=2, padding=1), nn.Conv2d(c, c, 3, 1, 1, bias=False),
+                         nn.BatchNorm2d(c), nn.ReLU())
+
+
+# stems per cost-volume scale (reference ESMStereo.py:528-583): name -> (cin, cout)
+_STEMS = {
+    4: (("stem_2", 3, 32), ("stem_4", 32, 48)),
+    8: (("stem_2", 3, 32), ("stem_4", 32, 48), ("stem_8", 48, 64)),
+    16: (("stem_2", 3, 16), ("stem_4", 16, 24), ("stem_8", 24, 32), ("stem_16", 32, 40)),
+}
+# matching-descriptor input channels (ESMStereo.py:585-597) and hourglass add_channel (:624-634)
+_DESC_IN = {4: 96, 8: 160, 16: 136}
+_ADD_CHANNEL = {4: 16, 8: 8, 16: 4}
+_UPSAMPLERS = {4: upsample4, 8: upsample8, 16: upsample16}
+
+
+class HotPath:
+    """The hot path (ESMStereo.py:700-745) compiled for one set of input shapes.
+
+    Inputs live in static device buffers (``ml``, ``mr``, ``att``, ``up``); ``launch()``
+    replays the native plan (a hipGraph by default) on the current stream; ``outputs``
+    are static buffers holding the ``*4``-scaled disparities.
+    """
+
+    def __init__(self, model: "ESMStereo", B: int, h: int, w: int, att_ch: int, up_shapes: Sequence[Tuple[int, ...]],
+                 device: torch.device, train_status: bool = False, graph: bool = True, channels: int = 64):
+        self.ctx = Ctx(device, plan=True)
+        self.device = torch.device(device)
+        e = self.ctx.empty
+        self.ml = e(B, channels, h, w)
+        self.mr = e(B, channels, h, w)
+        self.att = e(B, att_ch, h, w) if att_ch else None
+        self.up = [e(*s) for s in up_shapes]
+        self.outputs = model._emit_hot(self.ctx, self.ml, self.mr, self.att, self.up, train_status)
+        self.num_ops = lib.esm_plan_num_ops(self.ctx.plan)
+        self.graph = bool(graph)
+        self._graph_ready = False
+
+    def op_kinds(self) -> List[int]:
+        return [lib.esm_plan_op_kind(self.ctx.plan, i) for i in range(self.num_ops)]
+
+    def set_probe(self, index: int, ring: int = 1024) -> None:
+        check(lib.esm_plan_set_probe(self.ctx.plan, index, ring), "set_probe")
+        self._graph_ready = False
+
+    def probe_read(self, max_n: int = 4096) -> List[float]:
+        buf = (_lib.c_float * max_n)()
+        n = check(lib.esm_plan_probe_read(self.ctx.plan, buf, max_n), "probe_read")
+        return [buf[i] for i in range(n)]
+
+    def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        s = _lib.c_void_p((stream or torch.cuda.current_stream(self.device)).cuda_stream)
+        if self.graph:
+            if not self._graph_ready:
+                check(lib.esm_plan_graph_build(self.ctx.plan, s), "graph_build")
+                self._graph_ready = True
+            check(lib.esm_plan_graph_launch(self.ctx.plan, s), "graph_launch")
+        else:
+            check(lib.esm_plan_run(self.ctx.plan, s), "plan_run")
+
+    def load_inputs(self, ml, mr, att, up) -> None:
+        self.ml.copy_(ml)
+        self.mr.copy_(mr)
+        if self.att is not None:
+            self.att.copy_(att.reshape(self.att.shape))
+        for dst, src in zip(self.up, up):
+            dst.copy_(src)
+
+    def close(self) -> None:
+        self.ctx.close()
+
+
+class ESMStereo(nn.Module):
+    """ESMStereo stereo network with the HIP hot path (reference models/ESMStereo.py:511-745)."""
+
+    def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
+                 backbone: str = "efficientnet_b2", cv_scale: int = 4) -> None:
+        super().__init__()
+        self.maxdisp = maxdisp
+        self.vol_size = cv_scale
+        self.gwc = gwc
+        self.norm_correlation = norm_correlation
+        self.backbone = backbone
+        if cv_scale not in _STEMS:
+            raise ValueError("Choose the cost volume resolution: 4, 8, 16")
+        self.feature = Feature(self.backbone)
+        if cv_scale in (4, 8):
+            self.feature_up = FeatUp(self.feature.chans, cv_scale)
+        for name, cin, c in _STEMS[cv_scale]:
+            setattr(self, name, _stem(cin, c))
+        self.conv = BasicConv(_DESC_IN[cv_scale], 64, kernel_size=3, padding=1, stride=1)
+        self.desc = nn.Conv2d(64, 64, kernel_size=1, padding=0, stride=1)
+        if cv_scale == 16:
+            self.conv_f2 = BasicConv(96, 32, kernel_size=3, padding=1, stride=1)
+            self.conv_f0 = BasicConv(16, 24, kernel_size=3, padding=1, stride=1)
+        red = 8
+        if norm_correlation:
+            print("Cost volumes: norm correlation")
+            if cv_scale == 16:
+                self.semantic = nn.Sequential(BasicConv(96, 32, kernel_size=3, stride=1, padding=1),
+                                              nn.Conv2d(32, 8, 3, 1, 1, bias=False))
+            self.corr_stem = BasicConv(1, red, is_3d=True, kernel_size=3, padding=1, stride=1)
+        if gwc:
+            print("Cost volumes: gwc ")
+            if cv_scale == 16:
+                self.semantic = nn.Sequential(BasicConv(96, 64, kernel_size=3, stride=1, padding=1),
+                                              nn.Conv2d(64, 32, 3, 1, 1, bias=False))
+            self.num_groups = 32
+            self.group_stem = BasicConv(self.num_groups, red, is_3d=True, kernel_size=3, padding=1, stride=1)
+        self.agg = BasicConv(red, red, is_3d=True, kernel_size=3, padding=1, stride=1)
+        self.upsample_module = _UPSAMPLERS[cv_scale]()
+        self.aggregation_out = aggregation(red, _ADD_CHANNEL[cv_scale])
+        for name, mod in self.named_modules():  # launch names for profiles / the bench probe
+            object.__setattr__(mod, "_esm_name", name)
+        self._plans: "collections.OrderedDict" = collections.OrderedDict()
+        self.use_graph = os.environ.get("ESM_GRAPH", "1") != "0"
+
+    # ------------------------------------------------------------------ plan cache
+    def invalidate_plans(self) -> None:
+        """Drop compiled hot-path plans (call after editing weights in place)."""
+        for hp in self._plans.values():
+            hp.close()
+        self._plans.clear()
+
+    def _apply(self, fn, *args, **kwargs):
+        self.invalidate_plans()
+        return super()._apply(fn, *args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.invalidate_plans()
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    # ------------------------------------------------------------------ forward pieces
+    def prefix(self, left: torch.Tensor, right: torch.Tensor):
+        """Backbone side, reference lines 640-697 -> (match_left, match_right, att, upsampler feats)."""
+        vs = self.vol_size
+        fl = self.feature(left)
+        fr = self.feature(right)
+        if vs in (4, 8):
+            fl, fr = self.feature_up(fl, fr)
+        sx, sy = self.stem_2(left), self.stem_2(right)
+        stems_x, stems_y = [sx], [sy]
+        for name, _, _ in _STEMS[vs][1:]:
+            stems_x.append(getattr(self, name)(stems_x[-1]))
+            stems_y.append(getattr(self, name)(stems_y[-1]))
+        idx = {4: 0, 8: 1, 16: 3}[vs]
+        ml = self.desc(self.conv(torch.cat((fl[idx], stems_x[-1]), 1)))
+        mr = self.desc(self.conv(torch.cat((fr[idx], stems_y[-1]), 1)))
+        att = self.semantic(fl[3]) if vs == 16 else None
+        if vs == 4:
+            up = [fl[1], fl[0], sx]
+        elif vs == 8:
+            up = [fl[2], fl[1], fl[0], sx]
+        else:
+            up = [fl[2], self.conv_f2(fl[3]), fl[1], self.conv_f0(fl[0])]
+        return ml, mr, att, up
+
+    def _emit_hot(self, ctx: Ctx, ml: torch.Tensor, mr: torch.Tensor, att: Optional[torch.Tensor],
+                  up: Sequence[torch.Tensor], train_status: bool) -> List[torch.Tensor]:
+        B, C, h, w = (int(v) for v in ml.shape)
+        D = self.maxdisp // self.vol_size
+        vs = self.vol_size
+        if self.gwc:
+            V = ctx.empty(B, self.num_groups, D, h, w)
+            a = att.reshape(B, self.num_groups, h, w) if (vs == 16 and att is not None) else None
+            ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
+            vol = self.group_stem.emit(ctx, [V])
+        elif self.norm_correlation:
+            V = ctx.empty(B, 1, D, h, w)
+            work = ctx.empty(2, B, C, h, w)
+            ctx.normcorr(ml, mr, V, work, B, C, h, w, D)
+            mul = att.reshape(B, -1, h, w) if (vs == 16 and att is not None) else None
+            vol = self.corr_stem.emit(ctx, [V], mul=mul)
+        else:
+            raise UnboundLocalError("local variable 'volume' referenced before assignment")
+        vol = self.agg.emit(ctx, [vol])
+        cost = self.aggregation_out.emit(ctx, vol)
+        Dc = int(cost.shape[2])
+        if Dc != D:
+            raise RuntimeError(f"The size of tensor a ({Dc}) must match the size of tensor b ({D}) at non-singleton "
+                               f"dimension 1 (maxdisp // cv_scale must be even, SURVEY.md §0.4)")
+        init = ctx.empty(B, 1, h, w)
+        ctx.regression(1 if vs == 4 else 0, cost.view(B, D, h, w), init, B, D, h, w)
+        outs = self.upsample_module.emit(ctx, up, init, final_scale=4.0,
+                                         scaled_copies=4.0 if train_status else None)
+        if train_status:
+            finals, copies = outs
+            return [finals[0].view(B, finals[0].shape[-2], finals[0].shape[-1])] + \
+                   [c.view(B, c.shape[-2], c.shape[-1]) for c in copies]
+        return [outs[0].view(B, outs[0].shape[-2], outs[0].shape[-1])]
+
+    def hot_path(self, ml: torch.Tensor, mr: torch.Tensor, att: Optional[torch.Tensor], up: Sequence[torch.Tensor],
+                 train_status: bool = False) -> List[torch.Tensor]:
+        """Run reference lines 700-745 on given matching features (compiled + cached plan)."""
+        for t in [ml, mr, *up] + ([att] if att is not None else []):
+            require_device(t, "hot-path input")
+        key = (tuple(ml.shape), None if att is None else tuple(att.shape), tuple(tuple(u.shape) for u in up),
+               bool(train_status), ml.device)
+        hp = self._plans.get(key)
+        if hp is None:
+            hp = HotPath(self, int(ml.shape[0]), int(ml.shape[2]), int(ml.shape[3]),
+                         0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], ml.device,
+                         train_status, graph=self.use_graph, channels=int(ml.shape[1]))
+            self._plans[key] = hp
+            while len(self._plans) > 4:
+                self._plans.popitem(last=False)[1].close()
+        else:
+            self._plans.move_to_end(key)
+        hp.load_inputs(ml, mr, att, up)
+        hp.launch()
+        return [o.clone() for o in hp.outputs]
+
+    def forward(self, left: torch.Tensor, right: torch.Tensor, train_status: bool) -> List[torch.Tensor]:
+        if self.training:
+            raise NotImplementedError("esmstereo_amd is an inference engine (eval-mode BatchNorm folded into the "
+                                      "kernels); call model.eval()")
+        require_device(left, "left")
+        require_device(right, "right")
+        with torch.no_grad():
+            ml, mr, att, up = self.prefix(left, right)
+            return self.hot_path(ml, mr, att, up, train_status)

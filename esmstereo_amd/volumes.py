@@ -1,0 +1,98 @@
+"""Op-level drop-ins for the free functions of the reference ``models/submodule.py``.
+
+Same names, argument meaning and failure class as the reference (``maxdisp`` here is
+already the volume depth D, as at the call sites ``models/ESMStereo.py:701,708``); every
+computation runs in a HIP kernel of ``libesmstereo_amd.so``.  Device tensors only.
+"""
+from __future__ import annotations
+
+import torch
+
+from .engine import Ctx, require_device
+
+__all__ = ["build_gwc_volume", "build_concat_volume", "build_norm_correlation_volume", "disparity_regression",
+           "regression_topk"]
+
+
+def _feat_pair(refimg_fea: torch.Tensor, targetimg_fea: torch.Tensor):
+    require_device(refimg_fea, "refimg_fea")
+    require_device(targetimg_fea, "targetimg_fea")
+    if refimg_fea.dim() != 4 or refimg_fea.shape != targetimg_fea.shape:
+        raise RuntimeError(f"feature shapes must be equal [B,C,H,W]: {tuple(refimg_fea.shape)} vs "
+                           f"{tuple(targetimg_fea.shape)}")
+    return refimg_fea.contiguous(), targetimg_fea.contiguous()
+
+
+def build_gwc_volume(refimg_fea: torch.Tensor, targetimg_fea: torch.Tensor, maxdisp: int, num_groups: int,
+                     att: torch.Tensor = None) -> torch.Tensor:
+    """``build_gwc_volume`` (submodule.py:151-161) -> [B, G, maxdisp, H, W].
+
+    ``att`` ([B, G, H, W] or [B, G, 1, H, W]) optionally fuses the ESMStereo-S
+    ``volume * att`` of ESMStereo.py:711 into the same kernel.
+    """
+    L, R = _feat_pair(refimg_fea, targetimg_fea)
+    B, C, H, W = (int(v) for v in L.shape)
+    assert C % num_groups == 0  # the reference asserts (submodule.py:145)
+    V = torch.empty(B, num_groups, maxdisp, H, W, device=L.device, dtype=torch.float32)
+    if maxdisp == 0 or V.numel() == 0:
+        return V.zero_()
+    if att is not None:
+        require_device(att, "att")
+        att = att.reshape(B, num_groups, H, W).contiguous()
+    Ctx(L.device).gwc(L, R, att, V, B, C, H, W, int(maxdisp), int(num_groups))
+    return V
+
+
+def build_concat_volume(refimg_fea: torch.Tensor, targetimg_fea: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """``build_concat_volume`` (submodule.py:129-140) -> [B, 2C, maxdisp, H, W]."""
+    L, R = _feat_pair(refimg_fea, targetimg_fea)
+    B, C, H, W = (int(v) for v in L.shape)
+    V = torch.empty(B, 2 * C, maxdisp, H, W, device=L.device, dtype=torch.float32)
+    if maxdisp == 0 or V.numel() == 0:
+        return V.zero_()
+    Ctx(L.device).concat(L, R, V, B, C, H, W, int(maxdisp))
+    return V
+
+
+def build_norm_correlation_volume(refimg_fea: torch.Tensor, targetimg_fea: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """``build_norm_correlation_volume`` (submodule.py:191-200) -> [B, 1, maxdisp, H, W]."""
+    L, R = _feat_pair(refimg_fea, targetimg_fea)
+    B, C, H, W = (int(v) for v in L.shape)
+    V = torch.empty(B, 1, maxdisp, H, W, device=L.device, dtype=torch.float32)
+    if maxdisp == 0 or V.numel() == 0:
+        return V.zero_()
+    work = torch.empty(2, B, C, H, W, device=L.device, dtype=torch.float32)
+    Ctx(L.device).normcorr(L, R, V, work, B, C, H, W, int(maxdisp))
+    return V
+
+
+def disparity_regression(x: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """``disparity_regression`` (submodule.py:211-216): sum_d x[:, d] * d -> [B, H, W] (no softmax)."""
+    assert len(x.shape) == 4
+    require_device(x, "disparity_regression input")
+    B, D, H, W = (int(v) for v in x.shape)
+    if D != maxdisp:
+        raise RuntimeError(f"The size of tensor a ({D}) must match the size of tensor b ({maxdisp}) at "
+                           "non-singleton dimension 1")
+    x = x.contiguous()
+    out = torch.empty(B, H, W, device=x.device, dtype=torch.float32)
+    Ctx(x.device).regression(0, x, out, B, D, H, W)
+    return out
+
+
+def regression_topk(cost: torch.Tensor, disparity_samples: torch.Tensor, k: int) -> torch.Tensor:
+    """``regression_topk`` (submodule.py:218-225) -> [B, 1, H, W]; k = 2 (the ESMStereo call)."""
+    if k != 2:
+        raise NotImplementedError("esmstereo_amd implements regression_topk for k=2 (models/ESMStereo.py:721)")
+    require_device(cost, "regression_topk cost")
+    B, D, H, W = (int(v) for v in cost.shape)
+    if D < k:
+        raise RuntimeError(f"selected index k out of range (D={D}, k={k})")
+    cost = cost.contiguous()
+    samples = None
+    if disparity_samples is not None:
+        require_device(disparity_samples, "disparity_samples")
+        samples = disparity_samples.expand(B, D, H, W).contiguous()
+    out = torch.empty(B, 1, H, W, device=cost.device, dtype=torch.float32)
+    Ctx(cost.device).regression(1, cost, out, B, D, H, W, samples=samples)
+    return out

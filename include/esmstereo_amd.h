@@ -1,0 +1,179 @@
+/*
+ * esmstereo_amd — C ABI of the MI355X (gfx950) ESMStereo hot path.
+ *
+ * Every entry point takes caller-owned DEVICE pointers (fp32, contiguous unless a stride
+ * is given), plain sizes and a HIP stream handle passed as `void*` (a `hipStream_t`; NULL =
+ * the default stream).  Kernels never allocate or free; launches are stream-ordered and the
+ * library keeps no global mutable state apart from a thread-local last-error string.
+ * Return value: ESM_OK (0) or a negative ESM_ERR_* code; esm_last_error() says why.
+ *
+ * Each function replaces one reference interface (file:line in /root/reference):
+ *   esm_gwc_volume_f32        models/submodule.py:151-161 build_gwc_volume (+ the S-variant
+ *                             `volume * att` at models/ESMStereo.py:711 when att != NULL)
+ *   esm_concat_volume_f32     models/submodule.py:129-140 build_concat_volume
+ *   esm_normcorr_volume_f32   models/submodule.py:187-200 build_norm_correlation_volume
+ *   esm_disp_regression_f32   models/submodule.py:211-216 disparity_regression
+ *   esm_topk2_regression_f32  models/submodule.py:218-225 regression_topk(cost, arange, k=2)
+ *   esm_conv_f32              models/submodule.py:12-38 BasicConv (Conv2d/3d, ConvTranspose2d/3d,
+ *                             eval BatchNorm, GELU) and the plain convs of models/ESMStereo.py:
+ *                             129-509 with their fused neighbours (crop+cat :172,177,230,234;
+ *                             PixelShuffle+SiLU :265-268; bilinear-upsample + add :307,316;
+ *                             `* att` :703; residual adds of models/shufflemixer.py:130-131)
+ *   esm_smix_f32              models/shufflemixer.py:23-112 LayerNorm('BiasFree') +
+ *                             SplitPointMlp + channel shuffle + residual, optionally preceded
+ *                             by the depthwise 7x7 `spatial` conv
+ *   esm_plan_*                the orchestration of models/ESMStereo.py:700-745 as a native
+ *                             launch list, optionally replayed as one hipGraph
+ */
+#ifndef ESMSTEREO_AMD_H
+#define ESMSTEREO_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESM_OK 0
+#define ESM_ERR_ARG (-1)
+#define ESM_ERR_LAUNCH (-2)
+#define ESM_ERR_UNSUPPORTED (-3)
+#define ESM_ERR_RUNTIME (-4)
+
+#define ESM_ACT_NONE 0
+#define ESM_ACT_GELU 1 /* exact erf GELU, nn.GELU() */
+#define ESM_ACT_SILU 2
+#define ESM_ACT_RELU 3
+
+#define ESM_MAX_SRC 3
+
+/* One channel-slice source of a (possibly concatenated, possibly cropped) conv input.
+ * Element strides; the innermost (W) stride is 1.  For 2-D tensors sd is ignored. */
+typedef struct {
+    const float* ptr;
+    int32_t C;
+    int32_t reserved;
+    int64_t sb, sc, sd, sh;
+} esm_src;
+
+/* Implicit-GEMM convolution on NC(D)HW fp32, fp32 MFMA.
+ * 2-D convs use kd = 1, Di = Do = 1.
+ * Transposed convs are supported for kernel 4, stride 2, padding 1 (the only form the
+ * reference uses); out extent = 2 x in extent.
+ * weights: packed by esm_conv_pack_* conventions (see esmstereo_amd/engine.py):
+ *   normal:     w[tap][cin_pad][cout_pad], tap = (kd_i*kh + kh_i)*kw + kw_i
+ *   transposed: w[cls][tap][cin_pad][cout_pad], cls = parity class of the output voxel
+ * Epilogue order: v = acc*scale[c] + shift[c] (scale NULL -> 1, shift NULL -> 0);
+ *   v = act(v); v *= mul[b,c,y,x] (broadcast over d); v += res[b,c,d,y,x];
+ *   v = bilinear_up(up)[b,0,y,x] + v; store v * post_scale (through a PixelShuffle of
+ *   factor `shuffle` when > 1) and, when out2 != NULL, v * post_scale2 to out2. */
+typedef struct {
+    esm_src src[ESM_MAX_SRC];
+    int32_t nsrc;
+    int32_t B, Cin;
+    int32_t Di, Hi, Wi;
+    int32_t Do, Ho, Wo;
+    int32_t kd, kh, kw;
+    int32_t stride;
+    int32_t transposed;
+    int32_t pd, ph, pw;
+    int32_t Cout;
+    int32_t cin_pad, cout_pad;
+    const float* w;
+    const float* scale;
+    const float* shift;
+    int32_t act;
+    int32_t shuffle;
+    const float* mul;
+    int64_t mb, mc, mh;
+    const float* res;
+    int64_t rb, rc, rd, rh;
+    float* out;
+    int64_t ob, oc, od, oh;
+    const float* up;
+    int32_t up_h, up_w, up_f;
+    int32_t reserved;
+    int64_t ub, uh;
+    float post_scale;
+    float post_scale2;
+    float* out2; /* nullable: second copy of the result (same strides as out), x post_scale2 / post_scale */
+} esm_conv_desc;
+
+/* ShuffleMixer per-pixel chain on a [B, C, H, W] tensor, C in {8, 16}:
+ *   t = dw ? (depthwise KxK conv of x with bias) : x          (SMLayer.spatial)
+ *   for s in stages: t = shuffle(cat(fc2(silu(fc0(LN_s(t)[:C/2]))), LN_s(t)[C/2:])) + t
+ *   if res: t += res
+ * (SMLayer.forward, shufflemixer.py:108-112; FMBlock `net(x) + x`, :130). */
+#define ESM_SMIX_MAX_STAGES 2
+typedef struct {
+    const float* ln_w;  /* [C] */
+    const float* fc0_w; /* [C][C/2] */
+    const float* fc0_b; /* [C] */
+    const float* fc2_w; /* [C/2][C] */
+    const float* fc2_b; /* [C/2] */
+} esm_smix_stage;
+
+typedef struct {
+    const float* x;
+    float* out;
+    const float* res; /* nullable */
+    const float* dw_w; /* [C][K][K], nullable (no depthwise) */
+    const float* dw_b; /* [C] */
+    int32_t dw_k;
+    int32_t nstages;
+    esm_smix_stage stage[ESM_SMIX_MAX_STAGES];
+    int32_t B, C, H, W;
+} esm_smix_desc;
+
+const char* esm_last_error(void);
+int esm_version(void);
+/* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
+ * 2 esm_smix_stage, 3 esm_smix_desc; -1 for an unknown id. */
+int esm_struct_size(int which);
+
+int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* V, int B, int C, int H, int W,
+                       int D, int G, void* stream);
+int esm_concat_volume_f32(const float* L, const float* R, float* V, int B, int C, int H, int W, int D,
+                          void* stream);
+/* work: caller-owned scratch of 2*B*C*H*W floats (normalised features). */
+int esm_normcorr_volume_f32(const float* L, const float* R, float* V, float* work, int B, int C, int H, int W,
+                            int D, void* stream);
+int esm_disp_regression_f32(const float* cost, float* out, int B, int D, int H, int W, void* stream);
+/* samples: [B, D, H, W] disparity_samples, or NULL for arange(D) (the ESMStereo call). */
+int esm_topk2_regression_f32(const float* cost, const float* samples, float* out, int B, int D, int H, int W,
+                             void* stream);
+int esm_conv_f32(const esm_conv_desc* desc, void* stream);
+int esm_smix_f32(const esm_smix_desc* desc, void* stream);
+
+/* ---- native launch plan (the hot path as one replayable unit) ---- */
+typedef struct esm_plan esm_plan;
+esm_plan* esm_plan_create(void);
+void esm_plan_destroy(esm_plan* plan);
+int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
+int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
+int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
+                     int H, int W, int D, int G);
+int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
+                        int D);
+int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float* V, float* work, int B, int C,
+                          int H, int W, int D);
+/* kind 0 = disparity_regression, 1 = regression_topk k=2 */
+int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
+int esm_plan_num_ops(const esm_plan* plan);
+/* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression */
+int esm_plan_op_kind(const esm_plan* plan, int index);
+int esm_plan_run(esm_plan* plan, void* stream);
+/* Capture the launch list into a hipGraph (instantiated once; replays are cheap). */
+int esm_plan_graph_build(esm_plan* plan, void* stream);
+int esm_plan_graph_launch(esm_plan* plan, void* stream);
+/* Probe: record a hipEvent pair around op `index` on every run/replay (ring of `ring`
+ * pairs, ring <= 4096).  esm_plan_probe_read returns the elapsed ms of the completed
+ * runs since the last read (caller synchronises first); returns the count written. */
+int esm_plan_set_probe(esm_plan* plan, int index, int ring);
+int esm_plan_probe_read(esm_plan* plan, float* ms, int max);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ESMSTEREO_AMD_H */

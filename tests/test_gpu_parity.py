@@ -1,0 +1,359 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the reference goldens and the
+CPU oracle.  Run on the MI355X box: ``python -m pytest tests -m gpu``.
+
+Tolerances (fp32 everywhere; north_star: "EPE within 1e-3 of the PyTorch reference"):
+* cost volumes gwc / concat and disparity_regression: bit-exact (same rounding sequence);
+* norm-corr volume, top-2 regression, single convs, ShuffleMixer: relative max error <= 1e-5
+  (different but equally exact fp32 summation orders);
+* whole hot path, S / M: EPE (mean |d - d_ref|, px at full res) <= 1e-3 and relative max
+  error <= 1e-4;
+* whole hot path, L (``regression_topk`` is discontinuous at near-ties):
+  the count of low-res pixels whose top-2 index set flips is reported, and EPE <= 1e-3 is
+  required outside the dilated, upsampled flip mask.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import GOLDEN_DIR, feature_pair, load_golden, load_spec, seeded_state
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a ROCm GPU")]
+
+import esmstereo_amd as E  # noqa: E402
+from esmstereo_amd.engine import Ctx, pack_conv, run_conv, ACT_GELU, ACT_SILU, ACT_NONE  # noqa: E402
+from oracle import esm_oracle as O  # noqa: E402
+
+DEV = torch.device("cuda")
+
+with open(os.path.join(GOLDEN_DIR, "manifest.json")) as f:
+    MANIFEST = json.load(f)
+HOT = sorted(k for k in MANIFEST if k.startswith("hot_"))
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def epe(a, b):
+    return float((a.detach().double().cpu() - torch.as_tensor(b).double().cpu()).abs().mean())
+
+
+# ----------------------------------------------------------------------------- op level
+
+
+def test_ops_golden():
+    g = load_golden("ops.npz")
+    V = E.build_gwc_volume(cu(g["gwc_L"]), cu(g["gwc_R"]), 8, 32)
+    assert torch.equal(V.cpu(), torch.from_numpy(g["gwc_out"])), "gwc must be bit-exact"
+    Va = E.build_gwc_volume(cu(g["gwc_L"]), cu(g["gwc_R"]), 8, 32, att=cu(g["gwc_att"]))
+    assert torch.equal(Va.cpu(), torch.from_numpy(g["gwc_att_out"])), "gwc*att must be bit-exact"
+    Vc = E.build_concat_volume(cu(g["concat_L"]), cu(g["concat_R"]), 6)
+    assert torch.equal(Vc.cpu(), torch.from_numpy(g["concat_out"]))
+    Vn = E.build_norm_correlation_volume(cu(g["nc_L"]), cu(g["nc_R"]), 7)
+    assert rel(Vn, g["nc_out"]) < 1e-5
+    r = E.disparity_regression(cu(g["reg_cost"]), 12)
+    assert torch.equal(r.cpu(), torch.from_numpy(g["reg_out"])), "disparity_regression must be bit-exact"
+    tc = cu(g["topk_cost"])
+    ds = torch.arange(0, 12, dtype=torch.float32, device=DEV).view(1, 12, 1, 1).repeat(2, 1, 5, 9)
+    t = E.regression_topk(tc, ds, 2)
+    assert rel(t, g["topk_out"]) < 1e-6
+
+
+@pytest.mark.parametrize("B,C,H,W,D,G", [(1, 64, 24, 78, 12, 32), (2, 64, 7, 13, 9, 32), (1, 64, 5, 3, 8, 32),
+                                          (3, 32, 6, 10, 5, 4), (1, 64, 96, 312, 48, 32), (1, 8, 4, 6, 1, 8)])
+def test_volumes_vs_oracle(B, C, H, W, D, G):
+    L, R = feature_pair(B, C, H, W, 5, max(D, 2))
+    V = E.build_gwc_volume(L.to(DEV), R.to(DEV), D, G)
+    assert torch.equal(V.cpu(), O.gwc_volume(L, R, D, G))
+    Vc = E.build_concat_volume(L.to(DEV), R.to(DEV), D)
+    assert torch.equal(Vc.cpu(), O.concat_volume(L, R, D))
+    Vn = E.build_norm_correlation_volume(L.to(DEV), R.to(DEV), D)
+    assert rel(Vn, O.normcorr_volume(L, R, D)) < 1e-5
+
+
+def test_regressions_vs_oracle():
+    g = torch.Generator().manual_seed(3)
+    cost = torch.randn(2, 48, 17, 33, generator=g)
+    cost[0, 5, 0, :4] = cost[0, 9, 0, :4] = 10.0  # exact ties -> lowest index first
+    out = E.disparity_regression(cost.to(DEV), 48)
+    assert torch.equal(out.cpu(), O.disparity_regression(cost, 48))
+    t = E.regression_topk(cost.to(DEV), torch.arange(48, dtype=torch.float32, device=DEV).view(1, 48, 1, 1), 2)
+    assert rel(t, O.regression_topk2(cost)) < 1e-6
+    with pytest.raises(RuntimeError):
+        E.disparity_regression(cost.to(DEV), 47)
+
+
+# ----------------------------------------------------------------------------- convs
+
+
+def _ref_conv(x_list, conv, bn, act, mul=None, res=None, up=None, up_f=0, shuffle=1, post=1.0):
+    x = torch.cat([t.double() for t in x_list], 1)
+    w = conv.weight.detach().double()
+    nd = w.dim() - 2
+    if isinstance(conv, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d)):
+        fn = F.conv_transpose3d if nd == 3 else F.conv_transpose2d
+    else:
+        fn = F.conv3d if nd == 3 else F.conv2d
+    b = conv.bias.detach().double() if conv.bias is not None else None
+    y = fn(x, w, b, conv.stride, conv.padding)
+    if bn is not None:
+        y = F.batch_norm(y, bn.running_mean.double(), bn.running_var.double(), bn.weight.double(), bn.bias.double(),
+                         False, 0.0, bn.eps)
+    if shuffle > 1:
+        y = F.pixel_shuffle(y, shuffle)
+    y = {ACT_GELU: F.gelu, ACT_SILU: F.silu, ACT_NONE: lambda t: t}[act](y)
+    if mul is not None:
+        y = y * (mul.double().unsqueeze(2) if nd == 3 else mul.double())
+    if res is not None:
+        y = y + res.double()
+    if up is not None:
+        y = F.interpolate(up.double(), scale_factor=up_f, mode="bilinear", align_corners=False) + y
+    return (y * post).float()
+
+
+def _mk(nd, cin, cout, k, s, p, transposed=False, bias=False, bn=True, seed=0):
+    torch.manual_seed(seed)
+    cls = {(2, False): torch.nn.Conv2d, (3, False): torch.nn.Conv3d, (2, True): torch.nn.ConvTranspose2d,
+           (3, True): torch.nn.ConvTranspose3d}[(nd, transposed)]
+    conv = cls(cin, cout, k, s, p, bias=bias)
+    b = None
+    if bn:
+        b = (torch.nn.BatchNorm3d if nd == 3 else torch.nn.BatchNorm2d)(cout).eval()
+        b.running_mean.uniform_(-0.2, 0.2)
+        b.running_var.uniform_(0.5, 1.5)
+        b.weight.data.uniform_(0.8, 1.2)
+        b.bias.data.uniform_(-0.2, 0.2)
+    return conv, b
+
+
+CONV2D = [(1, 32, 5, 1, 1), (16, 16, 3, 1, 1), (16, 16, 3, 2, 1), (56, 16, 1, 1, 0), (16, 16, 1, 1, 1),
+          (8, 1, 3, 1, 1), (3, 32, 3, 2, 1), (40, 72, 3, 1, 1), (16, 24, 3, 1, 1), (24, 40, 3, 2, 1)]
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p", CONV2D)
+@pytest.mark.parametrize("act", [ACT_GELU, ACT_SILU])
+def test_conv2d(cin, cout, k, s, p, act):
+    conv, bn = _mk(2, cin, cout, k, s, p)
+    x = torch.randn(2, cin, 23, 37)
+    y = run_conv(Ctx(DEV), pack_conv(conv, bn, act), [x.to(DEV)])
+    assert rel(y, _ref_conv([x], conv, bn, act)) < 1e-5
+
+
+CONV3D = [(32, 8, 3, 1, 1), (8, 8, 3, 1, 1), (8, 24, 3, 2, 1), (24, 24, 3, 1, 1), (80, 40, 1, 1, 0), (1, 8, 3, 1, 1),
+          (40, 72, 3, 2, 1)]
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p", CONV3D)
+def test_conv3d(cin, cout, k, s, p):
+    conv, bn = _mk(3, cin, cout, k, s, p, seed=1)
+    x = torch.randn(1, cin, 6, 9, 21)
+    y = run_conv(Ctx(DEV), pack_conv(conv, bn, ACT_GELU), [x.to(DEV)])
+    assert rel(y, _ref_conv([x], conv, bn, ACT_GELU)) < 1e-5
+
+
+@pytest.mark.parametrize("nd,cin,cout,bn", [(2, 16, 16, True), (2, 16, 1, False), (3, 72, 40, True),
+                                            (3, 24, 1, False), (3, 16, 12, True), (2, 32, 32, True)])
+def test_conv_transposed(nd, cin, cout, bn):
+    conv, b = _mk(nd, cin, cout, 4, 2, 1, transposed=True, bn=bn, seed=2)
+    shape = (2, cin, 5, 11, 13) if nd == 3 else (2, cin, 11, 19)
+    x = torch.randn(*shape)
+    act = ACT_GELU if bn else ACT_NONE
+    y = run_conv(Ctx(DEV), pack_conv(conv, b, act), [x.to(DEV)])
+    assert rel(y, _ref_conv([x], conv, b, act)) < 1e-5
+
+
+def test_conv_multisource_crop_and_epilogues():
+    # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
+    conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
+    big = torch.randn(1, 16, 26, 40)
+    a = torch.randn(1, 16, 24, 39)
+    c = torch.randn(1, 24, 24, 39)
+    crop = big.to(DEV)[:, :, :24, :39]
+    y = run_conv(Ctx(DEV), pack_conv(conv, bn, ACT_GELU), [crop, a.to(DEV), c.to(DEV)])
+    assert rel(y, _ref_conv([big[:, :, :24, :39], a, c], conv, bn, ACT_GELU)) < 1e-5
+    # residual + mul (att broadcast over depth) on a 3-D conv
+    conv3, bn3 = _mk(3, 1, 8, 3, 1, 1, seed=4)
+    x3 = torch.randn(2, 1, 4, 6, 10)
+    att = torch.randn(2, 8, 6, 10)
+    res3 = torch.randn(2, 8, 4, 6, 10)
+    y3 = run_conv(Ctx(DEV), pack_conv(conv3, bn3, ACT_GELU), [x3.to(DEV)], mul=att.to(DEV), res=res3.to(DEV))
+    assert rel(y3, _ref_conv([x3], conv3, bn3, ACT_GELU, mul=att, res=res3)) < 1e-5
+    # ConvT 16->1 + bilinear(prev, x4) + x4 scale with an unscaled copy
+    ct, _ = _mk(2, 16, 1, 4, 2, 1, transposed=True, bn=False, seed=5)
+    xt = torch.randn(1, 16, 24, 40)
+    prev = torch.randn(1, 1, 12, 20)
+    cp = torch.empty(1, 1, 48, 80, device=DEV)
+    yt = run_conv(Ctx(DEV), pack_conv(ct, None, ACT_NONE), [xt.to(DEV)], up=prev.to(DEV), up_f=4, post_scale=4.0,
+                  out2=cp, post_scale2=1.0)
+    ref = _ref_conv([xt], ct, None, ACT_NONE, up=prev, up_f=4)
+    assert rel(yt, ref * 4) < 1e-5
+    assert rel(cp, ref) < 1e-5
+    # 1x1 conv + PixelShuffle(4) + SiLU
+    cs, _ = _mk(2, 8, 128, 1, 1, 0, bias=True, bn=False, seed=6)
+    xs = torch.randn(1, 8, 6, 20)
+    ys = run_conv(Ctx(DEV), pack_conv(cs, None, ACT_SILU), [xs.to(DEV)], shuffle=4)
+    assert rel(ys, _ref_conv([xs], cs, None, ACT_SILU, shuffle=4)) < 1e-5
+
+
+# ----------------------------------------------------------------------------- ShuffleMixer
+
+
+@pytest.mark.parametrize("C", [8, 16])
+def test_fmblock_vs_oracle(C):
+    torch.manual_seed(7)
+    blk = E.FMBlock(C, 7, 2).eval()
+    with torch.no_grad():
+        for n, p in blk.named_parameters():
+            if n.endswith("norm1.body.weight") or n.endswith("norm2.body.weight"):
+                p.uniform_(0.8, 1.2)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    x = torch.randn(2, C, 21, 45)
+    y = blk.to(DEV)(x.to(DEV))
+    assert rel(y, O.fm_block(sd, "", x)) < 1e-5
+
+
+# ----------------------------------------------------------------------------- hot path
+
+
+def _model_from_manifest(name, maxdisp=None):
+    m = MANIFEST[name]
+    model = E.ESMStereo(maxdisp or m["maxdisp"], m["cv"] == "gwc", m["cv"] == "nc", m["backbone"], m["cv_scale"])
+    sd = seeded_state(load_spec(m["spec"]), m["seed"])
+    model.load_state_dict(sd)
+    return model.eval().to(DEV), sd, m
+
+
+def _top2_sets(cost):
+    idx = torch.sort(cost.double(), dim=1, descending=True, stable=True)[1][:, :2]
+    return torch.sort(idx, dim=1)[0]
+
+
+def _check_disp(name, got, ref, m, flip_mask_lowres=None):
+    if flip_mask_lowres is None or not bool(flip_mask_lowres.any()):
+        assert epe(got, ref) <= 1e-3, (name, epe(got, ref))
+        assert rel(got, ref) <= 1e-4, (name, rel(got, ref))
+        return 0
+    f = got.shape[-1] // flip_mask_lowres.shape[-1]
+    mask = F.max_pool2d(flip_mask_lowres.float().unsqueeze(1), 9, 1, 4)  # dilate by the upsampler's reach
+    mask = F.interpolate(mask, scale_factor=f, mode="nearest")[:, 0] > 0
+    keep = ~mask
+    d = (got.double().cpu() - torch.as_tensor(ref).double()).abs()
+    assert float(d[keep].mean()) <= 1e-3, (name, float(d[keep].mean()))
+    return int(flip_mask_lowres.sum())
+
+
+@pytest.mark.parametrize("name", HOT)
+def test_hot_path_golden(name):
+    model, sd, m = _model_from_manifest(name)
+    g = load_golden(name)
+    up = [cu(g[f"up_{i}"]) for i in range(4) if f"up_{i}" in g]
+    att = cu(g["att"]) if "att" in g else None
+    # module-level pieces, eager
+    cost = model.aggregation_out(cu(g["agg"]))
+    assert rel(cost, g["cost"]) < 1e-5
+    flips = None
+    if m["cv_scale"] == 4:
+        flips = (_top2_sets(cost.squeeze(1).cpu()) != _top2_sets(torch.from_numpy(g["cost"][:, 0]))).any(1)
+    # whole hot path, compiled plan + graph, eval and train outputs
+    for train in (False, True):
+        outs = model.hot_path(cu(g["match_left"]), cu(g["match_right"]), att, up, train)
+        n = m["n_train_outputs"] if train else 1
+        assert len(outs) == n
+        for i in range(n):
+            assert outs[i].shape == g[f"disp_{i}"].shape
+            _check_disp(name, outs[i], g[f"disp_{i}"], m, flips)
+
+
+@pytest.mark.parametrize("name", HOT)
+def test_full_forward_golden(name):
+    """The drop-in module: backbone side on PyTorch/MIOpen + HIP BasicConvs, hot path on HIP."""
+    model, sd, m = _model_from_manifest(name)
+    g = load_golden(name)
+    with torch.no_grad():
+        out = model(cu(g["left"]), cu(g["right"]), False)
+    assert isinstance(out, list) and len(out) == 1
+    ref = g["disp_0"]
+    if m["cv_scale"] == 4:
+        assert epe(out[0], ref) < 0.05  # prefix differences (MIOpen vs CPU) may flip near-ties
+    else:
+        assert epe(out[0], ref) <= 1e-3, epe(out[0], ref)
+
+
+def test_dataparallel_wrapper_and_state_dict_roundtrip():
+    model, sd, m = _model_from_manifest("hot_S_gwc.npz")
+    dp = torch.nn.DataParallel(model, device_ids=[0])
+    sd2 = {"module." + k: v for k, v in sd.items()}
+    model_dict = dp.state_dict()
+    model_dict.update({k: v for k, v in sd2.items() if k in model_dict})
+    dp.load_state_dict(model_dict)
+    g = load_golden("hot_S_gwc.npz")
+    with torch.no_grad():
+        out = dp(cu(g["left"]), cu(g["right"]), train_status=False)
+    assert epe(out[0], g["disp_0"]) <= 1e-3
+
+
+def _full_inputs(model, B, H, W, seed):
+    torch.manual_seed(seed)
+    left = torch.randn(B, 3, H, W, device=DEV)
+    right = torch.roll(left, shifts=-5, dims=-1) + 0.05 * torch.randn(B, 3, H, W, device=DEV)
+    with torch.no_grad():
+        return model.prefix(left, right)
+
+
+@pytest.mark.parametrize("var,cv,B,H,W,maxdisp", [("S", "gwc", 1, 384, 1248, 192), ("S", "nc", 2, 384, 1248, 192),
+                                                  ("L", "gwc", 1, 384, 1248, 192), ("M", "gwc", 1, 256, 512, 192)])
+def test_hot_path_full_size_vs_oracle(var, cv, B, H, W, maxdisp):
+    model, sd, m = _model_from_manifest(f"hot_{var}_{cv}.npz", maxdisp=maxdisp)
+    ml, mr, att, up = _full_inputs(model, B, H, W, 11)
+    outs = model.hot_path(ml, mr, att, up, True)
+    with torch.no_grad():
+        ref = O.hot_path({k: v.cpu() for k, v in sd.items()}, m["cv_scale"], maxdisp, cv == "gwc", ml.cpu(), mr.cpu(),
+                         None if att is None else att.cpu(), [u.cpu() for u in up])
+    flips = None
+    if m["cv_scale"] == 4:
+        # oracle vs HIP cost volumes agree to fp32 rounding; compare top-2 sets via the HIP cost
+        cost = model.aggregation_out(model.agg(model.group_stem(E.build_gwc_volume(ml, mr, maxdisp // 4, 32))))
+        flips = (_top2_sets(cost.squeeze(1).cpu()) != _top2_sets(ref["cost"][:, 0])).any(1)
+        print(f"{var}-{cv} top-2 flips: {int(flips.sum())} of {flips.numel()} low-res pixels")
+    for i, o in enumerate(outs):
+        _check_disp(f"{var}{cv}{i}", o, ref[f"disp_{i}"], m, flips)
+
+
+def test_plan_modes_agree_and_probe():
+    model, sd, m = _model_from_manifest("hot_L_gwc.npz")
+    g = load_golden("hot_L_gwc.npz")
+    args = (cu(g["match_left"]), cu(g["match_right"]), None, [cu(g[f"up_{i}"]) for i in range(3)])
+    B, C, h, w = args[0].shape
+    hp_graph = E.HotPath(model, B, h, w, 0, [tuple(u.shape) for u in args[3]], DEV, graph=True)
+    hp_eager = E.HotPath(model, B, h, w, 0, [tuple(u.shape) for u in args[3]], DEV, graph=False)
+    for hp in (hp_graph, hp_eager):
+        hp.load_inputs(*args)
+        hp.set_probe(0, 8)
+        for _ in range(3):
+            hp.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(hp_graph.outputs[0], hp_eager.outputs[0])
+    for hp in (hp_graph, hp_eager):
+        t = hp.probe_read()
+        assert len(t) == 3 and all(v > 0 for v in t), t
+    assert hp_graph.num_ops > 30
+
+
+def test_expected_raises():
+    # reference raises on odd D and on H, W not multiples of 32 (§0.5)
+    for var, cv, H, W, maxdisp in [("S", "gwc", 128, 256, 48), ("L", "gwc", 64, 128, 52), ("S", "gwc", 80, 128, 64)]:
+        model, _, _ = _model_from_manifest(f"hot_{var}_{cv}.npz", maxdisp=maxdisp)
+        left = torch.randn(1, 3, H, W, device=DEV)
+        with pytest.raises(RuntimeError):
+            with torch.no_grad():
+                model(left, left, False)
