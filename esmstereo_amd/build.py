@@ -41,8 +41,13 @@ def _stale(obj: str, src: str) -> bool:
     return any(os.path.getmtime(p) > t for p in [src] + _deps())
 
 
+# kernels whose results must be bit-exact with the reference's separately rounded ops
+NO_CONTRACT = {"volumes.hip", "regression.hip"}
+
+
 def _compile(src: str, obj: str) -> str:
-    cmd = [_hipcc()] + CXXFLAGS + ["-c", src, "-o", obj]
+    extra = ["-ffp-contract=off"] if os.path.basename(src) in NO_CONTRACT else []
+    cmd = [_hipcc()] + CXXFLAGS + extra + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")

@@ -20,7 +20,10 @@ namespace {
 thread_local std::string g_error;
 }
 
-void set_error(const std::string& msg) { g_error = msg; }
+void set_error(const std::string& msg) {
+    g_error = msg;
+    (void)hipGetLastError();  // never leave a sticky HIP error behind for the caller's runtime
+}
 
 }  // namespace esm
 
@@ -71,6 +74,41 @@ int run_op(const Op& op, hipStream_t s) {
     }
 }
 
+// Nodes the next op captured on `s` will depend on (the last captured kernel node(s)).
+std::vector<hipGraphNode_t> capture_frontier(hipStream_t s) {
+    hipStreamCaptureStatus st;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t n = 0;
+    if (hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &n) != hipSuccess || !deps) return {};
+    return std::vector<hipGraphNode_t>(deps, deps + n);
+}
+
+std::vector<hipGraphNode_t> successors(const std::vector<hipGraphNode_t>& nodes) {
+    std::vector<hipGraphNode_t> out;
+    for (auto nd : nodes) {
+        size_t n = 0;
+        if (hipGraphNodeGetDependentNodes(nd, nullptr, &n) != hipSuccess || n == 0) continue;
+        std::vector<hipGraphNode_t> v(n);
+        hipGraphNodeGetDependentNodes(nd, v.data(), &n);
+        for (auto x : v) {
+            bool seen = false;
+            for (auto y : out) seen = seen || (x == y);
+            if (!seen) out.push_back(x);
+        }
+    }
+    return out;
+}
+
+std::vector<hipGraphNode_t> graph_roots(hipGraph_t g) {
+    size_t n = 0;
+    hipGraphGetRootNodes(g, nullptr, &n);
+    std::vector<hipGraphNode_t> v(n);
+    if (n) hipGraphGetRootNodes(g, v.data(), &n);
+    return v;
+}
+
 }  // namespace
 
 struct esm_plan {
@@ -107,17 +145,25 @@ struct esm_plan {
         if (cap_stream) hipStreamDestroy(cap_stream);
     }
     // Launch every op on s; when `slot` >= 0 record the probe pair `slot` around the probed op.
-    int launch_all(hipStream_t s, int slot) {
+    // Under stream capture the records become event-record graph nodes (hipEventRecordExternal).
+    int launch_all(hipStream_t s, int slot, bool capture = false) {
+        const unsigned flags = capture ? hipEventRecordExternal : 0u;
         for (int i = 0; i < static_cast<int>(ops.size()); ++i) {
-            if (i == probe_index && slot >= 0 && hipEventRecord(ev0[slot], s) != hipSuccess) {
-                esm::set_error("plan: hipEventRecord failed");
-                return ESM_ERR_RUNTIME;
+            if (i == probe_index && slot >= 0) {
+                const hipError_t e = hipEventRecordWithFlags(ev0[slot], s, flags);
+                if (e != hipSuccess) {
+                    esm::set_error(std::string("plan: hipEventRecord failed: ") + hipGetErrorString(e));
+                    return ESM_ERR_RUNTIME;
+                }
             }
             const int rc = run_op(ops[i], s);
             if (rc != ESM_OK) return rc;
-            if (i == probe_index && slot >= 0 && hipEventRecord(ev1[slot], s) != hipSuccess) {
-                esm::set_error("plan: hipEventRecord failed");
-                return ESM_ERR_RUNTIME;
+            if (i == probe_index && slot >= 0) {
+                const hipError_t e = hipEventRecordWithFlags(ev1[slot], s, flags);
+                if (e != hipSuccess) {
+                    esm::set_error(std::string("plan: hipEventRecord failed: ") + hipGetErrorString(e));
+                    return ESM_ERR_RUNTIME;
+                }
             }
         }
         return ESM_OK;
@@ -229,7 +275,15 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
         esm::set_error("plan: hipStreamBeginCapture failed");
         return ESM_ERR_RUNTIME;
     }
-    const int rc = plan->launch_all(plan->cap_stream, plan->probe_index >= 0 ? 0 : -1);
+    // Capture the launch list; around the probed op remember the capture frontier so the
+    // event-record nodes can be spliced in after capture (records inside capture are refused).
+    std::vector<hipGraphNode_t> before, after;
+    int rc = ESM_OK;
+    for (int i = 0; i < static_cast<int>(plan->ops.size()) && rc == ESM_OK; ++i) {
+        if (i == plan->probe_index) before = capture_frontier(plan->cap_stream);
+        rc = run_op(plan->ops[i], plan->cap_stream);
+        if (i == plan->probe_index) after = capture_frontier(plan->cap_stream);
+    }
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(plan->cap_stream, &g);
     if (rc != ESM_OK) {
@@ -241,22 +295,21 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
         return ESM_ERR_RUNTIME;
     }
     plan->graph = g;
-    if (plan->probe_index >= 0) {  // locate the two captured event-record nodes
-        size_t n = 0;
-        hipGraphGetNodes(g, nullptr, &n);
-        std::vector<hipGraphNode_t> nodes(n);
-        hipGraphGetNodes(g, nodes.data(), &n);
-        for (auto nd : nodes) {
-            hipGraphNodeType t;
-            if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeEventRecord) continue;
-            hipEvent_t e = nullptr;
-            hipGraphEventRecordNodeGetEvent(nd, &e);
-            if (e == plan->ev0[0]) plan->node0 = nd;
-            if (e == plan->ev1[0]) plan->node1 = nd;
-        }
-        if (!plan->node0 || !plan->node1) {
+    if (plan->probe_index >= 0) {
+        if (after.empty()) {
             plan->clear_graph();
-            esm::set_error("plan: probe events were not captured as graph nodes");
+            esm::set_error("plan: could not locate the probed op in the captured graph");
+            return ESM_ERR_UNSUPPORTED;
+        }
+        const std::vector<hipGraphNode_t> first = before.empty() ? graph_roots(g) : successors(before);
+        const std::vector<hipGraphNode_t> next = successors(after);
+        hipError_t e = hipGraphAddEventRecordNode(&plan->node0, g, before.data(), before.size(), plan->ev0[0]);
+        for (size_t k = 0; e == hipSuccess && k < first.size(); ++k) e = hipGraphAddDependencies(g, &plan->node0, &first[k], 1);
+        if (e == hipSuccess) e = hipGraphAddEventRecordNode(&plan->node1, g, after.data(), after.size(), plan->ev1[0]);
+        for (size_t k = 0; e == hipSuccess && k < next.size(); ++k) e = hipGraphAddDependencies(g, &plan->node1, &next[k], 1);
+        if (e != hipSuccess) {
+            plan->clear_graph();
+            esm::set_error(std::string("plan: cannot add probe event nodes: ") + hipGetErrorString(e));
             return ESM_ERR_UNSUPPORTED;
         }
     }

@@ -8,6 +8,9 @@
 //                        first on ties), softmax over the pair, sum of index*prob.
 #include "common.h"
 
+// products rounded, then summed (torch.sum(x * arange)): no FMA contraction
+#pragma clang fp contract(off)
+
 namespace esm {
 namespace {
 
@@ -21,7 +24,7 @@ __global__ void __launch_bounds__(kThreads) dispreg_kernel(const float* __restri
     const int p = i - b * HW;
     const float* c = cost + static_cast<long long>(b) * D * HW + p;
     float acc = 0.f;
-    for (int d = 0; d < D; ++d) acc = __fadd_rn(acc, __fmul_rn(c[static_cast<long long>(d) * HW], static_cast<float>(d)));
+    for (int d = 0; d < D; ++d) acc = acc + c[static_cast<long long>(d) * HW] * static_cast<float>(d);
     out[i] = acc;
 }
 
@@ -55,7 +58,7 @@ __global__ void __launch_bounds__(kThreads) topk2_kernel(const float* __restrict
     // disparity_samples gathered at the two indices (NULL samples = arange(D), as ESMStereo.py:719-720)
     const float d0 = samples ? samples[base + static_cast<long long>(i0) * HW] : static_cast<float>(i0);
     const float d1 = samples ? samples[base + static_cast<long long>(i1) * HW] : static_cast<float>(i1);
-    out[i] = __fadd_rn(__fmul_rn(d0, p0), __fmul_rn(d1, p1));
+    out[i] = d0 * p0 + d1 * p1;
 }
 
 }  // namespace

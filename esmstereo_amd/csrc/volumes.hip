@@ -10,16 +10,19 @@
 // plane (x >= d keeps it in row y).  So a workgroup owns a flat pixel tile [p0, p0+1024) of
 // one (b,g): it keeps its left values in registers, stages the right segment
 // [p0-D+1, p0+1024) once in LDS, and streams D planes of float4 stores (one 1 KiB
-// coalesced store per wave-instruction).  Products and the pairwise mean are computed with
-// explicit _rn intrinsics (no FMA contraction), so the gwc/concat results are bit-exact
-// with the reference's `(a*b).mean()`.
+// coalesced store per wave-instruction).  Products and the pairwise mean are rounded one
+// operation at a time (FMA contraction off for this file), so the gwc/concat results are
+// bit-exact with the reference's `(a*b).mean()`.
 #include "common.h"
+
+// The reference rounds every product and every sum separately; never fuse them into FMAs.
+#pragma clang fp contract(off)
 
 namespace esm {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPix = 4;                        // pixels per thread
+constexpr int kPix = 4;                       // pixels per thread
 constexpr int kTile = kThreads * kPix;         // flat pixels per workgroup
 constexpr int kDChunk = 8;                     // disparity planes per workgroup
 
@@ -68,11 +71,11 @@ __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__
 #pragma unroll
         for (int k = 0; k < kPix; ++k) {
             const int li = (pt + k - d) - lo;
-            float s = __fmul_rn(lv[0][k], rs[0][li]);
+            float s = lv[0][k] * rs[0][li];
 #pragma unroll
-            for (int c = 1; c < CPG; ++c) s = __fadd_rn(s, __fmul_rn(lv[c][k], rs[c][li]));
-            float v = __fmul_rn(s, inv);
-            if (ATT) v = __fmul_rn(v, av[k]);
+            for (int c = 1; c < CPG; ++c) s = s + lv[c][k] * rs[c][li];
+            float v = s * inv;
+            if (ATT) v = v * av[k];
             o[k] = (xs[k] >= d) ? v : 0.f;
         }
         float* dst = vb + static_cast<long long>(dd) * HW;
@@ -155,9 +158,9 @@ __global__ void __launch_bounds__(kThreads) l2norm_kernel(const float* __restric
     float ss = 0.f;
     for (int c = 0; c < C; ++c) {
         const float v = xb[static_cast<long long>(c) * HW];
-        ss = __fadd_rn(ss, __fmul_rn(v, v));
+        ss = ss + v * v;
     }
-    const float n = __fadd_rn(sqrtf(ss), 1e-05f);
+    const float n = sqrtf(ss) + 1e-05f;
     for (int c = 0; c < C; ++c) yb[static_cast<long long>(c) * HW] = xb[static_cast<long long>(c) * HW] / n;
 }
 
@@ -202,7 +205,7 @@ __global__ void __launch_bounds__(kThreads) normcorr_kernel(const float* __restr
                 if (k < dn) {
                     const int d = d0 + k;
                     const int j = p - d - lo;
-                    acc[k] = __fadd_rn(acc[k], __fmul_rn(lv, rs[cc][j]));
+                    acc[k] = acc[k] + lv * rs[cc][j];
                 }
             }
         }

@@ -40,6 +40,17 @@ def require_device(t: torch.Tensor, what: str) -> None:
         raise ValueError(f"{what}: innermost dimension must be contiguous")
 
 
+def require_on(dev: torch.device, what: str, *ts: Optional[torch.Tensor]) -> None:
+    """Every pointer a kernel dereferences must live on the launch device (a host or
+    other-device pointer would fault the GPU, so this is checked on the host first)."""
+    for t in ts:
+        if t is None:
+            continue
+        if t.device != dev or t.dtype != torch.float32:
+            raise RuntimeError(f"{what}: tensor on {t.device} ({t.dtype}); expected float32 on {dev} "
+                               "(move the module to the input's device)")
+
+
 # ----------------------------------------------------------------------------- packing
 
 
@@ -279,6 +290,7 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
         cin += int(s.shape[1])
     if cin != pc.cin:
         raise RuntimeError(f"conv: input has {cin} channels, layer expects {pc.cin}")
+    require_on(x0.device, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2)
     d.nsrc = len(srcs)
     d.B, d.Cin = B, cin
     d.Di, d.Hi, d.Wi = Di, Hi, Wi
@@ -313,6 +325,7 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
         else:
             out = ctx.empty(B, pc.cout, Do, Ho, Wo) if nd == 3 else ctx.empty(B, pc.cout, Ho, Wo)
     require_device(out, "conv output")
+    require_on(x0.device, "conv output", out)
     ost = out.stride()
     d.out = out.data_ptr()
     d.ob, d.oc = ost[0], ost[1]
@@ -390,6 +403,8 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
         d.dw_k = int(dw[0].shape[-1])
     if len(stages) > _lib.SMIX_MAX_STAGES:
         raise ValueError("smix: at most 2 stages per launch")
+    require_on(x.device, "smix", x, out, res, *(dw or ()),
+               *[t for st in stages for t in (st.ln_w, st.fc0_w, st.fc0_b, st.fc2_w, st.fc2_b)])
     d.nstages = len(stages)
     for i, st in enumerate(stages):
         d.stage[i].ln_w = st.ln_w.data_ptr()

@@ -36,7 +36,7 @@ def gwc_volume(L: torch.Tensor, R: torch.Tensor, D: int, G: int) -> torch.Tensor
     B, C, H, W = L.shape
     assert C % G == 0
     V = L.new_zeros(B, G, D, H, W)
-    for d in range(D):
+    for d in range(min(D, W)):  # planes d >= W stay zero (the reference slices are empty there)
         prod = L[..., d:] * R[..., : W - d]
         V[:, :, d, :, d:] = prod.view(B, G, C // G, H, W - d).mean(dim=2)
     return V
@@ -47,7 +47,7 @@ def concat_volume(L: torch.Tensor, R: torch.Tensor, D: int) -> torch.Tensor:
     B, C, H, W = L.shape
     V = L.new_zeros(B, 2 * C, D, H, W)
     V[:, :C] = L.unsqueeze(2)
-    for d in range(D):
+    for d in range(min(D, W)):
         V[:, C:, d, :, d:] = R[..., : W - d]
     return V
 
@@ -58,7 +58,7 @@ def normcorr_volume(L: torch.Tensor, R: torch.Tensor, D: int) -> torch.Tensor:
     Ln = L / (torch.norm(L, 2, 1, True) + 1e-05)
     Rn = R / (torch.norm(R, 2, 1, True) + 1e-05)
     V = L.new_zeros(B, 1, D, H, W)
-    for d in range(D):
+    for d in range(min(D, W)):
         V[:, :, d, :, d:] = torch.mean(Ln[..., d:] * Rn[..., : W - d], dim=1, keepdim=True)
     return V
 

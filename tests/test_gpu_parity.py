@@ -11,6 +11,7 @@ Tolerances (fp32 everywhere; north_star: "EPE within 1e-3 of the PyTorch referen
   the count of low-res pixels whose top-2 index set flips is reported, and EPE <= 1e-3 is
   required outside the dilated, upsampled flip mask.
 """
+import copy
 import json
 import os
 
@@ -121,6 +122,13 @@ def _ref_conv(x_list, conv, bn, act, mul=None, res=None, up=None, up_f=0, shuffl
     return (y * post).float()
 
 
+def pk(conv, bn, act):
+    """Pack a CPU-built layer after moving a copy to the GPU (kernels read device weights)."""
+    conv = copy.deepcopy(conv).to(DEV)
+    bn = copy.deepcopy(bn).to(DEV) if bn is not None else None
+    return pack_conv(conv, bn, act)
+
+
 def _mk(nd, cin, cout, k, s, p, transposed=False, bias=False, bn=True, seed=0):
     torch.manual_seed(seed)
     cls = {(2, False): torch.nn.Conv2d, (3, False): torch.nn.Conv3d, (2, True): torch.nn.ConvTranspose2d,
@@ -145,7 +153,7 @@ CONV2D = [(1, 32, 5, 1, 1), (16, 16, 3, 1, 1), (16, 16, 3, 2, 1), (56, 16, 1, 1,
 def test_conv2d(cin, cout, k, s, p, act):
     conv, bn = _mk(2, cin, cout, k, s, p)
     x = torch.randn(2, cin, 23, 37)
-    y = run_conv(Ctx(DEV), pack_conv(conv, bn, act), [x.to(DEV)])
+    y = run_conv(Ctx(DEV), pk(conv, bn, act), [x.to(DEV)])
     assert rel(y, _ref_conv([x], conv, bn, act)) < 1e-5
 
 
@@ -157,7 +165,7 @@ CONV3D = [(32, 8, 3, 1, 1), (8, 8, 3, 1, 1), (8, 24, 3, 2, 1), (24, 24, 3, 1, 1)
 def test_conv3d(cin, cout, k, s, p):
     conv, bn = _mk(3, cin, cout, k, s, p, seed=1)
     x = torch.randn(1, cin, 6, 9, 21)
-    y = run_conv(Ctx(DEV), pack_conv(conv, bn, ACT_GELU), [x.to(DEV)])
+    y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)])
     assert rel(y, _ref_conv([x], conv, bn, ACT_GELU)) < 1e-5
 
 
@@ -168,7 +176,7 @@ def test_conv_transposed(nd, cin, cout, bn):
     shape = (2, cin, 5, 11, 13) if nd == 3 else (2, cin, 11, 19)
     x = torch.randn(*shape)
     act = ACT_GELU if bn else ACT_NONE
-    y = run_conv(Ctx(DEV), pack_conv(conv, b, act), [x.to(DEV)])
+    y = run_conv(Ctx(DEV), pk(conv, b, act), [x.to(DEV)])
     assert rel(y, _ref_conv([x], conv, b, act)) < 1e-5
 
 
@@ -179,21 +187,21 @@ def test_conv_multisource_crop_and_epilogues():
     a = torch.randn(1, 16, 24, 39)
     c = torch.randn(1, 24, 24, 39)
     crop = big.to(DEV)[:, :, :24, :39]
-    y = run_conv(Ctx(DEV), pack_conv(conv, bn, ACT_GELU), [crop, a.to(DEV), c.to(DEV)])
+    y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [crop, a.to(DEV), c.to(DEV)])
     assert rel(y, _ref_conv([big[:, :, :24, :39], a, c], conv, bn, ACT_GELU)) < 1e-5
     # residual + mul (att broadcast over depth) on a 3-D conv
     conv3, bn3 = _mk(3, 1, 8, 3, 1, 1, seed=4)
     x3 = torch.randn(2, 1, 4, 6, 10)
     att = torch.randn(2, 8, 6, 10)
     res3 = torch.randn(2, 8, 4, 6, 10)
-    y3 = run_conv(Ctx(DEV), pack_conv(conv3, bn3, ACT_GELU), [x3.to(DEV)], mul=att.to(DEV), res=res3.to(DEV))
+    y3 = run_conv(Ctx(DEV), pk(conv3, bn3, ACT_GELU), [x3.to(DEV)], mul=att.to(DEV), res=res3.to(DEV))
     assert rel(y3, _ref_conv([x3], conv3, bn3, ACT_GELU, mul=att, res=res3)) < 1e-5
     # ConvT 16->1 + bilinear(prev, x4) + x4 scale with an unscaled copy
     ct, _ = _mk(2, 16, 1, 4, 2, 1, transposed=True, bn=False, seed=5)
     xt = torch.randn(1, 16, 24, 40)
     prev = torch.randn(1, 1, 12, 20)
     cp = torch.empty(1, 1, 48, 80, device=DEV)
-    yt = run_conv(Ctx(DEV), pack_conv(ct, None, ACT_NONE), [xt.to(DEV)], up=prev.to(DEV), up_f=4, post_scale=4.0,
+    yt = run_conv(Ctx(DEV), pk(ct, None, ACT_NONE), [xt.to(DEV)], up=prev.to(DEV), up_f=4, post_scale=4.0,
                   out2=cp, post_scale2=1.0)
     ref = _ref_conv([xt], ct, None, ACT_NONE, up=prev, up_f=4)
     assert rel(yt, ref * 4) < 1e-5
@@ -201,7 +209,7 @@ def test_conv_multisource_crop_and_epilogues():
     # 1x1 conv + PixelShuffle(4) + SiLU
     cs, _ = _mk(2, 8, 128, 1, 1, 0, bias=True, bn=False, seed=6)
     xs = torch.randn(1, 8, 6, 20)
-    ys = run_conv(Ctx(DEV), pack_conv(cs, None, ACT_SILU), [xs.to(DEV)], shuffle=4)
+    ys = run_conv(Ctx(DEV), pk(cs, None, ACT_SILU), [xs.to(DEV)], shuffle=4)
     assert rel(ys, _ref_conv([xs], cs, None, ACT_SILU, shuffle=4)) < 1e-5
 
 
