@@ -31,7 +31,7 @@ def _hipcc() -> str:
 
 
 def _deps():
-    return [os.path.join(CSRC, "common.h"), HEADER]
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [HEADER]
 
 
 def _stale(obj: str, src: str) -> bool:

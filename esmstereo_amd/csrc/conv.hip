@@ -1,0 +1,55 @@
+// esm_conv_f32: descriptor validation (host side, before anything touches the GPU) and
+// dispatch to the 2-D / 3-D implicit-GEMM instantiations (conv2d.hip, conv3d.hip).
+#include "common.h"
+
+namespace esm {
+
+int launch_conv2d(const esm_conv_desc& a, hipStream_t s);
+int launch_conv3d(const esm_conv_desc& a, hipStream_t s);
+
+int launch_conv(const esm_conv_desc* d, hipStream_t s) {
+    if (!d) return arg_error("conv: null descriptor");
+    const esm_conv_desc& a = *d;
+    if (!a.w || !a.out) return arg_error("conv: null weights/output");
+    if (a.nsrc < 1 || a.nsrc > ESM_MAX_SRC) return arg_error("conv: nsrc must be 1..3");
+    int cin = 0;
+    for (int i = 0; i < ESM_MAX_SRC; ++i) {
+        if (i < a.nsrc) {
+            if (!a.src[i].ptr || a.src[i].C <= 0) return arg_error("conv: bad source");
+            cin += a.src[i].C;
+        } else if (a.src[i].C != 0) {
+            return arg_error("conv: unused source slots must have C = 0");
+        }
+    }
+    if (cin != a.Cin) return arg_error("conv: Cin != sum of source channels");
+    if (a.B <= 0 || a.Cout <= 0) return arg_error("conv: bad B/Cout");
+    if (a.cin_pad % 16 || a.cin_pad < a.Cin) return arg_error("conv: cin_pad must be a multiple of 16 >= Cin");
+    if (a.cout_pad % 32 || a.cout_pad < a.Cout) return arg_error("conv: cout_pad must be a multiple of 32 >= Cout");
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    if (a.kh != a.kw) return arg_error("conv: kh must equal kw");
+    if (d3 && a.kd != a.kh) return arg_error("conv: 3-D kernels must be cubic");
+    if (!d3 && (a.Di != 1 || a.Do != 1)) return arg_error("conv: 2-D conv needs Di = Do = 1");
+    if (a.shuffle > 1 && (d3 || a.transposed)) return arg_error("conv: pixel shuffle only for 2-D convs");
+    if (a.up && (a.Cout != 1 || d3 || a.up_f <= 0)) return arg_error("conv: bilinear add needs 2-D, Cout == 1");
+    if (a.Hi <= 0 || a.Wi <= 0 || a.Di <= 0) return arg_error("conv: empty input");
+    if (a.transposed) {
+        if (a.kh != 4 || a.stride != 2 || a.ph != 1 || a.pw != 1 || (d3 && a.pd != 1))
+            return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
+        if (a.Ho != 2 * a.Hi || a.Wo != 2 * a.Wi || (d3 && a.Do != 2 * a.Di))
+            return arg_error("conv: transposed output extent must be 2x the input");
+        return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
+    }
+    const int S = a.stride;
+    if (S != 1 && S != 2) return arg_error("conv: stride must be 1 or 2");
+    if (a.Ho != (a.Hi + 2 * a.ph - a.kh) / S + 1 || a.Wo != (a.Wi + 2 * a.pw - a.kw) / S + 1 ||
+        (d3 && a.Do != (a.Di + 2 * a.pd - a.kd) / S + 1))
+        return arg_error("conv: output extent inconsistent with kernel/stride/padding");
+    if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
+    return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
+}
+
+}  // namespace esm
+
+extern "C" int esm_conv_f32(const esm_conv_desc* desc, void* stream) {
+    return esm::launch_conv(desc, esm::as_stream(stream));
+}

@@ -89,14 +89,14 @@ def pack_weight(W: torch.Tensor, transposed: bool) -> Tuple[torch.Tensor, int, i
     if not transposed:
         cout, cin = W.shape[:2]
         taps = int(W[0, 0].numel())
-        cin_pad, cout_pad = _rup(cin, 4), _rup(cout, 32)
+        cin_pad, cout_pad = _rup(cin, 16), _rup(cout, 32)
         P = W.new_zeros(taps, cin_pad, cout_pad)
         P[:, :cin, :cout] = W.reshape(cout, cin, taps).permute(2, 1, 0)
         return P.contiguous(), cin_pad, cout_pad
     cin, cout = W.shape[:2]
     if any(s != 4 for s in W.shape[2:]):
         raise ValueError("transposed conv: only kernel 4 is supported")
-    cin_pad, cout_pad = _rup(cin, 4), _rup(cout, 32)
+    cin_pad, cout_pad = _rup(cin, 16), _rup(cout, 32)
     n = 2 ** nd
     P = W.new_zeros(n, n, cin_pad, cout_pad)
     for cls in range(n):

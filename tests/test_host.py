@@ -86,7 +86,7 @@ def test_pack_conv3d_indexing(k, s, p):
     x = torch.randn(2, 5, 4, 5, 6, generator=g)
     conv = torch.nn.Conv3d(5, 7, k, s, p, bias=False)
     P, cin_pad, cout_pad = pack_weight(conv.weight, False)
-    assert P.shape == (k ** 3, 8, 32)
+    assert P.shape == (k ** 3, 16, 32)
     ref = F.conv3d(x.double(), conv.weight.double(), None, s, p)
     got = _emulate_packed(x, P, False, k, s, p)[:, :7]
     assert torch.allclose(got, ref, atol=1e-9)
@@ -97,7 +97,7 @@ def test_pack_convtranspose3d_parity_classes():
     x = torch.randn(1, 6, 3, 4, 5, generator=g)
     conv = torch.nn.ConvTranspose3d(6, 3, 4, 2, 1, bias=False)
     P, _, _ = pack_weight(conv.weight, True)
-    assert P.shape == (8, 8, 8, 32)
+    assert P.shape == (8, 8, 16, 32)
     ref = F.conv_transpose3d(x.double(), conv.weight.double(), None, 2, 1)
     got = _emulate_packed(x, P, True, 4, 2, 1)[:, :3]
     assert torch.allclose(got, ref, atol=1e-9)
