@@ -11,13 +11,18 @@
 //            B = 4 k x 16 pixels  (lane l: k l>>4, pixel l&15) from the LDS input patch,
 //            C = 16 couts x 16 px, row (cout) = (l>>4)*4 + j, col (pixel) = l&15, so every
 //            store instruction writes 16 consecutive output pixels per cout.
+// C1 path    single-output-channel layers (tail convs, the refinement heads) would use
+//            1/16 of an MFMA tile; they run as a VALU dot product instead, one output pixel
+//            per lane, weights broadcast from LDS.
 // Tiling     a 256-thread workgroup (4 waves) owns a TH=4 x TW=16*NT output tile of one
 //            (batch, depth) plane and 16*MT couts; wave w computes output row w of the tile.
-//            Per input-channel chunk of CC channels the workgroup stages (a) the input patch
-//            the tile needs (all taps; zero-padded borders) and (b) the weight slab
-//            [tap][CC][16*MT] in LDS with all loads in flight at once, then runs the
-//            TAPS x CC/4 MFMA steps fully unrolled from LDS: one global round trip per
-//            chunk instead of one per K-step.
+// Staging    per input-channel chunk of CC channels the workgroup needs (a) the input patch
+//            of the tile (all taps, zero-padded borders) and (b) the weight slab
+//            [tap][CC][16*MT].  Every thread issues its share of both as one batch of
+//            independent loads into registers (fully unrolled, compile-time counts), and the
+//            batch for chunk c+1 is issued before the MFMAs of chunk c, so global latency
+//            overlaps compute; the MFMA loop over TAPS x CC/4 k-steps is fully unrolled and
+//            reads its operands from LDS.
 // LDS banks  channel planes are padded so lanes 0-15 (k=0) and 16-31 (k=1) of a ds_read_b32
 //            hit disjoint banks: plane = 16 (mod 32) at unit pixel stride, odd at stride 2;
 //            the 32-wide weight row is padded to 48 floats for the same reason.
@@ -26,7 +31,8 @@
 //            1 - q + 2t for output 2m + q), so the gather is dense.
 // Fusions    multi-source K (torch.cat along channels, crops = smaller logical extent than
 //            the source), BN scale/shift, GELU / SiLU / ReLU, broadcast multiply (`* att`),
-//            residual add, bilinear-upsample-and-add, final scales, PixelShuffle remap.
+//            residual add, bilinear-upsample-and-add, final scales, PixelShuffle remap (with
+//            one 16-byte store per lane for r = 4).
 #pragma once
 
 #include "common.h"
@@ -45,7 +51,7 @@ constexpr int pad_plane(int raw, bool stride2) {
     return (up - 16 >= raw) ? up - 16 : up + 16;
 }
 
-template <bool D3, int K, int S, bool TR, int MT, int NT, int CC>
+template <bool D3, int K, int S, bool TR, int MT, int NT, int CC, bool C1>
 struct Cfg {
     static constexpr int TW = 16 * NT;
     static constexpr int KT = TR ? 2 : K;
@@ -57,18 +63,24 @@ struct Cfg {
     static constexpr int PC = TR ? TW + 1 : (TW - 1) * S + K;
     static constexpr int RAW = PZ * PR * PC;
     static constexpr int PLANE = pad_plane(RAW, S == 2 && !TR);
-    static constexpr int CO = 16 * MT;
-    static constexpr int WROW = MT == 1 ? 16 : 48;
+    static constexpr int CO = C1 ? 4 : 16 * MT;       // couts staged per workgroup (C1: 1 used)
+    static constexpr int WROW = C1 ? 4 : (MT == 1 ? 16 : 48);
     static constexpr int XS = CC * PLANE;
     static constexpr int WS = TAPS * CC * WROW;
+    // patch staging walks [CC][RAW64]: RAW64 = RAW rounded up to 64 so each wave-instruction stays
+    // inside one channel (channel -> source selection is then wave-uniform, scalar)
+    static constexpr int RAW64 = (RAW + 63) / 64 * 64;
+    static constexpr int NX = (CC * RAW64 + kThreads - 1) / kThreads;         // patch loads / thread
+    static constexpr int NW = (TAPS * CC * CO / 4 + kThreads - 1) / kThreads;  // float4 weight loads / thread
     static_assert((XS + WS) * 4 <= 64 * 1024, "conv tile exceeds the 64 KiB LDS budget (2 workgroups/CU)");
+    static_assert(!C1 || NT == 4, "C1 path maps one output pixel per lane (TW = 64)");
 };
 
-template <bool D3, int K, int S, bool TR, int MT, int NT, int CC>
+template <bool D3, int K, int S, bool TR, int MT, int NT, int CC, bool C1>
 __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
-    using C = Cfg<D3, K, S, TR, MT, NT, CC>;
+    using C = Cfg<D3, K, S, TR, MT, NT, CC, C1>;
+    __shared__ __attribute__((aligned(16))) float wl[C::WS];
     __shared__ float xs[C::XS];
-    __shared__ float wl[C::WS];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -87,7 +99,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     const int b = blockIdx.y / Ds;
     const int zs = blockIdx.y - b * Ds;
     const int cls = TR ? static_cast<int>(blockIdx.z % C::NCLS) : 0;
-    const int cob = static_cast<int>(TR ? blockIdx.z / C::NCLS : blockIdx.z) * C::CO;
+    const int cob = static_cast<int>(TR ? blockIdx.z / C::NCLS : blockIdx.z) * (C1 ? 1 : C::CO);
     const int qd = (TR && D3) ? (cls >> 2) & 1 : 0;
     const int qh = TR ? (cls >> 1) & 1 : 0;
     const int qw = TR ? cls & 1 : 0;
@@ -97,84 +109,130 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     const int ro = TR ? y0 + qh - 1 : y0 * S - a.ph;
     const int xo = TR ? x0 + qw - 1 : x0 * S - a.pw;
 
+    const long long wcls = static_cast<long long>(cls) * C::TAPS * a.cin_pad * a.cout_pad;
+    const int c_src0 = a.src[0].C;
+    const int c_src1 = a.src[1].C;
+
+    float rx[C::NX];
+    floatx4 rw[C::NW];
+
+    // ---- issue the global loads of one chunk into registers (all independent, in flight together)
+    auto load_chunk = [&](int c0) {
+#pragma unroll
+        for (int k = 0; k < C::NX; ++k) {
+            const int i = tid + k * kThreads;
+            // channel of this wave-instruction: uniform by construction (RAW64 % 64 == 0)
+            const int c = __builtin_amdgcn_readfirstlane(i / C::RAW64);
+            const int e = i - c * C::RAW64;
+            const int z = e / (C::PR * C::PC);
+            const int rem = e - z * (C::PR * C::PC);
+            const int r = rem / C::PC;
+            const int col = rem - r * C::PC;
+            const int cg = c0 + c;
+            const int id = zo + z, ih = ro + r, iw = xo + col;
+            const bool ok = c < CC && e < C::RAW && cg < a.Cin && ih >= 0 && ih < a.Hi && iw >= 0 &&
+                            iw < a.Wi && (!D3 || (id >= 0 && id < a.Di));
+            // scalar source selection and 64-bit base; per-lane 32-bit offset
+            const float* base;
+            long long sd_, sh_;
+            if (cg < c_src0) {
+                base = a.src[0].ptr + b * a.src[0].sb + cg * a.src[0].sc;
+                sd_ = a.src[0].sd;
+                sh_ = a.src[0].sh;
+            } else if (cg - c_src0 < c_src1) {
+                base = a.src[1].ptr + b * a.src[1].sb + (cg - c_src0) * a.src[1].sc;
+                sd_ = a.src[1].sd;
+                sh_ = a.src[1].sh;
+            } else {
+                base = a.src[2].ptr + b * a.src[2].sb + (cg - c_src0 - c_src1) * a.src[2].sc;
+                sd_ = a.src[2].sd;
+                sh_ = a.src[2].sh;
+            }
+            if (cg >= a.Cin) base = a.src[0].ptr;  // past Cin: every lane masked, keep the address valid
+            const int off = ok ? static_cast<int>((D3 ? id * sd_ : 0) + ih * sh_) + iw : 0;
+            const float v = base[off];
+            rx[k] = ok ? v : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < C::NW; ++k) {
+            const int i = tid + k * kThreads;  // float4 index into [tap][CC][CO/4]
+            const int tap = i / (CC * C::CO / 4);
+            const int rem = i - tap * (CC * C::CO / 4);
+            const int c = rem / (C::CO / 4);
+            const int q4 = rem - c * (C::CO / 4);
+            const bool ok = i < C::TAPS * CC * C::CO / 4;
+            const long long g = ok ? wcls + (static_cast<long long>(tap) * a.cin_pad + c0 + c) * a.cout_pad +
+                                         (cob & ~3) + 4 * q4
+                                   : 0;
+            rw[k] = *reinterpret_cast<const floatx4*>(a.w + g);
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int k = 0; k < C::NX; ++k) {
+            const int i = tid + k * kThreads;
+            const int c = i / C::RAW64;
+            const int e = i - c * C::RAW64;
+            if (c < CC && e < C::RAW) xs[c * C::PLANE + e] = rx[k];
+        }
+#pragma unroll
+        for (int k = 0; k < C::NW; ++k) {
+            const int i = tid + k * kThreads;
+            if (i < C::TAPS * CC * C::CO / 4) {
+                const int row = i / (C::CO / 4);  // tap*CC + c
+                const int q4 = i - row * (C::CO / 4);
+                *reinterpret_cast<floatx4*>(wl + row * C::WROW + 4 * q4) = rw[k];
+            }
+        }
+    };
+
     floatx4 acc[MT][NT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float acc1 = 0.f;  // C1 path
 
-    const long long wcls = static_cast<long long>(cls) * C::TAPS * a.cin_pad * a.cout_pad;
-    const int c_src0 = a.src[0].C;
-    const int c_src1 = a.src[1].C;
-
+    load_chunk(0);
     for (int c0 = 0; c0 < a.Cin; c0 += CC) {
-        __syncthreads();  // the previous chunk's LDS readers are done
-        // ---- stage the input patch (zero outside the tensor / past Cin)
-        for (int i = tid; i < CC * C::RAW; i += kThreads) {
-            const int c = i / C::RAW;
-            int rem = i - c * C::RAW;
-            const int z = rem / (C::PR * C::PC);
-            rem -= z * (C::PR * C::PC);
-            const int r = rem / C::PC;
-            const int col = rem - r * C::PC;
-            const int cg = c0 + c;
-            const int id = zo + z, ih = ro + r, iw = xo + col;
-            float v = 0.f;
-            if (cg < a.Cin && ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi && (!D3 || (id >= 0 && id < a.Di))) {
-                const float* p;
-                long long off;
-                if (cg < c_src0) {
-                    p = a.src[0].ptr;
-                    off = b * a.src[0].sb + cg * a.src[0].sc + (D3 ? id * a.src[0].sd : 0) + ih * a.src[0].sh;
-                } else if (cg - c_src0 < c_src1) {
-                    const int cl = cg - c_src0;
-                    p = a.src[1].ptr;
-                    off = b * a.src[1].sb + cl * a.src[1].sc + (D3 ? id * a.src[1].sd : 0) + ih * a.src[1].sh;
-                } else {
-                    const int cl = cg - c_src0 - c_src1;
-                    p = a.src[2].ptr;
-                    off = b * a.src[2].sb + cl * a.src[2].sc + (D3 ? id * a.src[2].sd : 0) + ih * a.src[2].sh;
-                }
-                v = p[off + iw];
-            }
-            xs[c * C::PLANE + (z * C::PR + r) * C::PC + col] = v;
-        }
-        // ---- stage the weight slab [tap][CC][16*MT]
-        for (int i = tid; i < C::TAPS * CC * C::CO; i += kThreads) {
-            const int tap = i / (CC * C::CO);
-            const int rem = i - tap * (CC * C::CO);
-            const int c = rem / C::CO;
-            const int co = rem - c * C::CO;
-            wl[(tap * CC + c) * C::WROW + co] =
-                a.w[wcls + (static_cast<long long>(tap) * a.cin_pad + c0 + c) * a.cout_pad + cob + co];
-        }
+        __syncthreads();  // every wave is done reading the previous chunk
+        store_chunk();
         __syncthreads();
-        // ---- MFMA over the chunk, fully unrolled, operands from LDS
-#pragma unroll
+        if (c0 + CC < a.Cin) load_chunk(c0 + CC);  // in flight during this chunk's math
+        // taps stay a loop (unrolling them lets the compiler hoist every LDS read and run out of
+        // VGPRs while the next chunk's loads are held in registers); the k-steps inside unroll
+#pragma unroll 1
         for (int tap = 0; tap < C::TAPS; ++tap) {
             const int td = tap / (C::KT * C::KT);
             const int th = (tap / C::KT) % C::KT;
             const int tw = tap % C::KT;
             const int zi = (D3 && TR) ? 1 - td : td;
             const int ri = TR ? wave + 1 - th : wave * S + th;
+            if constexpr (C1) {
+                const int ci = TR ? lane + 1 - tw : lane * S + tw;
 #pragma unroll
-            for (int c4 = 0; c4 < CC / 4; ++c4) {
-                const int c = c4 * 4 + kq;
-                const float* xrow = xs + c * C::PLANE + (zi * C::PR + ri) * C::PC;
-                float bv[NT];
+                for (int c = 0; c < CC; ++c)
+                    acc1 += wl[(tap * CC + c) * C::WROW + (cob & 3)] * xs[c * C::PLANE + (zi * C::PR + ri) * C::PC + ci];
+            } else {
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-                    const int ci = TR ? nt * 16 + n16 + 1 - tw : (nt * 16 + n16) * S + tw;
-                    bv[nt] = xrow[ci];
+                for (int c4 = 0; c4 < CC / 4; ++c4) {
+                    const int c = c4 * 4 + kq;
+                    const float* xrow = xs + c * C::PLANE + (zi * C::PR + ri) * C::PC;
+                    float bv[NT];
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const int ci = TR ? nt * 16 + n16 + 1 - tw : (nt * 16 + n16) * S + tw;
+                        bv[nt] = xrow[ci];
+                    }
+                    float av[MT];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) av[mt] = wl[(tap * CC + c) * C::WROW + mt * 16 + n16];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
                 }
-                float av[MT];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) av[mt] = wl[(tap * CC + c) * C::WROW + mt * 16 + n16];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
             }
         }
     }
@@ -182,40 +240,71 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     // ---------------------------------------------------------------- epilogue
     const int ys = y0 + wave;  // sub-grid / output row of this wave
     if (ys >= Hs) return;
-    const int r = a.shuffle > 1 ? a.shuffle : 1;
     const int oz = TR ? 2 * zs + qd : zs;
     const int oy = TR ? 2 * ys + qh : ys;
+    auto finish = [&](float v, int co, int ox) -> float {
+        const float scl = a.scale ? a.scale[co] : 1.f;
+        const float shf = a.shift ? a.shift[co] : 0.f;
+        v = a.scale ? v * scl + shf : v + shf;
+        v = apply_act(v, a.act);
+        if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + oy * a.mh + ox];
+        if (a.res) v = v + a.res[b * a.rb + co * a.rc + oz * a.rd + oy * a.rh + ox];
+        if (a.up) v = bilinear_at(a.up + b * a.ub, a.up_h, a.up_w, a.uh, a.up_f, oy, ox) + v;
+        return v;
+    };
+    auto put = [&](float v, int co, int ox) {
+        const long long o = b * a.ob + co * a.oc + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox;
+        a.out[o] = v * a.post_scale;
+        if (a.out2) a.out2[o] = v * a.post_scale2;
+    };
+    if constexpr (C1) {
+        const int xsub = x0 + lane;
+        if (xsub < Ws) {
+            const int ox = TR ? 2 * xsub + qw : xsub;
+            put(finish(acc1, cob, ox), cob, ox);
+        }
+        return;
+    } else {
+        const int r = a.shuffle > 1 ? a.shuffle : 1;
+        const bool vec4 = r == 4 && !a.out2 && ((a.ob | a.oc | a.oh) & 3) == 0 &&
+                          (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = cob + mt * 16 + kq * 4 + j;
-            if (co >= a.Cout) continue;
-            const float scl = a.scale ? a.scale[co] : 1.f;
-            const float shf = a.shift ? a.shift[co] : 0.f;
+        for (int mt = 0; mt < MT; ++mt) {
+            const int cq = cob + mt * 16 + kq * 4;  // first of this lane's 4 couts
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 const int xsub = x0 + nt * 16 + n16;
                 if (xsub >= Ws) continue;
                 const int ox = TR ? 2 * xsub + qw : xsub;
-                float v = acc[mt][nt][j];
-                v = a.scale ? v * scl + shf : v + shf;
-                v = apply_act(v, a.act);
-                if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + oy * a.mh + ox];
-                if (a.res) v = v + a.res[b * a.rb + co * a.rc + oz * a.rd + oy * a.rh + ox];
-                if (a.up) v = bilinear_at(a.up + b * a.ub, a.up_h, a.up_w, a.uh, a.up_f, oy, ox) + v;
-                long long o;
-                if (r > 1) {
-                    const int cs = co / (r * r);
-                    const int rem = co - cs * r * r;
-                    const int yy = oy * r + rem / r;
-                    const int xx = ox * r + (rem - (rem / r) * r);
-                    o = b * a.ob + cs * a.oc + static_cast<long long>(yy) * a.oh + xx;
-                } else {
-                    o = b * a.ob + co * a.oc + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox;
+                if (vec4 && cq + 3 < a.Cout) {
+                    // PixelShuffle(4): couts cq..cq+3 are dx = 0..3 of one (channel, dy) -> one 16-B store
+                    float4 v4;
+                    v4.x = finish(acc[mt][nt][0], cq + 0, ox) * a.post_scale;
+                    v4.y = finish(acc[mt][nt][1], cq + 1, ox) * a.post_scale;
+                    v4.z = finish(acc[mt][nt][2], cq + 2, ox) * a.post_scale;
+                    v4.w = finish(acc[mt][nt][3], cq + 3, ox) * a.post_scale;
+                    const int cs = cq / 16, dy = (cq / 4) & 3;
+                    const long long o = b * a.ob + cs * a.oc + static_cast<long long>(oy * 4 + dy) * a.oh + ox * 4;
+                    *reinterpret_cast<float4*>(a.out + o) = v4;
+                    continue;
                 }
-                a.out[o] = v * a.post_scale;
-                if (a.out2) a.out2[o] = v * a.post_scale2;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = cq + j;
+                    if (co >= a.Cout) continue;
+                    const float v = finish(acc[mt][nt][j], co, ox);
+                    if (r > 1) {
+                        const int cs = co / (r * r);
+                        const int rem = co - cs * r * r;
+                        const int yy = oy * r + rem / r;
+                        const int xx = ox * r + (rem - (rem / r) * r);
+                        const long long o = b * a.ob + cs * a.oc + static_cast<long long>(yy) * a.oh + xx;
+                        a.out[o] = v * a.post_scale;
+                        if (a.out2) a.out2[o] = v * a.post_scale2;
+                    } else {
+                        put(v, co, ox);
+                    }
+                }
             }
         }
     }
@@ -230,16 +319,17 @@ constexpr int chunk() {
     return S == 2 ? 8 : 16;
 }
 
-template <bool D3, int K, int S, bool TR, int MT, int NT>
+template <bool D3, int K, int S, bool TR, int MT, int NT, bool C1 = false>
 int launch_nt(const esm_conv_desc& a, hipStream_t s) {
     constexpr int CC = chunk<D3, K, S, TR>();
-    using C = Cfg<D3, K, S, TR, MT, NT, CC>;
+    using C = Cfg<D3, K, S, TR, MT, NT, CC, C1>;
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
     const long long tiles = static_cast<long long>((Ws + C::TW - 1) / C::TW) * ((Hs + kTH - 1) / kTH);
-    dim3 grid(static_cast<unsigned>(tiles), a.B * Ds, ceil_div(a.Cout, C::CO) * C::NCLS);
+    const unsigned zc = C1 ? static_cast<unsigned>(a.Cout) : ceil_div(a.Cout, C::CO);
+    dim3 grid(static_cast<unsigned>(tiles), a.B * Ds, zc * C::NCLS);
     if (tiles > 0x7fffffffLL || grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-    hipLaunchKernelGGL((conv_kernel<D3, K, S, TR, MT, NT, CC>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((conv_kernel<D3, K, S, TR, MT, NT, CC, C1>), grid, dim3(kThreads), 0, s, a);
     return check_launch("conv");
 }
 
@@ -249,6 +339,7 @@ template <bool D3, int K, int S, bool TR>
 int launch_geom(const esm_conv_desc& a, hipStream_t s) {
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
+    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_nt<D3, K, S, TR, 1, 4, true>(a, s);
     const int MT = a.Cout > 16 ? 2 : 1;
     constexpr int NTMAX = (D3 && K == 3 && S == 2) ? 2 : 4;
     int nt = Ws > 32 ? 4 : (Ws > 16 ? 2 : 1);

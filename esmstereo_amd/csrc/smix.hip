@@ -4,9 +4,10 @@
 //              LN = BiasFree_LayerNorm over C (mean IS subtracted) :47-62
 //              SplitPointMlp :23-37, channel shuffle 'b (g d) -> b (d g)', g = 8
 //   [optional] + res                                              (FMBlock `net(x) + x` :130)
-// One thread owns one pixel and keeps its C (8 or 16) channels in registers; the tiny
-// weights are wave-uniform (scalar loads).  With the depthwise conv, a 16x16 pixel tile and
-// its (K-1)/2 halo are staged in LDS once per channel group.
+// One thread owns one pixel and keeps its C (8 or 16) channels in registers.  All weights
+// (<= 1.4K floats) and, with the depthwise conv, the 16x16 pixel tile plus its (K-1)/2 halo
+// are staged in LDS by one batch of loads at kernel start; the math then reads weights as
+// LDS broadcasts (no dependent scalar-load chains).
 #include "common.h"
 
 namespace esm {
@@ -17,7 +18,15 @@ constexpr int kTileW = 16;
 constexpr int kThreads = kTileH * kTileW;
 
 template <int C>
-__device__ __forceinline__ void mix_stage(float (&t)[C], const esm_smix_stage& st) {
+struct SmixLayout {
+    static constexpr int H2 = C / 2;
+    static constexpr int LN = 0, F0W = C, F0B = F0W + C * H2, F2W = F0B + C, F2B = F2W + H2 * C;
+    static constexpr int STAGE = F2B + H2;  // floats per stage
+};
+
+template <int C>
+__device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict__ w) {
+    using Lyt = SmixLayout<C>;
     constexpr int H2 = C / 2;
     constexpr int DD = C / 8;
     float mu = 0.f;
@@ -34,26 +43,26 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const esm_smix_stage& s
     const float den = sqrtf(var + 1e-5f);
     float n[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) / den * st.ln_w[c];
+    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) / den * w[Lyt::LN + c];
     float h[C];
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-        float s = st.fc0_b[j];
+        float s = w[Lyt::F0B + j];
 #pragma unroll
-        for (int i = 0; i < H2; ++i) s += st.fc0_w[j * H2 + i] * n[i];
+        for (int i = 0; i < H2; ++i) s += w[Lyt::F0W + j * H2 + i] * n[i];
         h[j] = silu(s);
     }
     float cat[C];
 #pragma unroll
     for (int i = 0; i < H2; ++i) {
-        float s = st.fc2_b[i];
+        float s = w[Lyt::F2B + i];
 #pragma unroll
-        for (int j = 0; j < C; ++j) s += st.fc2_w[i * C + j] * h[j];
+        for (int j = 0; j < C; ++j) s += w[Lyt::F2W + i * C + j] * h[j];
         cat[i] = s;
     }
 #pragma unroll
     for (int i = H2; i < C; ++i) cat[i] = n[i];
-    // out[d*8 + g] = cat[g*DD + d]
+    // out[d*8 + g] = cat[g*DD + d]  (einops 'b (g d) h w -> b (d g) h w', g = 8)
     float o[C];
 #pragma unroll
     for (int g = 0; g < 8; ++g)
@@ -63,46 +72,72 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const esm_smix_stage& s
     for (int c = 0; c < C; ++c) t[c] = o[c];
 }
 
+__device__ __forceinline__ void stage_copy(float* dst, const float* __restrict__ src, int n, int tid) {
+    for (int i = tid; i < n; i += kThreads) dst[i] = src[i];
+}
+
 template <int C, int K>
 __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
+    using Lyt = SmixLayout<C>;
     constexpr int R = K / 2;
     constexpr int LH = kTileH + 2 * R;
     constexpr int LW = kTileW + 2 * R;
+    constexpr int NW = ESM_SMIX_MAX_STAGES * Lyt::STAGE + (K > 1 ? C * K * K + C : 0);
+    __shared__ float wsh[NW];
     __shared__ float tile[(K > 1) ? C : 1][(K > 1) ? LH : 1][(K > 1) ? LW + 1 : 1];
+    const int tid = threadIdx.x;
     const int H = a.H, W = a.W;
     const int b = blockIdx.z;
     const int y0 = blockIdx.y * kTileH, x0 = blockIdx.x * kTileW;
-    const int ty = threadIdx.x / kTileW, tx = threadIdx.x - (threadIdx.x / kTileW) * kTileW;
+    const int ty = tid / kTileW, tx = tid - (tid / kTileW) * kTileW;
     const int y = y0 + ty, x = x0 + tx;
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
-    float t[C];
+
+    // ---- one staging phase: weights of every stage (+ depthwise), the pixel tile with halo
+    for (int s = 0; s < a.nstages; ++s) {
+        float* d = wsh + s * Lyt::STAGE;
+        const esm_smix_stage& st = a.stage[s];
+        stage_copy(d + Lyt::LN, st.ln_w, C, tid);
+        stage_copy(d + Lyt::F0W, st.fc0_w, C * Lyt::H2, tid);
+        stage_copy(d + Lyt::F0B, st.fc0_b, C, tid);
+        stage_copy(d + Lyt::F2W, st.fc2_w, Lyt::H2 * C, tid);
+        stage_copy(d + Lyt::F2B, st.fc2_b, Lyt::H2, tid);
+    }
+    constexpr int DWO = ESM_SMIX_MAX_STAGES * Lyt::STAGE;
     if (K > 1) {
-        for (int i = threadIdx.x; i < C * LH * LW; i += kThreads) {
+        stage_copy(wsh + DWO, a.dw_w, C * K * K, tid);
+        stage_copy(wsh + DWO + C * K * K, a.dw_b, C, tid);
+        for (int i = tid; i < C * LH * LW; i += kThreads) {
             const int c = i / (LH * LW);
             const int rem = i - c * LH * LW;
             const int ly = rem / LW, lx = rem - (rem / LW) * LW;
             const int gy = y0 + ly - R, gx = x0 + lx - R;
-            tile[c][ly][lx] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? xb[c * plane + gy * W + gx] : 0.f;
+            const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const float v = xb[ok ? c * plane + gy * W + gx : 0];
+            tile[c][ly][lx] = ok ? v : 0.f;
         }
-        __syncthreads();
-        if (y >= H || x >= W) return;
+    }
+    __syncthreads();
+    if (y >= H || x >= W) return;
+    float t[C];
+    if (K > 1) {
+        const float* dww = wsh + DWO;
+        const float* dwb = wsh + DWO + C * K * K;
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             float s = 0.f;
-            const float* wc = a.dw_w + c * K * K;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) s += wc[ky * K + kx] * tile[c][ty + ky][tx + kx];
-            t[c] = s + a.dw_b[c];
+                for (int kx = 0; kx < K; ++kx) s += dww[(c * K + ky) * K + kx] * tile[c][ty + ky][tx + kx];
+            t[c] = s + dwb[c];
         }
     } else {
-        if (y >= H || x >= W) return;
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = xb[c * plane + y * W + x];
     }
-    for (int s = 0; s < a.nstages; ++s) mix_stage<C>(t, a.stage[s]);
+    for (int s = 0; s < a.nstages; ++s) mix_stage<C>(t, wsh + s * Lyt::STAGE);
     const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
     if (a.res) {
 #pragma unroll
