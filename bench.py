@@ -57,6 +57,7 @@ def seeded_init(model: torch.nn.Module, seed: int) -> None:
                     else max(1, w.shape[0] * w[0, 0].numel() // (2 ** (w.dim() - 2)))
                 # refinement residual heads at 0.1x (as tests/helpers.py REFINE_HEAD): realistic disparities
                 gain = 0.1 if (name.startswith("upsample_module.ref") and name.endswith("conv1_up.conv")) else 1.0
+                gain = 0.25 if name == "aggregation_out.conv1_up.conv" else gain  # cost head, as tests/helpers.py
                 w.copy_(torch.randn(w.shape, generator=g) * math.sqrt(2.0 / fan) * gain)
                 if m.bias is not None:
                     m.bias.copy_(torch.rand(m.bias.shape, generator=g) * 0.2 - 0.1)

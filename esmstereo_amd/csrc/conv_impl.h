@@ -14,15 +14,17 @@
 // C1 path    single-output-channel layers (tail convs, the refinement heads) would use
 //            1/16 of an MFMA tile; they run as a VALU dot product instead, one output pixel
 //            per lane, weights broadcast from LDS.
-// Tiling     a 256-thread workgroup (4 waves) owns a TH=4 x TW=16*NT output tile of one
-//            (batch, depth) plane and 16*MT couts; wave w computes output row w of the tile.
+// Tiling     a 256-thread workgroup (4 waves) owns a TH x TW(=16*NT) output tile of one
+//            (batch, depth) plane and 16*MT couts.  KS = 1: TH = 4, wave w computes row w.
+//            KS = 4 (small, latency-bound layers): TH = 1 and the 4 waves split the taps of
+//            the same tile, their partial sums added in LDS in a fixed order at the end
+//            (deterministic), which cuts the serial MFMA chain per wave by 4.
 // Staging    per input-channel chunk of CC channels the workgroup needs (a) the input patch
 //            of the tile (all taps, zero-padded borders) and (b) the weight slab
 //            [tap][CC][16*MT].  Every thread issues its share of both as one batch of
-//            independent loads into registers (fully unrolled, compile-time counts), and the
-//            batch for chunk c+1 is issued before the MFMAs of chunk c, so global latency
-//            overlaps compute; the MFMA loop over TAPS x CC/4 k-steps is fully unrolled and
-//            reads its operands from LDS.
+//            independent loads into registers (compile-time counts), and the batch for chunk
+//            c+1 is issued before the MFMAs of chunk c, so global latency overlaps compute.
+//            CC is the largest of 16/8/4 whose tile fits 64 KiB of LDS (2 workgroups/CU).
 // LDS banks  channel planes are padded so lanes 0-15 (k=0) and 16-31 (k=1) of a ds_read_b32
 //            hit disjoint banks: plane = 16 (mod 32) at unit pixel stride, odd at stride 2;
 //            the 32-wide weight row is padded to 48 floats for the same reason.
@@ -43,7 +45,7 @@ namespace conv {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
-constexpr int kTH = 4;  // output rows per workgroup (one per wave)
+constexpr int kLdsBudget = 64 * 1024;
 
 constexpr int pad_plane(int raw, bool stride2) {
     if (stride2) return raw | 1;
@@ -51,40 +53,54 @@ constexpr int pad_plane(int raw, bool stride2) {
     return (up - 16 >= raw) ? up - 16 : up + 16;
 }
 
-template <bool D3, int K, int S, bool TR, int MT, int NT, int CC, bool C1>
-struct Cfg {
+template <bool D3, int K, int S, bool TR, int MT, int NT, bool C1, int KS>
+struct Geo {
+    static constexpr int TH = 4 / KS;
     static constexpr int TW = 16 * NT;
     static constexpr int KT = TR ? 2 : K;
     static constexpr int KDT = D3 ? KT : 1;
     static constexpr int TAPS = KDT * KT * KT;
     static constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
     static constexpr int PZ = KDT;
-    static constexpr int PR = TR ? kTH + 1 : (kTH - 1) * S + K;
+    static constexpr int PR = TR ? TH + 1 : (TH - 1) * S + K;
     static constexpr int PC = TR ? TW + 1 : (TW - 1) * S + K;
     static constexpr int RAW = PZ * PR * PC;
     static constexpr int PLANE = pad_plane(RAW, S == 2 && !TR);
-    static constexpr int CO = C1 ? 4 : 16 * MT;       // couts staged per workgroup (C1: 1 used)
+    static constexpr int CO = C1 ? 4 : 16 * MT;  // couts staged per workgroup (C1: 1 used)
     static constexpr int WROW = C1 ? 4 : (MT == 1 ? 16 : 48);
+    static constexpr int RAW64 = (RAW + 63) / 64 * 64;
+    static constexpr int RED = (KS - 1) * TH * 64 * MT * NT * 4;  // K-split partial sums
+    static constexpr int lds_bytes(int cc) {
+        const int xs = cc * PLANE, ws = TAPS * cc * WROW;
+        return 4 * ((xs + ws) > RED ? (xs + ws) : RED);
+    }
+    static constexpr int nx(int cc) { return (cc * RAW64 + kThreads - 1) / kThreads; }
+    // largest channel chunk that fits the LDS budget with a bounded staging register file
+    static constexpr int CC = (lds_bytes(16) <= kLdsBudget && nx(16) <= 40) ? 16
+                              : (lds_bytes(8) <= kLdsBudget && nx(8) <= 40) ? 8 : 4;
     static constexpr int XS = CC * PLANE;
     static constexpr int WS = TAPS * CC * WROW;
-    // patch staging walks [CC][RAW64]: RAW64 = RAW rounded up to 64 so each wave-instruction stays
-    // inside one channel (channel -> source selection is then wave-uniform, scalar)
-    static constexpr int RAW64 = (RAW + 63) / 64 * 64;
-    static constexpr int NX = (CC * RAW64 + kThreads - 1) / kThreads;         // patch loads / thread
+    static constexpr int SMEM = (XS + WS) > RED ? (XS + WS) : RED;
+    static constexpr int NX = nx(CC);                                            // patch loads / thread
     static constexpr int NW = (TAPS * CC * CO / 4 + kThreads - 1) / kThreads;  // float4 weight loads / thread
-    static_assert((XS + WS) * 4 <= 64 * 1024, "conv tile exceeds the 64 KiB LDS budget (2 workgroups/CU)");
-    static_assert(!C1 || NT == 4, "C1 path maps one output pixel per lane (TW = 64)");
+    static constexpr bool OK = SMEM * 4 <= kLdsBudget;  // configurations that do not fit are never launched
+    static_assert(XS % 4 == 0, "weight slab must start 16-B aligned");
+    static_assert(!C1 || (NT == 4 && KS == 1), "C1 path maps one output pixel per lane (TW = 64)");
 };
 
-template <bool D3, int K, int S, bool TR, int MT, int NT, int CC, bool C1>
+template <bool D3, int K, int S, bool TR, int MT, int NT, bool C1, int KS>
 __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
-    using C = Cfg<D3, K, S, TR, MT, NT, CC, C1>;
-    __shared__ __attribute__((aligned(16))) float wl[C::WS];
-    __shared__ float xs[C::XS];
+    using C = Geo<D3, K, S, TR, MT, NT, C1, KS>;
+    constexpr int CC = C::CC;
+    __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+    float* xs = smem;
+    float* wl = smem + C::XS;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    const int row = wave / KS;    // output row of the tile this wave computes
+    const int kpart = wave % KS;  // tap subset (K-split)
     const int n16 = lane & 15;
     const int kq = lane >> 4;
 
@@ -94,7 +110,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     const int tiles_w = (Ws + C::TW - 1) / C::TW;
     const int ty = blockIdx.x / tiles_w;
     const int tx = blockIdx.x - ty * tiles_w;
-    const int y0 = ty * kTH;
+    const int y0 = ty * C::TH;
     const int x0 = tx * C::TW;
     const int b = blockIdx.y / Ds;
     const int zs = blockIdx.y - b * Ds;
@@ -123,35 +139,32 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
             const int i = tid + k * kThreads;
             // channel of this wave-instruction: uniform by construction (RAW64 % 64 == 0)
             const int c = __builtin_amdgcn_readfirstlane(i / C::RAW64);
-            const int e = i - c * C::RAW64;
-            const int z = e / (C::PR * C::PC);
-            const int rem = e - z * (C::PR * C::PC);
-            const int r = rem / C::PC;
-            const int col = rem - r * C::PC;
             const int cg = c0 + c;
-            const int id = zo + z, ih = ro + r, iw = xo + col;
-            const bool ok = c < CC && e < C::RAW && cg < a.Cin && ih >= 0 && ih < a.Hi && iw >= 0 &&
-                            iw < a.Wi && (!D3 || (id >= 0 && id < a.Di));
-            // scalar source selection and 64-bit base; per-lane 32-bit offset
-            const float* base;
-            long long sd_, sh_;
-            if (cg < c_src0) {
-                base = a.src[0].ptr + b * a.src[0].sb + cg * a.src[0].sc;
-                sd_ = a.src[0].sd;
-                sh_ = a.src[0].sh;
-            } else if (cg - c_src0 < c_src1) {
-                base = a.src[1].ptr + b * a.src[1].sb + (cg - c_src0) * a.src[1].sc;
-                sd_ = a.src[1].sd;
-                sh_ = a.src[1].sh;
-            } else {
-                base = a.src[2].ptr + b * a.src[2].sb + (cg - c_src0 - c_src1) * a.src[2].sc;
-                sd_ = a.src[2].sd;
-                sh_ = a.src[2].sh;
+            float v = 0.f;
+            if (c < CC && cg < a.Cin) {  // wave-uniform: no loads for padding channels
+                const int e = i - c * C::RAW64;
+                const int z = e / (C::PR * C::PC);
+                const int rem = e - z * (C::PR * C::PC);
+                const int r = rem / C::PC;
+                const int col = rem - r * C::PC;
+                const int id = zo + z, ih = ro + r, iw = xo + col;
+                const bool ok = e < C::RAW && ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi &&
+                                (!D3 || (id >= 0 && id < a.Di));
+                // one wave-uniform branch per source, each with its own constant-index kernarg
+                // fields (a select between sources becomes a scratch lookup table in hipcc)
+#pragma unroll
+                for (int s = 0; s < ESM_MAX_SRC; ++s) {
+                    const int lo = s == 0 ? 0 : (s == 1 ? c_src0 : c_src0 + c_src1);
+                    if (s < a.nsrc && cg >= lo && cg - lo < a.src[s].C) {
+                        const esm_src& sr = a.src[s];
+                        const float* base = sr.ptr + b * sr.sb + (cg - lo) * sr.sc;
+                        const int off = ok ? static_cast<int>((D3 ? id * sr.sd : 0) + ih * sr.sh) + iw : 0;
+                        const float t = base[off];
+                        v = ok ? t : 0.f;
+                    }
+                }
             }
-            if (cg >= a.Cin) base = a.src[0].ptr;  // past Cin: every lane masked, keep the address valid
-            const int off = ok ? static_cast<int>((D3 ? id * sd_ : 0) + ih * sh_) + iw : 0;
-            const float v = base[off];
-            rx[k] = ok ? v : 0.f;
+            rx[k] = v;
         }
 #pragma unroll
         for (int k = 0; k < C::NW; ++k) {
@@ -179,9 +192,9 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
         for (int k = 0; k < C::NW; ++k) {
             const int i = tid + k * kThreads;
             if (i < C::TAPS * CC * C::CO / 4) {
-                const int row = i / (C::CO / 4);  // tap*CC + c
-                const int q4 = i - row * (C::CO / 4);
-                *reinterpret_cast<floatx4*>(wl + row * C::WROW + 4 * q4) = rw[k];
+                const int rowi = i / (C::CO / 4);  // tap*CC + c
+                const int q4 = i - rowi * (C::CO / 4);
+                *reinterpret_cast<floatx4*>(wl + rowi * C::WROW + 4 * q4) = rw[k];
             }
         }
     };
@@ -193,52 +206,88 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
     float acc1 = 0.f;  // C1 path
 
+    // one tap of the current chunk: CC/4 MFMA k-steps (or CC VALU FMAs on the C1 path)
+    auto do_tap = [&](int tap) {
+        const int td = tap / (C::KT * C::KT);
+        const int th = (tap / C::KT) % C::KT;
+        const int tw = tap % C::KT;
+        const int zi = (D3 && TR) ? 1 - td : td;
+        const int ri = TR ? row + 1 - th : row * S + th;
+        if constexpr (C1) {
+            const int ci = TR ? lane + 1 - tw : lane * S + tw;
+#pragma unroll
+            for (int c = 0; c < CC; ++c)
+                acc1 += wl[(tap * CC + c) * C::WROW + (cob & 3)] * xs[c * C::PLANE + (zi * C::PR + ri) * C::PC + ci];
+        } else {
+#pragma unroll
+            for (int c4 = 0; c4 < CC / 4; ++c4) {
+                const int c = c4 * 4 + kq;
+                const float* xrow = xs + c * C::PLANE + (zi * C::PR + ri) * C::PC;
+                float bv[NT];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int ci = TR ? nt * 16 + n16 + 1 - tw : (nt * 16 + n16) * S + tw;
+                    bv[nt] = xrow[ci];
+                }
+                float av[MT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) av[mt] = wl[(tap * CC + c) * C::WROW + mt * 16 + n16];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
+            }
+        }
+    };
+
     load_chunk(0);
     for (int c0 = 0; c0 < a.Cin; c0 += CC) {
         __syncthreads();  // every wave is done reading the previous chunk
         store_chunk();
         __syncthreads();
         if (c0 + CC < a.Cin) load_chunk(c0 + CC);  // in flight during this chunk's math
-        // taps stay a loop (unrolling them lets the compiler hoist every LDS read and run out of
-        // VGPRs while the next chunk's loads are held in registers); the k-steps inside unroll
+        if constexpr (KS == 1) {
+            // one row of KT taps per iteration: enough independent LDS reads to cover their latency
+            // without hoisting the whole chunk's operands (which would exhaust the VGPRs)
 #pragma unroll 1
-        for (int tap = 0; tap < C::TAPS; ++tap) {
-            const int td = tap / (C::KT * C::KT);
-            const int th = (tap / C::KT) % C::KT;
-            const int tw = tap % C::KT;
-            const int zi = (D3 && TR) ? 1 - td : td;
-            const int ri = TR ? wave + 1 - th : wave * S + th;
-            if constexpr (C1) {
-                const int ci = TR ? lane + 1 - tw : lane * S + tw;
+            for (int tg = 0; tg < C::TAPS / C::KT; ++tg) {
 #pragma unroll
-                for (int c = 0; c < CC; ++c)
-                    acc1 += wl[(tap * CC + c) * C::WROW + (cob & 3)] * xs[c * C::PLANE + (zi * C::PR + ri) * C::PC + ci];
-            } else {
-#pragma unroll
-                for (int c4 = 0; c4 < CC / 4; ++c4) {
-                    const int c = c4 * 4 + kq;
-                    const float* xrow = xs + c * C::PLANE + (zi * C::PR + ri) * C::PC;
-                    float bv[NT];
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        const int ci = TR ? nt * 16 + n16 + 1 - tw : (nt * 16 + n16) * S + tw;
-                        bv[nt] = xrow[ci];
-                    }
-                    float av[MT];
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) av[mt] = wl[(tap * CC + c) * C::WROW + mt * 16 + n16];
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt)
-                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
-                }
+                for (int tw = 0; tw < C::KT; ++tw) do_tap(tg * C::KT + tw);
             }
+        } else {
+#pragma unroll 2
+            for (int tap = kpart; tap < C::TAPS; tap += KS) do_tap(tap);
         }
     }
 
+    if constexpr (KS > 1) {  // add the K-split partial sums in a fixed order (deterministic)
+        __syncthreads();
+        constexpr int E = MT * NT * 4;
+        if (kpart > 0) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        smem[(((kpart - 1) * C::TH + row) * E + (mt * NT + nt) * 4 + j) * 64 + lane] = acc[mt][nt][j];
+        }
+        __syncthreads();
+        if (kpart > 0) return;
+#pragma unroll
+        for (int p = 1; p < KS; ++p)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[mt][nt][j] += smem[(((p - 1) * C::TH + row) * E + (mt * NT + nt) * 4 + j) * 64 + lane];
+    }
+
     // ---------------------------------------------------------------- epilogue
-    const int ys = y0 + wave;  // sub-grid / output row of this wave
+    const int ys = y0 + row;  // sub-grid / output row of this wave
     if (ys >= Hs) return;
     const int oz = TR ? 2 * zs + qd : zs;
     const int oy = TR ? 2 * ys + qh : ys;
@@ -278,14 +327,14 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
                 const int ox = TR ? 2 * xsub + qw : xsub;
                 if (vec4 && cq + 3 < a.Cout) {
                     // PixelShuffle(4): couts cq..cq+3 are dx = 0..3 of one (channel, dy) -> one 16-B store
-                    float4 v4;
+                    floatx4 v4;
                     v4.x = finish(acc[mt][nt][0], cq + 0, ox) * a.post_scale;
                     v4.y = finish(acc[mt][nt][1], cq + 1, ox) * a.post_scale;
                     v4.z = finish(acc[mt][nt][2], cq + 2, ox) * a.post_scale;
                     v4.w = finish(acc[mt][nt][3], cq + 3, ox) * a.post_scale;
                     const int cs = cq / 16, dy = (cq / 4) & 3;
                     const long long o = b * a.ob + cs * a.oc + static_cast<long long>(oy * 4 + dy) * a.oh + ox * 4;
-                    *reinterpret_cast<float4*>(a.out + o) = v4;
+                    *reinterpret_cast<floatx4*>(a.out + o) = v4;
                     continue;
                 }
 #pragma unroll
@@ -310,51 +359,45 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     }
 }
 
-// Channel-chunk size per geometry (fits 2 workgroups per CU at the largest NT, MT).
-template <bool D3, int K, int S, bool TR>
-constexpr int chunk() {
-    if (TR) return D3 ? 8 : 16;
-    if (D3) return K == 1 ? 16 : 4;
-    if (K == 5) return 4;
-    return S == 2 ? 8 : 16;
-}
-
-template <bool D3, int K, int S, bool TR, int MT, int NT, bool C1 = false>
-int launch_nt(const esm_conv_desc& a, hipStream_t s) {
-    constexpr int CC = chunk<D3, K, S, TR>();
-    using C = Cfg<D3, K, S, TR, MT, NT, CC, C1>;
+template <bool D3, int K, int S, bool TR, int MT, int NT, bool C1, int KS>
+int launch_cfg(const esm_conv_desc& a, hipStream_t s) {
+    using C = Geo<D3, K, S, TR, MT, NT, C1, KS>;
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
-    const long long tiles = static_cast<long long>((Ws + C::TW - 1) / C::TW) * ((Hs + kTH - 1) / kTH);
+    const long long tiles = static_cast<long long>((Ws + C::TW - 1) / C::TW) * ((Hs + C::TH - 1) / C::TH);
     const unsigned zc = C1 ? static_cast<unsigned>(a.Cout) : ceil_div(a.Cout, C::CO);
     dim3 grid(static_cast<unsigned>(tiles), a.B * Ds, zc * C::NCLS);
     if (tiles > 0x7fffffffLL || grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-    hipLaunchKernelGGL((conv_kernel<D3, K, S, TR, MT, NT, CC, C1>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((conv_kernel<D3, K, S, TR, MT, NT, C1, KS>), grid, dim3(kThreads), 0, s, a);
     return check_launch("conv");
 }
 
-// Tile width: cover the row with as little waste as possible, then trade width for
-// parallelism while the grid is small (tiny problems are latency-bound).
+template <bool D3, int K, int S, bool TR, int MT, int KS>
+int launch_nt(const esm_conv_desc& a, hipStream_t s, int nt) {
+    if constexpr (Geo<D3, K, S, TR, MT, 4, false, KS>::OK)
+        if (nt == 4) return launch_cfg<D3, K, S, TR, MT, 4, false, KS>(a, s);
+    if constexpr (Geo<D3, K, S, TR, MT, 2, false, KS>::OK)
+        if (nt >= 2) return launch_cfg<D3, K, S, TR, MT, 2, false, KS>(a, s);
+    static_assert(Geo<D3, K, S, TR, MT, 1, false, KS>::OK, "narrowest conv tile must fit the LDS budget");
+    return launch_cfg<D3, K, S, TR, MT, 1, false, KS>(a, s);
+}
+
+// Tile shape: cover the row with as little waste as possible, then trade width for
+// parallelism while the grid is small; tiny layers split their taps over the 4 waves.
 template <bool D3, int K, int S, bool TR>
 int launch_geom(const esm_conv_desc& a, hipStream_t s) {
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
-    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_nt<D3, K, S, TR, 1, 4, true>(a, s);
+    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
     const int MT = a.Cout > 16 ? 2 : 1;
-    constexpr int NTMAX = (D3 && K == 3 && S == 2) ? 2 : 4;
+    constexpr int TAPS = (TR ? 2 : K) * (TR ? 2 : K) * (D3 ? (TR ? 2 : K) : 1);
     int nt = Ws > 32 ? 4 : (Ws > 16 ? 2 : 1);
-    if (nt > NTMAX) nt = NTMAX;
-    const long long per = static_cast<long long>(a.B) * Ds * ((Hs + kTH - 1) / kTH) * ceil_div(a.Cout, 16 * MT) *
-                          (TR ? (D3 ? 8 : 4) : 1);
-    while (nt > 1 && per * ((Ws + 16 * nt - 1) / (16 * nt)) < 512) nt /= 2;
-    if (MT == 1) {
-        if (nt == 4) return launch_nt<D3, K, S, TR, 1, NTMAX>(a, s);
-        if (nt == 2) return launch_nt<D3, K, S, TR, 1, 2>(a, s);
-        return launch_nt<D3, K, S, TR, 1, 1>(a, s);
-    }
-    if (nt == 4) return launch_nt<D3, K, S, TR, 2, NTMAX>(a, s);
-    if (nt == 2) return launch_nt<D3, K, S, TR, 2, 2>(a, s);
-    return launch_nt<D3, K, S, TR, 2, 1>(a, s);
+    const long long per = static_cast<long long>(a.B) * Ds * ceil_div(a.Cout, 16 * MT) * (TR ? (D3 ? 8 : 4) : 1);
+    auto blocks = [&](int n, int th) { return per * ((Hs + th - 1) / th) * ((Ws + 16 * n - 1) / (16 * n)); };
+    while (nt > 1 && blocks(nt, 4) < 512) nt /= 2;
+    const bool ksplit = TAPS >= 8 && blocks(nt, 4) < 1024;
+    if (ksplit) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, nt) : launch_nt<D3, K, S, TR, 2, 4>(a, s, nt);
+    return MT == 1 ? launch_nt<D3, K, S, TR, 1, 1>(a, s, nt) : launch_nt<D3, K, S, TR, 2, 1>(a, s, nt);
 }
 
 }  // namespace conv

@@ -55,6 +55,8 @@ def module_spec(model: nn.Module) -> List[SpecEntry]:
         kind = kinds[k]
         if kind == "deconv" and REFINE_HEAD.match(k):
             kind = "deconv_head"
+        elif kind == "deconv" and COST_HEAD.match(k):
+            kind = "deconv_cost_head"
         spec.append((k, list(v.shape), kind))
     return spec
 
@@ -65,6 +67,11 @@ def module_spec(model: nn.Module) -> List[SpecEntry]:
 # magnitude and random-weight outputs reach 1e3-1e4 px, where "EPE <= 1e-3 px" would measure
 # fp32 rounding at an unrealistic scale rather than parity.
 REFINE_HEAD = re.compile(r"(^|\.)upsample_module\.ref\d+x\.conv1_up\.conv\.weight$")
+# The aggregated-cost head (``aggregation_out.conv1_up``) at 0.25x: disparity_regression has no
+# softmax, so at full scale sum_d cost[d]*d of a random net leaves [0, D);
+# 0.25x keeps the initial disparity in the range a trained model produces.
+COST_HEAD = re.compile(r"(^|\.)aggregation_out\.conv1_up\.conv\.weight$")
+HEAD_GAIN = {"deconv_head": 0.1, "deconv_cost_head": 0.25}
 
 
 def seeded_state(spec: Sequence[SpecEntry], seed: int) -> Dict[str, torch.Tensor]:
@@ -76,10 +83,10 @@ def seeded_state(spec: Sequence[SpecEntry], seed: int) -> Dict[str, torch.Tensor
         if kind == "conv":
             fan = int(np.prod(shape[1:]))
             a = rng.standard_normal(n) * math.sqrt(2.0 / fan)
-        elif kind == "deconv" or kind == "deconv_head":
+        elif kind.startswith("deconv"):
             nd = len(shape) - 2
             fan = max(1, shape[0] * int(np.prod(shape[2:])) // (2 ** nd))
-            a = rng.standard_normal(n) * math.sqrt(2.0 / fan) * (0.1 if kind == "deconv_head" else 1.0)
+            a = rng.standard_normal(n) * math.sqrt(2.0 / fan) * HEAD_GAIN.get(kind, 1.0)
         elif kind == "bias" or kind == "bn_bias" or kind == "bn_mean":
             a = rng.uniform(-0.1, 0.1, n)
         elif kind == "bn_weight" or kind == "ln_weight":
