@@ -39,7 +39,7 @@ class EsmConvDesc(Structure):
         ("mul", c_void_p), ("mb", c_int64), ("mc", c_int64), ("mh", c_int64),
         ("res", c_void_p), ("rb", c_int64), ("rc", c_int64), ("rd", c_int64), ("rh", c_int64),
         ("out", c_void_p), ("ob", c_int64), ("oc", c_int64), ("od", c_int64), ("oh", c_int64),
-        ("up", c_void_p), ("up_h", c_int32), ("up_w", c_int32), ("up_f", c_int32), ("reserved", c_int32),
+        ("up", c_void_p), ("up_h", c_int32), ("up_w", c_int32), ("up_f", c_int32), ("hint", c_int32),
         ("ub", c_int64), ("uh", c_int64),
         ("post_scale", c_float), ("post_scale2", c_float), ("out2", c_void_p),
     ]

@@ -388,15 +388,30 @@ template <bool D3, int K, int S, bool TR>
 int launch_geom(const esm_conv_desc& a, hipStream_t s) {
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
-    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
     const int MT = a.Cout > 16 ? 2 : 1;
+    if (a.hint) {  // explicit tile (tuning sweeps, tests of every variant)
+        const int hnt = a.hint & 15, hks = (a.hint >> 4) & 15, hc1 = (a.hint >> 8) & 1;
+        if ((hnt != 1 && hnt != 2 && hnt != 4) || (hks != 1 && hks != 4)) return arg_error("conv: bad tile hint");
+        if (hc1) {
+            if (D3 || a.Cout > 2 || a.shuffle > 1 || hnt != 4 || hks != 1) return arg_error("conv: C1 hint not applicable");
+            return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
+        }
+        if (hks == 4) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 4>(a, s, hnt);
+        return MT == 1 ? launch_nt<D3, K, S, TR, 1, 1>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 1>(a, s, hnt);
+    }
+    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
+    // Rules fitted to scripts/conv_sweep.py on MI355X (profiles/r01_conv_sweep.txt): the
+    // narrow 4x16 tile wins almost everywhere (more blocks, lower VGPR pressure); only
+    // very large, channel-heavy layers amortise their weight fragments over two N tiles,
+    // and only grids far below one wave per CU profit from splitting the taps.
     constexpr int TAPS = (TR ? 2 : K) * (TR ? 2 : K) * (D3 ? (TR ? 2 : K) : 1);
-    int nt = Ws > 32 ? 4 : (Ws > 16 ? 2 : 1);
     const long long per = static_cast<long long>(a.B) * Ds * ceil_div(a.Cout, 16 * MT) * (TR ? (D3 ? 8 : 4) : 1);
-    auto blocks = [&](int n, int th) { return per * ((Hs + th - 1) / th) * ((Ws + 16 * n - 1) / (16 * n)); };
-    while (nt > 1 && blocks(nt, 4) < 512) nt /= 2;
-    const bool ksplit = TAPS >= 8 && blocks(nt, 4) < 1024;
-    if (ksplit) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, nt) : launch_nt<D3, K, S, TR, 2, 4>(a, s, nt);
+    const long long b1 = per * ((Hs + 3) / 4) * ((Ws + 15) / 16);
+    int nt = 1;
+    if (!D3 && a.Cin <= 4 && Ws >= 64) nt = 4;          // patch per channel is cheap; widen
+    else if (b1 >= 8192 && a.cin_pad >= 32) nt = 2;
+    const bool ksplit = TAPS >= 8 && b1 < 300;
+    if (ksplit) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, 1) : launch_nt<D3, K, S, TR, 2, 4>(a, s, 1);
     return MT == 1 ? launch_nt<D3, K, S, TR, 1, 1>(a, s, nt) : launch_nt<D3, K, S, TR, 2, 1>(a, s, nt);
 }
 

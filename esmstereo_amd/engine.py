@@ -165,6 +165,19 @@ class Ctx:
         self.meta: List[dict] = []
         self.stream = None if plan else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def launch(self, graph: bool = True, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Run a plan context's launch list (as a hipGraph by default) on the current stream."""
+        if not self.plan:
+            raise RuntimeError("launch() needs a plan context")
+        s = ctypes.c_void_p((stream or torch.cuda.current_stream(self.device)).cuda_stream)
+        if graph:
+            if not getattr(self, "_graph_ready", False):
+                check(lib.esm_plan_graph_build(self.plan, s), "graph_build")
+                self._graph_ready = True
+            check(lib.esm_plan_graph_launch(self.plan, s), "graph_launch")
+        else:
+            check(lib.esm_plan_run(self.plan, s), "plan_run")
+
     def close(self) -> None:
         if self.plan:
             lib.esm_plan_destroy(self.plan)
@@ -261,7 +274,8 @@ def _spatial(t: torch.Tensor, nd: int) -> Tuple[int, int, int]:
 def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, *,
              mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
              up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
-             out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv") -> torch.Tensor:
+             out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
+             hint: int = 0) -> torch.Tensor:
     """One implicit-GEMM conv launch; ``srcs`` are concatenated along channels (each may be a
     cropped view), the epilogue applies BN/bias, activation, ``*mul``, ``+res``,
     ``+bilinear(up)``, ``*post_scale`` and an optional PixelShuffle(``shuffle``)."""
@@ -352,6 +366,7 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
         if d.up_h * up_f != Ho or d.up_w * up_f != Wo:
             raise ValueError("conv: bilinear source extent x factor must equal the output extent")
     d.post_scale = float(post_scale)
+    d.hint = int(hint)
     if out2 is not None:
         require_device(out2, "conv out2")
         if out2.stride() != out.stride() or out2.shape != out.shape:

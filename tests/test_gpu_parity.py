@@ -185,6 +185,42 @@ def test_conv_transposed(nd, cin, cout, bn):
     assert rel(y, _ref_conv([x], conv, b, act)) < 1e-5
 
 
+TILE_HINTS = [0x11, 0x12, 0x14, 0x41, 0x42, 0x44]
+
+
+@pytest.mark.parametrize("nd,cin,cout,k,s,tr", [(2, 16, 16, 3, 1, False), (2, 40, 72, 3, 2, False),
+                                                (2, 1, 16, 3, 2, False), (3, 32, 8, 3, 1, False),
+                                                (3, 16, 24, 3, 2, False), (3, 24, 12, 4, 2, True),
+                                                (2, 16, 16, 4, 2, True), (2, 56, 16, 1, 1, False)])
+def test_conv_every_tile_variant(nd, cin, cout, k, s, tr):
+    """Every (NT, KS) tile the hint can force gives the same result as the automatic choice
+    and the fp64 torch reference (tolerance 1e-5 relative)."""
+    conv, bn = _mk(nd, cin, cout, k, s, 1 if k == 4 else k // 2, transposed=tr, seed=3)
+    shape = (2, cin, 5, 9, 37) if nd == 3 else (2, cin, 21, 70)
+    x = torch.randn(*shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    xs = [x.to(DEV)]
+    auto = run_conv(Ctx(DEV), p, xs)
+    assert rel(auto, ref) < 1e-5
+    for h in TILE_HINTS:
+        y = run_conv(Ctx(DEV), p, xs, hint=h)
+        assert rel(y, ref) < 1e-5, hex(h)
+    if nd == 2 and cout <= 2:
+        assert rel(run_conv(Ctx(DEV), p, xs, hint=0x114), ref) < 1e-5
+
+
+def test_conv_c1_hint():
+    conv, _ = _mk(2, 8, 1, 3, 1, 1, bn=False, seed=4)
+    x = torch.randn(1, 8, 30, 150)
+    ref = _ref_conv([x], conv, None, ACT_NONE)
+    p = pk(conv, None, ACT_NONE)
+    for h in (0, 0x11, 0x114):
+        assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
+    with pytest.raises(E.EsmError):
+        run_conv(Ctx(DEV), p, [x.to(DEV)], hint=0x3)
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
