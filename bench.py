@@ -88,9 +88,14 @@ def synthetic_pair(B: int, H: int, W: int, maxdisp: int, seed: int, device) -> t
     return left.to(device), right.to(device)
 
 
+RIDGE_FLOP_PER_BYTE = PEAK_F32_MFMA_TFS * 1e12 / (PEAK_HBM_GBS * 1e9)  # ~19.7
+
+
 def kernel_roofline(meta: dict, avg_ms: float) -> dict:
+    """Price the kernel against the roof its arithmetic intensity puts it under: MFMA when
+    algorithmic flops / algorithmic bytes exceeds the fp32 ridge point, HBM otherwise."""
     sec = avg_ms * 1e-3
-    if meta["kind"] == "conv":
+    if meta["flops"] > RIDGE_FLOP_PER_BYTE * meta["bytes"]:
         ach = meta["flops"] / sec / 1e12
         return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_F32_MFMA_TFS, 4)}
@@ -270,7 +275,8 @@ def main() -> None:
         roof.update({"traffic": pmc_traffic(meta[dom]["name"], workload), "kernel": meta[dom]["name"],
                      "kernel_shape": meta[dom].get("shape", ""), "avg_us": round(avg_kms * 1e3, 2),
                      "launches_timed": len(ktimes), "probe": probe_mode, "probe_error": probe_error,
-                     "algorithmic_per_launch": meta[dom]["flops"] if meta[dom]["kind"] == "conv" else meta[dom]["bytes"]})
+                     "algorithmic_flops_per_launch": meta[dom]["flops"],
+                     "algorithmic_bytes_per_launch": meta[dom]["bytes"]})
         total = args.batch * world * args.steps
         line = {
             "metric": METRIC,

@@ -1,0 +1,67 @@
+"""Batch sharding of the hot path over the GPUs of one node.
+
+Stereo pairs are independent in eval mode, so a global batch splits into contiguous slices,
+one per rank (one process per GPU); the only exchange is gathering the disparity maps.  Over
+RCCL (backend "nccl" on ROCm) that is one ``all_gather_into_tensor`` over xGMI; over gloo
+(CPU tests) the list form of ``all_gather``.  Uneven batches are padded to the largest slice
+for the collective and trimmed after it.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(batch: int, world: int, rank: int) -> Tuple[int, int]:
+    """[lo, hi) of ``rank``'s contiguous slice of a ``batch``-pair global batch; the first
+    ``batch % world`` ranks take one extra pair."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"shard_range: rank {rank} outside world {world}")
+    if batch < 0:
+        raise ValueError("shard_range: negative batch")
+    base, extra = divmod(batch, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard(t: torch.Tensor, world: Optional[int] = None, rank: Optional[int] = None) -> torch.Tensor:
+    """This rank's slice (a view) of a global-batch tensor."""
+    world = dist.get_world_size() if world is None else world
+    rank = dist.get_rank() if rank is None else rank
+    lo, hi = shard_range(int(t.shape[0]), world, rank)
+    return t[lo:hi]
+
+
+def gather_disparities(local: torch.Tensor, batch: int, group=None) -> torch.Tensor:
+    """Concatenate every rank's ``[b_r, ...]`` result into the ``[batch, ...]`` global result
+    on every rank (rank order = batch order)."""
+    world = dist.get_world_size(group)
+    rows = [shard_range(batch, world, r) for r in range(world)]
+    mx = max(hi - lo for lo, hi in rows)
+    me = dist.get_rank(group)
+    if local.shape[0] != rows[me][1] - rows[me][0]:
+        raise ValueError(f"gather_disparities: rank {me} holds {local.shape[0]} pairs, expected "
+                         f"{rows[me][1] - rows[me][0]}")
+    buf = local.contiguous()
+    if buf.shape[0] < mx:  # pad to a uniform slice for the collective
+        buf = torch.cat([buf, buf.new_zeros((mx - buf.shape[0],) + tuple(buf.shape[1:]))])
+    if dist.get_backend(group) == "nccl":
+        full = buf.new_empty((world * mx,) + tuple(buf.shape[1:]))
+        dist.all_gather_into_tensor(full, buf, group=group)
+        parts = full.split(mx)
+    else:
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, rows)])
+
+
+def sharded_forward(model, left: torch.Tensor, right: torch.Tensor, group=None) -> torch.Tensor:
+    """Eval forward of a global batch split across the ranks of ``group``: every rank runs its
+    slice through ``model`` and receives the full ``[B, H, W]`` disparity batch."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_range(int(left.shape[0]), world, rank)
+    with torch.no_grad():
+        disp = model(left[lo:hi], right[lo:hi], False)[0]
+    return gather_disparities(disp, int(left.shape[0]), group)

@@ -1,0 +1,77 @@
+"""Per-op memory-side traffic of the bench step from two rocprofv3 PMC passes.
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python3 bench.py ...
+    python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/ops.json \
+        "ESMStereo-S gwc 384x1248 md192 B1" profiles/pmc_traffic.json
+
+Dispatches of our kernels are assigned to the launch list by position (the timed steps replay
+it in order; the oldest block is dropped, as in prof_ops.py).  Units and the gfx950
+correction follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB, and FETCH_SIZE
+reports half of the bytes a wide coalesced read moves, so
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+Both raw counters are kept next to the corrected figure (the x2 is calibrated for 16-B/lane
+streams; other widths are uncalibrated, so the raw numbers are the primary record).
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+OURS = ("conv_kernel", "smix_kernel", "gwc_kernel", "concat_kernel", "normcorr_kernel", "l2norm_kernel",
+        "dispreg_kernel", "topk2_kernel")
+
+
+def per_dispatch(d: str, counter: str):
+    vals = defaultdict(float)
+    names = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] != counter or not any(s in r["Kernel_Name"] for s in OURS):
+                    continue
+                k = int(r["Dispatch_Id"])
+                vals[k] += float(r["Counter_Value"])
+                names[k] = r["Kernel_Name"]
+    order = sorted(vals)
+    return [vals[k] for k in order]
+
+
+def assign(seq, n):
+    steps = len(seq) // n
+    if steps == 0:
+        raise SystemExit("fewer dispatches than one step")
+    tail = seq[-(steps - 1) * n:] if steps > 1 else seq[-n:]
+    acc = defaultdict(list)
+    for i, v in enumerate(tail):
+        acc[i % n].append(v)
+    return {i: sum(v) / len(v) for i, v in acc.items()}
+
+
+def main():
+    fdir, wdir, ops_json, workload, out = sys.argv[1:6]
+    ops = json.load(open(ops_json))
+    n = len(ops)
+    fetch = assign(per_dispatch(fdir, "FETCH_SIZE"), n)
+    write = assign(per_dispatch(wdir, "WRITE_SIZE"), n)
+    tab = json.load(open(out)) if os.path.exists(out) else {}
+    rows = {}
+    for i, op in enumerate(ops):
+        f, w = fetch.get(i, 0.0), write.get(i, 0.0)
+        rows[op["name"]] = {"fetch_size_kib": round(f, 1), "write_size_kib": round(w, 1),
+                            "hbm_bytes_per_launch": int((2 * f + w) * 1024),
+                            "algorithmic_bytes": op["bytes"]}
+    tab[workload] = rows
+    with open(out, "w") as fh:
+        json.dump(tab, fh, indent=1)
+    top = sorted(rows.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:15]
+    for k, v in top:
+        print(f"{k[:50]:50s} {v['hbm_bytes_per_launch'] / 1e6:9.3f} MB  (alg {v['algorithmic_bytes'] / 1e6:8.3f} MB)")
+
+
+if __name__ == "__main__":
+    main()
