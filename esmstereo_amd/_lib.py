@@ -10,7 +10,8 @@ import os
 from ctypes import POINTER, Structure, c_float, c_int, c_int32, c_int64, c_void_p
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libesmstereo_amd.so")
+# ESM_LIB: load another build of the same ABI (the diagnostic build of esmstereo_amd/build.py)
+LIB_PATH = os.environ.get("ESM_LIB") or os.path.join(PKG, "libesmstereo_amd.so")
 ROOT = os.path.dirname(PKG)
 HEADER_PATH = os.path.join(ROOT, "include", "esmstereo_amd.h")
 

@@ -37,12 +37,12 @@
 //            one 16-byte store per lane for r = 4).
 #pragma once
 
-#include "common.h"
+#include "conv_direct.h"
+#include "conv_rows.h"
+#include "conv_epilogue.h"
 
 namespace esm {
 namespace conv {
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 constexpr int kLdsBudget = 64 * 1024;
@@ -291,71 +291,15 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     if (ys >= Hs) return;
     const int oz = TR ? 2 * zs + qd : zs;
     const int oy = TR ? 2 * ys + qh : ys;
-    auto finish = [&](float v, int co, int ox) -> float {
-        const float scl = a.scale ? a.scale[co] : 1.f;
-        const float shf = a.shift ? a.shift[co] : 0.f;
-        v = a.scale ? v * scl + shf : v + shf;
-        v = apply_act(v, a.act);
-        if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + oy * a.mh + ox];
-        if (a.res) v = v + a.res[b * a.rb + co * a.rc + oz * a.rd + oy * a.rh + ox];
-        if (a.up) v = bilinear_at(a.up + b * a.ub, a.up_h, a.up_w, a.uh, a.up_f, oy, ox) + v;
-        return v;
-    };
-    auto put = [&](float v, int co, int ox) {
-        const long long o = b * a.ob + co * a.oc + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox;
-        a.out[o] = v * a.post_scale;
-        if (a.out2) a.out2[o] = v * a.post_scale2;
-    };
     if constexpr (C1) {
         const int xsub = x0 + lane;
         if (xsub < Ws) {
             const int ox = TR ? 2 * xsub + qw : xsub;
-            put(finish(acc1, cob, ox), cob, ox);
+            conv_put(a, conv_finish(a, acc1, b, cob, oz, oy, ox), b, cob, oz, oy, ox);
         }
         return;
     } else {
-        const int r = a.shuffle > 1 ? a.shuffle : 1;
-        const bool vec4 = r == 4 && !a.out2 && ((a.ob | a.oc | a.oh) & 3) == 0 &&
-                          (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const int cq = cob + mt * 16 + kq * 4;  // first of this lane's 4 couts
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int xsub = x0 + nt * 16 + n16;
-                if (xsub >= Ws) continue;
-                const int ox = TR ? 2 * xsub + qw : xsub;
-                if (vec4 && cq + 3 < a.Cout) {
-                    // PixelShuffle(4): couts cq..cq+3 are dx = 0..3 of one (channel, dy) -> one 16-B store
-                    floatx4 v4;
-                    v4.x = finish(acc[mt][nt][0], cq + 0, ox) * a.post_scale;
-                    v4.y = finish(acc[mt][nt][1], cq + 1, ox) * a.post_scale;
-                    v4.z = finish(acc[mt][nt][2], cq + 2, ox) * a.post_scale;
-                    v4.w = finish(acc[mt][nt][3], cq + 3, ox) * a.post_scale;
-                    const int cs = cq / 16, dy = (cq / 4) & 3;
-                    const long long o = b * a.ob + cs * a.oc + static_cast<long long>(oy * 4 + dy) * a.oh + ox * 4;
-                    *reinterpret_cast<floatx4*>(a.out + o) = v4;
-                    continue;
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int co = cq + j;
-                    if (co >= a.Cout) continue;
-                    const float v = finish(acc[mt][nt][j], co, ox);
-                    if (r > 1) {
-                        const int cs = co / (r * r);
-                        const int rem = co - cs * r * r;
-                        const int yy = oy * r + rem / r;
-                        const int xx = ox * r + (rem - (rem / r) * r);
-                        const long long o = b * a.ob + cs * a.oc + static_cast<long long>(yy) * a.oh + xx;
-                        a.out[o] = v * a.post_scale;
-                        if (a.out2) a.out2[o] = v * a.post_scale2;
-                    } else {
-                        put(v, co, ox);
-                    }
-                }
-            }
-        }
+        conv_store_tile<MT, NT>(a, acc, b, oz, oy, x0, Ws, TR, qw, cob, lane, conv_epi_const<MT>(a, cob, lane));
     }
 }
 
@@ -382,16 +326,48 @@ int launch_nt(const esm_conv_desc& a, hipStream_t s, int nt) {
     return launch_cfg<D3, K, S, TR, MT, 1, false, KS>(a, s);
 }
 
-// Tile shape: cover the row with as little waste as possible, then trade width for
-// parallelism while the grid is small; tiny layers split their taps over the 4 waves.
+// Direct form: N tiles (1/2) and K-split (1/4) as requested; rows per workgroup so that the
+// grid holds about 2048 waves (4 rows per wave at most, for L1 reuse of the tap rows).
+template <bool D3, int K, int S, bool TR, int MT>
+int launch_direct_sel(const esm_conv_desc& a, hipStream_t s, int nt, int ks, int rows_per_wave = 0) {
+    const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
+    const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
+    const long long rows = static_cast<long long>(a.B) * Ds * Hs * ((Ws + 16 * nt - 1) / (16 * nt)) *
+                           ceil_div(a.Cout, 16 * MT) * (TR ? (D3 ? 8 : 4) : 1);
+    if (ks == 4) {
+        return nt == 2 ? launch_direct<D3, K, S, TR, MT, 2, 4>(a, s, 1) : launch_direct<D3, K, S, TR, MT, 1, 4>(a, s, 1);
+    }
+    const long long per_wave = rows_per_wave > 0 ? rows_per_wave : rows / 2048;
+    const int rb = 4 * static_cast<int>(per_wave < 1 ? 1 : (per_wave > 8 ? 8 : per_wave));
+    return nt == 2 ? launch_direct<D3, K, S, TR, MT, 2, 1>(a, s, rb) : launch_direct<D3, K, S, TR, MT, 1, 1>(a, s, rb);
+}
+
+// Tile choice.  hint (esm_conv_desc.hint) forces one: NT | KS << 4 | C1 << 8 | DIRECT << 9 |
+// ROWS << 10 (row-streaming form, conv_rows.h) | rows-per-wave << 12 (direct form).
+// Automatic: single-output-channel layers take the VALU path; everything the direct form can
+// address takes it (fewest instructions per MFMA, no barriers), K-split when the grid is far
+// below one wave per SIMD; the LDS-staged form covers the rest.
 template <bool D3, int K, int S, bool TR>
 int launch_geom(const esm_conv_desc& a, hipStream_t s) {
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
     const int MT = a.Cout > 16 ? 2 : 1;
     if (a.hint) {  // explicit tile (tuning sweeps, tests of every variant)
-        const int hnt = a.hint & 15, hks = (a.hint >> 4) & 15, hc1 = (a.hint >> 8) & 1;
+        const int hnt = a.hint & 15, hks = (a.hint >> 4) & 15, hc1 = (a.hint >> 8) & 1, hdir = (a.hint >> 9) & 1;
+        const int hrw = (a.hint >> 12) & 15;  // direct form: rows per wave (0 = automatic)
+        if ((a.hint >> 10) & 1) {  // row-streaming form
+            if constexpr (!TR && S == 1 && (K & 1)) {
+                if (MT == 1 ? rows_ok<D3, K, 1>(a) : rows_ok<D3, K, 2>(a))
+                    return MT == 1 ? launch_rows<D3, K, 1>(a, s) : launch_rows<D3, K, 2>(a, s);
+            }
+            return arg_error("conv: row-streaming hint not applicable");
+        }
         if ((hnt != 1 && hnt != 2 && hnt != 4) || (hks != 1 && hks != 4)) return arg_error("conv: bad tile hint");
+        if (hdir) {
+            if (hc1 || hnt == 4 || !direct_ok(a)) return arg_error("conv: direct hint not applicable");
+            return MT == 1 ? launch_direct_sel<D3, K, S, TR, 1>(a, s, hnt, hks, hrw)
+                           : launch_direct_sel<D3, K, S, TR, 2>(a, s, hnt, hks, hrw);
+        }
         if (hc1) {
             if (D3 || a.Cout > 2 || a.shuffle > 1 || hnt != 4 || hks != 1) return arg_error("conv: C1 hint not applicable");
             return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
@@ -399,16 +375,29 @@ int launch_geom(const esm_conv_desc& a, hipStream_t s) {
         if (hks == 4) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 4>(a, s, hnt);
         return MT == 1 ? launch_nt<D3, K, S, TR, 1, 1>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 1>(a, s, hnt);
     }
-    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1) return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
-    // Rules fitted to scripts/conv_sweep.py on MI355X (profiles/r01_conv_sweep.txt): the
-    // narrow 4x16 tile wins almost everywhere (more blocks, lower VGPR pressure); only
-    // very large, channel-heavy layers amortise their weight fragments over two N tiles,
-    // and only grids far below one wave per CU profit from splitting the taps.
+    // row-streaming form for stride-1 layers with horizontal taps to share (1x1 layers measured
+    // faster in the direct form)
+    if constexpr (!TR && S == 1 && (K & 1) && K >= 3) {
+        if (MT == 1 ? rows_ok<D3, K, 1>(a) : rows_ok<D3, K, 2>(a))
+            return MT == 1 ? launch_rows<D3, K, 1>(a, s) : launch_rows<D3, K, 2>(a, s);
+    }
+    // single-output-channel layers the direct form cannot take: VALU path
+    if (!D3 && a.Cout <= 2 && Ws >= 64 && a.shuffle <= 1 && !direct_ok(a))
+        return launch_cfg<D3, K, S, TR, 1, 4, true, 1>(a, s);
     constexpr int TAPS = (TR ? 2 : K) * (TR ? 2 : K) * (D3 ? (TR ? 2 : K) : 1);
     const long long per = static_cast<long long>(a.B) * Ds * ceil_div(a.Cout, 16 * MT) * (TR ? (D3 ? 8 : 4) : 1);
+    const long long rows1 = per * Hs * ((Ws + 15) / 16);  // 16-pixel row segments
+    if (direct_ok(a)) {
+        // sweep-fitted (profiles/r01_conv_sweep*.txt): two N tiles pay off for concatenated 1x1
+        // inputs and for wide-input, narrow-output 3-D layers; tiny grids split the taps
+        const int ks = (TAPS >= 8 && rows1 < 256) ? 4 : 1;
+        const int nt = (ks == 1 && ((K == 1 && a.nsrc > 1) || (D3 && a.Cin >= 32 && a.Cout <= 16))) ? 2 : 1;
+        return MT == 1 ? launch_direct_sel<D3, K, S, TR, 1>(a, s, nt, ks) : launch_direct_sel<D3, K, S, TR, 2>(a, s, nt, ks);
+    }
+    // LDS-staged form; rules fitted to scripts/conv_sweep.py on MI355X (profiles/r01_conv_sweep.txt)
     const long long b1 = per * ((Hs + 3) / 4) * ((Ws + 15) / 16);
     int nt = 1;
-    if (!D3 && a.Cin <= 4 && Ws >= 64) nt = 4;          // patch per channel is cheap; widen
+    if (!D3 && a.Cin <= 4 && Ws >= 64) nt = 4;
     else if (b1 >= 8192 && a.cin_pad >= 32) nt = 2;
     const bool ksplit = TAPS >= 8 && b1 < 300;
     if (ksplit) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, 1) : launch_nt<D3, K, S, TR, 2, 4>(a, s, 1);

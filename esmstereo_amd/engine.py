@@ -152,6 +152,17 @@ def param_token(*mods: torch.nn.Module) -> Tuple:
 # ----------------------------------------------------------------------------- context
 
 
+def _spans(*ts) -> List[Tuple[int, int]]:
+    """(base address, bytes) of the allocations behind tensors: the unit the plan's
+    dependency analysis works in (a view depends on its whole allocation)."""
+    out = []
+    for t in ts:
+        if t is not None:
+            st = t.untyped_storage()
+            out.append((st.data_ptr(), st.nbytes()))
+    return out
+
+
 class Ctx:
     """Where ops go: launched now (``plan=False``) or appended to a native plan."""
 
@@ -215,7 +226,8 @@ class Ctx:
 
     def gwc(self, L, R, att, V, B, C, H, W, D, G) -> None:
         self.meta.append(dict(name="gwc_volume", kind="gwc", flops=2 * B * C * D * H * W,
-                              bytes=4 * B * (2 * C * H * W + G * D * H * W + (G * H * W if att is not None else 0))))
+                              bytes=4 * B * (2 * C * H * W + G * D * H * W + (G * H * W if att is not None else 0)),
+                              reads=_spans(L, R, att), writes=_spans(V)))
         a = att.data_ptr() if att is not None else None
         if self.plan:
             self.hold(L, R, att, V)
@@ -226,7 +238,7 @@ class Ctx:
 
     def concat(self, L, R, V, B, C, H, W, D) -> None:
         self.meta.append(dict(name="concat_volume", kind="concat", flops=0,
-                              bytes=4 * B * (2 * C * H * W + 2 * C * D * H * W)))
+                              bytes=4 * B * (2 * C * H * W + 2 * C * D * H * W), reads=_spans(L, R), writes=_spans(V)))
         if self.plan:
             self.hold(L, R, V)
             check(lib.esm_plan_add_concat(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D), "concat")
@@ -236,7 +248,7 @@ class Ctx:
 
     def normcorr(self, L, R, V, work, B, C, H, W, D) -> None:
         self.meta.append(dict(name="normcorr_volume", kind="normcorr", flops=2 * B * C * D * H * W,
-                              bytes=4 * B * (2 * C * H * W + D * H * W)))
+                              bytes=4 * B * (2 * C * H * W + D * H * W), reads=_spans(L, R), writes=_spans(V, work)))
         if self.plan:
             self.hold(L, R, V, work)
             check(lib.esm_plan_add_normcorr(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C,
@@ -247,7 +259,8 @@ class Ctx:
 
     def regression(self, kind, cost, out, B, D, H, W, samples=None) -> None:
         self.meta.append(dict(name="regression_topk2" if kind else "disparity_regression", kind="regression",
-                              flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W))
+                              flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W, reads=_spans(cost, samples),
+                              writes=_spans(out)))
         if self.plan:
             if samples is not None:
                 raise ValueError("plan regression: disparity samples are arange(D)")
@@ -384,7 +397,8 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
     extra = 4 * (res.numel() if res is not None else 0) + 4 * (mul.numel() if mul is not None else 0)
     ctx.meta.append(dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
                          shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
-                               f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}"))
+                               f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
+                         reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2)))
     ctx.conv(d)
     return out
 
@@ -430,6 +444,7 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
     ctx.hold(x, out, res, *(dw or ()))
     npix = B * H * W
     ctx.meta.append(dict(name=tag, kind="smix", flops=npix * (2 * C * C * len(stages) + (2 * C * d.dw_k ** 2 if dw else 0)),
-                         bytes=4 * npix * C * (3 if res is not None else 2), shape=f"C{C} {H}x{W} dw{d.dw_k}"))
+                         bytes=4 * npix * C * (3 if res is not None else 2), shape=f"C{C} {H}x{W} dw{d.dw_k}",
+                         reads=_spans(x, res), writes=_spans(out)))
     ctx.smix(d)
     return out

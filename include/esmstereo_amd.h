@@ -92,7 +92,8 @@ typedef struct {
     int64_t ob, oc, od, oh;
     const float* up;
     int32_t up_h, up_w, up_f;
-    int32_t hint; /* 0 = automatic tile choice; else NT | (KS << 4) | (C1 << 8) (tuning / tests) */
+    int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 12
+                     (tuning sweeps / tests; see conv_impl.h launch_geom) */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;

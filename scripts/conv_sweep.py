@@ -38,7 +38,7 @@ LAYERS = [
     ("L conv1.1 3d k3 24->24 24x48x156", 3, [24], 24, 3, 1, False, (24, 48, 156), ACT_GELU, 1),
 ]
 
-HINTS = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x44, 0x114]
+HINTS = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x44, 0x114, 0x211, 0x212, 0x241, 0x242]
 
 
 def make(nd, cins, cout, k, s, tr, act, dev):

@@ -185,7 +185,7 @@ def test_conv_transposed(nd, cin, cout, bn):
     assert rel(y, _ref_conv([x], conv, b, act)) < 1e-5
 
 
-TILE_HINTS = [0x11, 0x12, 0x14, 0x41, 0x42, 0x44]
+TILE_HINTS = [0x11, 0x12, 0x14, 0x41, 0x42, 0x44, 0x211, 0x212, 0x241, 0x242]  # LDS-staged, then direct
 
 
 @pytest.mark.parametrize("nd,cin,cout,k,s,tr", [(2, 16, 16, 3, 1, False), (2, 40, 72, 3, 2, False),
@@ -208,6 +208,49 @@ def test_conv_every_tile_variant(nd, cin, cout, k, s, tr):
         assert rel(y, ref) < 1e-5, hex(h)
     if nd == 2 and cout <= 2:
         assert rel(run_conv(Ctx(DEV), p, xs, hint=0x114), ref) < 1e-5
+
+
+ROWS_CASES = [(2, 16, 16, 3, 1, 37, 70), (2, 8, 16, 3, 1, 9, 29), (2, 1, 16, 5, 1, 24, 78), (2, 1, 16, 5, 2, 24, 78),
+              (2, 16, 8, 1, 0, 11, 33), (2, 16, 32, 3, 1, 13, 45), (2, 16, 24, 3, 1, 6, 17), (2, 4, 1, 3, 1, 20, 50),
+              (3, 16, 16, 3, 1, (5, 9, 37), None), (3, 8, 8, 3, 1, (6, 7, 19), None), (3, 16, 24, 1, 0, (3, 6, 20), None)]
+
+
+@pytest.mark.parametrize("nd,cin,cout,k,p,H,W", ROWS_CASES)
+def test_conv_rows_form(nd, cin, cout, k, p, H, W):
+    """The row-streaming form (DPP-shifted B operands, LDS weights, pipelined rows) against the
+    fp64 torch reference, forced (hint 0x411) and automatic; rel <= 1e-5."""
+    conv, bn = _mk(nd, cin, cout, k, 1, p, seed=5)
+    shape = (2, cin) + (H if nd == 3 else (H, W))
+    x = torch.randn(*shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    pc = pk(conv, bn, ACT_GELU)
+    for h in (0, 0x411):
+        y = run_conv(Ctx(DEV), pc, [x.to(DEV)], hint=h)
+        assert rel(y, ref) < 1e-5, hex(h)
+
+
+def test_conv_rows_form_epilogues():
+    conv, bn = _mk(2, 16, 16, 3, 1, 1, seed=6)
+    x = torch.randn(1, 16, 30, 64)
+    res = torch.randn(1, 16, 30, 64)
+    mul = torch.randn(1, 16, 30, 64)
+    ref = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res, post=4.0)
+    y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], mul=mul.to(DEV), res=res.to(DEV), post_scale=4.0,
+                 hint=0x411)
+    assert rel(y, ref) < 1e-5
+    c1, _ = _mk(2, 16, 1, 3, 1, 1, bn=False, seed=9)  # the tail conv: 1 channel + bilinear residual
+    up = torch.randn(1, 1, 15, 32)
+    ref1 = _ref_conv([x], c1, None, ACT_NONE, up=up, up_f=2, post=4.0)
+    y1 = run_conv(Ctx(DEV), pk(c1, None, ACT_NONE), [x.to(DEV)], up=up.to(DEV), up_f=2, post_scale=4.0, hint=0x411)
+    assert rel(y1, ref1) < 1e-5
+    c2, _ = _mk(2, 8, 64, 1, 1, 0, bias=True, bn=False, seed=7)
+    x2 = torch.randn(1, 8, 12, 40)
+    ref2 = _ref_conv([x2], c2, None, ACT_SILU, shuffle=4)
+    y2 = run_conv(Ctx(DEV), pk(c2, None, ACT_SILU), [x2.to(DEV)], shuffle=4, hint=0x411)
+    assert rel(y2, ref2) < 1e-5
+    with pytest.raises(E.EsmError):  # stride 2 is not a row-streaming layer
+        c3, b3 = _mk(2, 16, 16, 3, 2, 1, seed=8)
+        run_conv(Ctx(DEV), pk(c3, b3, ACT_GELU), [x.to(DEV)], hint=0x411)
 
 
 def test_conv_c1_hint():
