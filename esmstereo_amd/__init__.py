@@ -8,7 +8,7 @@ Drop-in for the reference ``models`` package on the hot path:
 Op-level drop-ins for ``models/submodule.py`` live in :mod:`esmstereo_amd.volumes`;
 the ShuffleMixer blocks in :mod:`esmstereo_amd.mixer`; the hot-path modules in
 :mod:`esmstereo_amd.blocks`.  Importing requires the in-tree ``libesmstereo_amd.so``
-(build: ``python -m esmstereo_amd.build``); there is no CPU fallback.
+(build: ``python esmstereo_amd/build.py``); there is no CPU fallback.
 """
 from ._lib import EsmError  # noqa: F401  (loads and checks the native library)
 from .blocks import BasicConv, Conv2x, aggregation, up_refinement, upsample4, upsample8, upsample16  # noqa: F401

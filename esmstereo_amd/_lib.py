@@ -95,7 +95,7 @@ def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"esmstereo_amd: native library {LIB_PATH} not found. Build it with "
-            "`python -m esmstereo_amd.build` (hipcc --offload-arch=gfx950); there is no fallback.")
+            "`python esmstereo_amd/build.py` (hipcc --offload-arch=gfx950); there is no fallback.")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -1,6 +1,6 @@
 """Build the gfx950 shared library ``esmstereo_amd/libesmstereo_amd.so`` in-tree.
 
-``python -m esmstereo_amd.build`` (or ``__graft_entry__.build()``) compiles every
+``python esmstereo_amd/build.py`` (or ``__graft_entry__.build()``) compiles every
 ``csrc/*.hip`` with ``hipcc --offload-arch=gfx950`` into objects (in parallel, skipping
 up-to-date ones) and links one C-ABI shared library.  No torch headers are involved: the
 library's interface is ``include/esmstereo_amd.h``.

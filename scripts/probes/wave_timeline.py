@@ -1,6 +1,6 @@
 """Per-wave timeline of one direct-conv launch (diagnostic build only).
 
-    python -m esmstereo_amd.build --diag
+    python esmstereo_amd/build.py --diag
     ESM_LIB=esmstereo_amd/_build_diag/libesmstereo_amd.so python scripts/probes/wave_timeline.py [--h 192]
 
 Each wave of the 2-D direct kernel records s_memrealtime (100 MHz, chip-wide) at entry and
@@ -17,7 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 if "ESM_LIB" not in os.environ:
-    raise SystemExit("set ESM_LIB to the diagnostic build (python -m esmstereo_amd.build --diag)")
+    raise SystemExit("set ESM_LIB to the diagnostic build (python esmstereo_amd/build.py --diag)")
 from esmstereo_amd import _lib  # noqa: E402
 from esmstereo_amd.engine import ACT_GELU, Ctx, pack_conv, run_conv  # noqa: E402
 
