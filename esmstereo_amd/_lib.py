@@ -57,6 +57,14 @@ class EsmSmixDesc(Structure):
                 ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32)]
 
 
+class EsmShuffleTailDesc(Structure):
+    _fields_ = [("x", c_void_p), ("xb", c_int64), ("xc", c_int64), ("xh", c_int64),
+                ("up_w", c_void_p), ("up_b", c_void_p), ("tail_w", c_void_p), ("tail_b", c_void_p),
+                ("out", c_void_p), ("ob", c_int64), ("oh", c_int64),
+                ("B", c_int32), ("nf", c_int32), ("H", c_int32), ("W", c_int32), ("r", c_int32),
+                ("reserved", c_int32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/esmstereo_amd.h
 SIGNATURES = {
     "esm_last_error": (ctypes.c_char_p, []),
@@ -69,16 +77,19 @@ SIGNATURES = {
     "esm_topk2_regression_f32": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
     "esm_conv_f32": (c_int, [POINTER(EsmConvDesc), c_void_p]),
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
+    "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
     "esm_plan_create": (c_void_p, []),
     "esm_plan_destroy": (None, [c_void_p]),
     "esm_plan_add_conv": (c_int, [c_void_p, POINTER(EsmConvDesc)]),
     "esm_plan_add_smix": (c_int, [c_void_p, POINTER(EsmSmixDesc)]),
+    "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_regression": (c_int, [c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 4),
     "esm_plan_num_ops": (c_int, [c_void_p]),
     "esm_plan_op_kind": (c_int, [c_void_p, c_int]),
+    "esm_plan_set_conv_hint": (c_int, [c_void_p, c_int, c_int]),
     "esm_plan_run": (c_int, [c_void_p, c_void_p]),
     "esm_plan_graph_build": (c_int, [c_void_p, c_void_p]),
     "esm_plan_graph_launch": (c_int, [c_void_p, c_void_p]),
@@ -101,7 +112,7 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc)):
+    for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc, EsmShuffleTailDesc)):
         if lib.esm_struct_size(which) != ctypes.sizeof(st):
             raise ImportError(f"esmstereo_amd: ABI mismatch for {st.__name__}: "
                               f"C {lib.esm_struct_size(which)} vs ctypes {ctypes.sizeof(st)}")

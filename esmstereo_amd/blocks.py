@@ -10,7 +10,8 @@ whole-hot-path plan).  Fusions relative to the reference op graph:
   next conv; nothing is materialised;
 * BatchNorm (eval) and conv biases fold into a per-channel scale/shift epilogue, GELU /
   SiLU run in the same epilogue;
-* ``Conv2d(1x1) -> PixelShuffle -> SiLU`` is one conv with a shuffled store;
+* ``Conv2d(1x1) -> PixelShuffle -> SiLU -> tail Conv2d(3x3 -> 1)`` is one launch
+  (``esm_shuffle_tail_f32``): the shuffled map is never written;
 * ``F.interpolate(prev, bilinear) + refinement`` is the epilogue of the refinement's last
   transposed conv, and the final ``* 4`` (ESMStereo.py:737-745) folds into its store.
 """
@@ -22,7 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import ACT_GELU, ACT_NONE, ACT_SILU, Ctx, PackedConv, pack_conv, param_token, run_conv
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token,
+                     run_conv, run_shuffle_tail)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -220,11 +222,11 @@ class _ESMUpsampler(nn.Module):
         tok = param_token(*self.modules())
         if self._esm is None or self._esm[0] != tok:
             p = {"to_feat": pack_conv(self.to_feat)}
-            for (tag, *_r) in self.STAGES:
+            for (tag, _C, _cat, _spx, r, *_r) in self.STAGES:
                 spx = getattr(self, f"spx_{tag}")
                 p[f"spx1_{tag}"] = pack_conv(spx[1], spx[2], ACT_GELU)
-                p[f"up_{tag}"] = pack_conv(getattr(self, f"upsampling{tag[:-1]}")[0], act=ACT_SILU)
-                p[f"tail_{tag}"] = pack_conv(getattr(self, f"tail{tag}"))
+                p[f"up_{tag}"] = pack_shuffle_tail(getattr(self, f"upsampling{tag[:-1]}")[0], getattr(self, f"tail{tag}"),
+                                                   r)
             self._esm = (tok, p)
         return self._esm[1]
 
@@ -251,8 +253,8 @@ class _ESMUpsampler(nn.Module):
                 x = run_conv(ctx, p["to_feat"], [x], tag=f"{me}.to_feat")
                 for blk in self.blocks:
                     x = blk.emit(ctx, x)
-            x = run_conv(ctx, p[f"up_{tag}"], [x], shuffle=r, tag=f"{me}.upsampling{tag[:-1]}.0")
-            x = run_conv(ctx, p[f"tail_{tag}"], [x], tag=f"{me}.tail{tag}")
+            # upsampling (1x1 -> PixelShuffle -> SiLU) + tail (3x3 -> 1): one launch
+            x = run_shuffle_tail(ctx, x, p[f"up_{tag}"], tag=f"{me}.upsampling{tag[:-1]}+tail{tag}")
             last = i == n - 1
             epi = dict(up=prev, up_f=r, post_scale=final_scale if last else 1.0)
             if scaled_copies is not None and not last:

@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
     constexpr int TAPS = KDT * KT * KT;
     constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
     constexpr int TW = 16 * NT;
-    constexpr int NC = KS > 1 ? 1 : (MT * NT >= 4 ? 1 : 4 / (MT * NT));  // accumulation chains per tile
+    constexpr int NC = MT * NT >= 4 ? 1 : 4 / (MT * NT);  // accumulation chains per tile
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -223,12 +223,19 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
                                         av[t][k][mt], bv[t][k][nt], accs[(t * CK + k) % NC][mt][nt], 0, 0, 0);
                 }
             } else {
-                // K-split: wave w takes taps w, w + 4, ...; the column offsets are recomputed per tap
-                for (int tap = wave; tap < TAPS; tap += KS) {
+                // K-split: wave w takes taps w, w + 4, ...  The tap loop is unrolled at compile time and
+                // every load of the wave's taps is issued before the first MFMA (one memory round trip
+                // per chunk); a tap past TAPS reads zeros (kOOB row) against zero weights (past the
+                // weight buffer's range)
+                constexpr int TPW = (TAPS + KS - 1) / KS;
+                float bv[TPW][CK][NT], av[TPW][CK][MT];
+#pragma unroll
+                for (int tt = 0; tt < TPW; ++tt) {
+                    const int tap = wave + tt * KS;
                     const int td = tap / (KT * KT), th = (tap / KT) % KT, tw = tap % KT;
                     const int zi = D3 ? (TR ? zs + qd - td : zs * S - a.pd + td) : 0;
                     const int yi = TR ? ys + qh - th : ys * S - a.ph + th;
-                    const bool rok = yi >= 0 && yi < a.Hi && (!D3 || (zi >= 0 && zi < a.Di));
+                    const bool rok = tap < TAPS && yi >= 0 && yi < a.Hi && (!D3 || (zi >= 0 && zi < a.Di));
                     unsigned xo[NT];
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt) {
@@ -236,24 +243,26 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
                         const int xi = TR ? xs + qw - tw : xs * S - a.pw + tw;
                         xo[nt] = (xs < Ws && xi >= 0 && xi < a.Wi) ? 4u * xi : kOOB;
                     }
-                    float bv[CK][NT], av[CK][MT];
 #pragma unroll
                     for (int k = 0; k < CK; ++k) {
                         const int roff = rok ? 4 * ((D3 ? zi * sdk[k] : 0) + yi * shk[k]) : static_cast<int>(kOOB);
 #pragma unroll
-                        for (int nt = 0; nt < NT; ++nt) bv[k][nt] = buf_load_s(rs[k], chk[k] + xo[nt], roff);
+                        for (int nt = 0; nt < NT; ++nt) bv[tt][k][nt] = buf_load_s(rs[k], chk[k] + xo[nt], roff);
 #pragma unroll
                         for (int mt = 0; mt < MT; ++mt)
-                            av[k][mt] = buf_load_s(wrs, wlane, wchunk + 4 * ((tap * a.cin_pad + 4 * k) * a.cout_pad + mt * 16));
+                            av[tt][k][mt] = buf_load_s(wrs, wlane, wchunk + 4 * ((tap * a.cin_pad + 4 * k) * a.cout_pad + mt * 16));
                     }
+                }
+#pragma unroll
+                for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
                     for (int k = 0; k < CK; ++k)
 #pragma unroll
                         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                             for (int nt = 0; nt < NT; ++nt)
-                                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][mt], bv[k][nt], acc[mt][nt], 0, 0, 0);
-                }
+                                accs[(tt * CK + k) % NC][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    av[tt][k][mt], bv[tt][k][nt], accs[(tt * CK + k) % NC][mt][nt], 0, 0, 0);
             }
         }
 

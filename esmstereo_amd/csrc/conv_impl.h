@@ -37,6 +37,7 @@
 //            one 16-byte store per lane for r = 4).
 #pragma once
 
+#include "conv_c1.h"
 #include "conv_direct.h"
 #include "conv_rows.h"
 #include "conv_epilogue.h"
@@ -343,7 +344,8 @@ int launch_direct_sel(const esm_conv_desc& a, hipStream_t s, int nt, int ks, int
 }
 
 // Tile choice.  hint (esm_conv_desc.hint) forces one: NT | KS << 4 | C1 << 8 | DIRECT << 9 |
-// ROWS << 10 (row-streaming form, conv_rows.h) | rows-per-wave << 12 (direct form).
+// ROWS << 10 (row-streaming form, conv_rows.h) | rows-per-wave << 12 (direct form) |
+// C1T << 16 (VALU single-output-channel transposed form, conv_c1.h).
 // Automatic: single-output-channel layers take the VALU path; everything the direct form can
 // address takes it (fewest instructions per MFMA, no barriers), K-split when the grid is far
 // below one wave per SIMD; the LDS-staged form covers the rest.
@@ -352,6 +354,12 @@ int launch_geom(const esm_conv_desc& a, hipStream_t s) {
     const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
     const int MT = a.Cout > 16 ? 2 : 1;
+    if (a.hint & (1 << 16)) {  // VALU single-output-channel transposed form (conv_c1.h)
+        if constexpr (TR) {
+            if (convt_c1_ok(a)) return launch_convt_c1<D3>(a, s);
+        }
+        return arg_error("conv: c1-transposed hint not applicable");
+    }
     if (a.hint) {  // explicit tile (tuning sweeps, tests of every variant)
         const int hnt = a.hint & 15, hks = (a.hint >> 4) & 15, hc1 = (a.hint >> 8) & 1, hdir = (a.hint >> 9) & 1;
         const int hrw = (a.hint >> 12) & 15;  // direct form: rows per wave (0 = automatic)
@@ -374,6 +382,10 @@ int launch_geom(const esm_conv_desc& a, hipStream_t s) {
         }
         if (hks == 4) return MT == 1 ? launch_nt<D3, K, S, TR, 1, 4>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 4>(a, s, hnt);
         return MT == 1 ? launch_nt<D3, K, S, TR, 1, 1>(a, s, hnt) : launch_nt<D3, K, S, TR, 2, 1>(a, s, hnt);
+    }
+    // single-output-channel transposed layers (the hourglasses' last decoder step): VALU form
+    if constexpr (TR) {
+        if (convt_c1_ok(a)) return launch_convt_c1<D3>(a, s);
     }
     // row-streaming form for stride-1 layers with horizontal taps to share (1x1 layers measured
     // faster in the direct form)

@@ -15,6 +15,7 @@ int launch_normcorr(const float*, const float*, float*, float*, int, int, int, i
 int launch_regression(int, const float*, const float*, float*, int, int, int, int, hipStream_t);
 int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
+int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 
 namespace {
 thread_local std::string g_error;
@@ -29,7 +30,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7 };
 
 struct VolArgs {
     const float* L;
@@ -51,6 +52,7 @@ struct Op {
     int kind = 0;
     esm_conv_desc conv{};
     esm_smix_desc smix{};
+    esm_shuffle_tail_desc st{};
     VolArgs vol{};
     RegArgs reg{};
 };
@@ -59,6 +61,7 @@ int run_op(const Op& op, hipStream_t s) {
     switch (op.kind) {
         case kConv: return esm::launch_conv(&op.conv, s);
         case kSmix: return esm::launch_smix(&op.smix, s);
+        case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
                                    op.vol.D, op.vol.G, s);
@@ -182,6 +185,7 @@ int esm_struct_size(int which) {
         case 1: return static_cast<int>(sizeof(esm_conv_desc));
         case 2: return static_cast<int>(sizeof(esm_smix_stage));
         case 3: return static_cast<int>(sizeof(esm_smix_desc));
+        case 4: return static_cast<int>(sizeof(esm_shuffle_tail_desc));
         default: return -1;
     }
 }
@@ -210,6 +214,14 @@ int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc) {
     Op op;
     op.kind = kSmix;
     op.smix = *desc;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc) {
+    if (!desc) return esm::arg_error("plan: null shuffle_tail desc");
+    Op op;
+    op.kind = kShuffleTail;
+    op.st = *desc;
     return add_op(plan, std::move(op));
 }
 
@@ -256,6 +268,16 @@ static int next_slot(esm_plan* plan) {
     plan->issued++;
     if (plan->issued - plan->consumed > plan->ring) plan->consumed = plan->issued - plan->ring;
     return slot;
+}
+
+int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (index < 0 || index >= static_cast<int>(plan->ops.size()) || plan->ops[index].kind != kConv)
+        return esm::arg_error("plan: op is not a conv");
+    const int prev = plan->ops[index].conv.hint;
+    plan->clear_graph();
+    plan->ops[index].conv.hint = hint;
+    return prev;
 }
 
 int esm_plan_run(esm_plan* plan, void* stream) {

@@ -1,0 +1,190 @@
+// Fused ESM upsampling head: Conv2d 1x1 (nf -> nf*r*r, bias) -> PixelShuffle(r) -> SiLU ->
+// Conv2d 3x3 (nf -> 1, pad 1, bias), i.e. `upsampling{2,4}` followed by `tail{2x,4x}` of the
+// ESM upsamplers (models/ESMStereo.py:264-271,290-296 upsample4; :363-407 upsample8;
+// :455-500 upsample16; forward :301-302,311-312 and the like).
+//
+// The shuffled nf-channel map at r x the input resolution (S at KITTI: 8 x 384 x 1248 fp32,
+// 15 MB) is never written: a workgroup owns a TH x 64 tile of the 1-channel output, stages the
+// low-resolution input pixels under the tile plus a one-pixel halo and every weight in LDS with
+// one batch of loads, builds the shuffled tile + halo in LDS (a thread takes one channel of one
+// low-resolution pixel and produces its r*r sub-pixels, so the 1x1 weights are wave-uniform
+// LDS broadcasts), then runs the 3x3 conv from LDS, 4 consecutive outputs per thread and one
+// 16-byte store.  Arithmetic per element is the unfused order: bias + sum_i w*x, SiLU, then
+// bias + sum over (channel, ky, kx) of w*v.
+#include "conv_epilogue.h"
+
+namespace esm {
+namespace {
+
+constexpr int kThreads = 256;
+
+// SiLU with the hardware exp2 / reciprocal (a few ulp; the unfused epilogue uses the libm forms)
+__device__ __forceinline__ float silu_fast(float x) { return __fdividef(x, 1.0f + __expf(-x)); }
+
+template <int NF, int R, int TH, int kTW>
+struct StGeo {
+    static constexpr int LRH = TH / R + 2;  // low-res rows under tile + halo
+    static constexpr int LRW = kTW / R + 2;
+    static constexpr int MH = TH + 2, MW = kTW + 2, MWP = MW + 2;  // shuffled tile (+halo); 16-B aligned rows
+    static constexpr int NUP = NF * R * R;
+    static constexpr int WN = NUP * NF + NUP + NF * 9 + 1;  // up_w, up_b, tail_w, tail_b
+    static constexpr int XN = NF * LRH * LRW;
+    static constexpr int PIX = LRH * LRW;
+    static constexpr int PIXP = (PIX + 63) / 64 * 64;  // items per channel, padded to whole waves
+};
+
+template <int NF, int R, int TH, int kTW>
+__global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffle_tail_desc a) {
+    using G = StGeo<NF, R, TH, kTW>;
+    constexpr int LRH = G::LRH, LRW = G::LRW, MH = G::MH, MW = G::MW, MWP = G::MWP, PIX = G::PIX, PIXP = G::PIXP;
+    constexpr int NUP = G::NUP, WN = G::WN, XN = G::XN;
+    constexpr int WR = (WN + kThreads - 1) / kThreads;
+    constexpr int XR = (XN + kThreads - 1) / kThreads;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ float lr[NF][LRH][LRW];
+    __shared__ __attribute__((aligned(16))) float mid[NF][MH][MWP];
+
+    const int tid = threadIdx.x;
+    const int H = a.H, W = a.W, HO = H * R, WO = W * R;
+    const int b = blockIdx.z;
+    const int Y0 = blockIdx.y * TH, X0 = blockIdx.x * kTW;
+    const int ly0 = Y0 / R - 1, lx0 = X0 / R - 1;  // low-res pixel of lr[.][0][0]
+    const float* xb = a.x + b * a.xb;
+
+    // ---- stage (one round trip): weights and the low-res tile
+    float rw[WR], rx[XR];
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        const int i = tid + k * kThreads;
+        const float* p = i < NUP * NF ? a.up_w : i < NUP * NF + NUP ? a.up_b : i < WN - 1 ? a.tail_w : a.tail_b;
+        const int off = i < NUP * NF ? i : i < NUP * NF + NUP ? i - NUP * NF : i < WN - 1 ? i - NUP * NF - NUP : 0;
+        const bool ok = i < WN && p;
+        const float v = ok ? p[off] : 0.f;
+        rw[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int i = tid + k * kThreads;
+        const int c = i / (LRH * LRW);
+        const int rem = i - c * LRH * LRW;
+        const int yy = ly0 + rem / LRW, xx = lx0 + rem % LRW;
+        const bool ok = i < XN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+        rx[k] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < WR; ++k)
+        if (tid + k * kThreads < WN) wsh[tid + k * kThreads] = rw[k];
+#pragma unroll
+    for (int k = 0; k < XR; ++k)
+        if (tid + k * kThreads < XN) (&lr[0][0][0])[tid + k * kThreads] = rx[k];
+    __syncthreads();
+
+    // ---- shuffled tile: item = (channel c, low-res pixel), channel-major with each channel's
+    //      items padded to whole waves, so c (and every 1x1 weight a wave reads) is wave-uniform
+    const float* upw = wsh;
+    const float* upb = wsh + NUP * NF;
+    const float* tw = wsh + NUP * NF + NUP;
+    const float tb = a.tail_b ? wsh[WN - 1] : 0.f;
+    for (int i = tid; i < NF * PIXP; i += kThreads) {
+        const int c = __builtin_amdgcn_readfirstlane(i / PIXP);
+        const int rem = i - c * PIXP;
+        if (rem >= PIX) continue;
+        const int py = rem / LRW, px = rem - (rem / LRW) * LRW;
+        float xv[NF];
+#pragma unroll
+        for (int j = 0; j < NF; ++j) xv[j] = lr[j][py][px];
+#pragma unroll
+        for (int sy = 0; sy < R; ++sy)
+#pragma unroll
+            for (int sx = 0; sx < R; ++sx) {
+                // shuffled output position, in tile coordinates (tile row 0 = output row Y0 - 1)
+                const int Y = (ly0 + py) * R + sy, X = (lx0 + px) * R + sx;
+                const int my = Y - (Y0 - 1), mx = X - (X0 - 1);
+                if (my < 0 || my >= MH || mx < 0 || mx >= MW) continue;
+                float v = 0.f;  // zero padding of the 3x3 conv outside the shuffled map
+                if (Y >= 0 && Y < HO && X >= 0 && X < WO) {
+                    const float* wr = upw + (c * R * R + sy * R + sx) * NF;  // wave-uniform row
+                    float s = 0.f;
+#pragma unroll
+                    for (int j = 0; j < NF; ++j) s += wr[j] * xv[j];
+                    v = silu_fast(s + upb[c * R * R + sy * R + sx]);
+                }
+                mid[c][my][mx] = v;
+            }
+    }
+    __syncthreads();
+
+    // ---- 3x3 tail: thread (row, column quad)
+    constexpr int QPR = kTW / 4;  // quads per row
+    for (int q = tid; q < TH * QPR; q += kThreads) {
+        const int r = q / QPR, g = q - (q / QPR) * QPR;
+        const int oy = Y0 + r, ox = X0 + 4 * g;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+        for (int c = 0; c < NF; ++c) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                float v[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) v[j] = mid[c][r + ky][4 * g + j];
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float w = tw[(c * 3 + ky) * 3 + kx];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                }
+            }
+        }
+        if (oy >= HO) continue;
+        float* o = a.out + b * a.ob + static_cast<long long>(oy) * a.oh + ox;
+        if (ox + 3 < WO && ((reinterpret_cast<uintptr_t>(o)) & 15) == 0) {
+            *reinterpret_cast<conv::floatx4*>(o) = conv::floatx4{acc[0] + tb, acc[1] + tb, acc[2] + tb, acc[3] + tb};
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (ox + j < WO) o[j] = acc[j] + tb;
+        }
+    }
+}
+
+template <int NF, int R, int TH, int TW>
+int launch_tile(const esm_shuffle_tail_desc& a, hipStream_t s) {
+    dim3 grid(ceil_div(static_cast<long long>(a.W) * R, TW), ceil_div(static_cast<long long>(a.H) * R, TH), a.B);
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_tail: grid too large");
+    hipLaunchKernelGGL((shuffle_tail_kernel<NF, R, TH, TW>), grid, dim3(kThreads), 0, s, a);
+    return check_launch("shuffle_tail");
+}
+
+// 16 (8 for nf = 16) x 64 output tiles when that gives the chip ~one workgroup per CU, else
+// 8 x 32 tiles (4x the workgroups for the coarse stage's small output).
+template <int NF, int R>
+int launch_nr(const esm_shuffle_tail_desc& a, hipStream_t s) {
+    constexpr int TH = NF <= 8 ? 16 : 8;
+    const long long big = static_cast<long long>(ceil_div(static_cast<long long>(a.W) * R, 64)) *
+                          ceil_div(static_cast<long long>(a.H) * R, TH) * a.B;
+    return big >= 256 ? launch_tile<NF, R, TH, 64>(a, s) : launch_tile<NF, R, 8, 32>(a, s);
+}
+
+}  // namespace
+
+int launch_shuffle_tail(const esm_shuffle_tail_desc* d, hipStream_t s) {
+    if (!d) return arg_error("shuffle_tail: null descriptor");
+    const esm_shuffle_tail_desc& a = *d;
+    if (!a.x || !a.out || !a.up_w || !a.up_b || !a.tail_w) return arg_error("shuffle_tail: null pointer");
+    if (a.B <= 0 || a.H <= 0 || a.W <= 0) return arg_error("shuffle_tail: bad size");
+    if (a.xh < a.W || a.xc < static_cast<long long>(a.H) * a.xh || a.oh < static_cast<long long>(a.W) * a.r)
+        return arg_error("shuffle_tail: strides inconsistent with the extents");
+    if (a.nf == 8 && a.r == 4) return launch_nr<8, 4>(a, s);
+    if (a.nf == 8 && a.r == 2) return launch_nr<8, 2>(a, s);
+    if (a.nf == 16 && a.r == 2) return launch_nr<16, 2>(a, s);
+    if (a.nf == 16 && a.r == 4) return launch_nr<16, 4>(a, s);
+    set_error("shuffle_tail: (nf, r) must be one of (8, 2), (8, 4), (16, 2), (16, 4)");
+    return ESM_ERR_UNSUPPORTED;
+}
+
+}  // namespace esm
+
+extern "C" int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream) {
+    return esm::launch_shuffle_tail(desc, esm::as_stream(stream));
+}

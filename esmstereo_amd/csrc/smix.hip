@@ -5,7 +5,7 @@
 //              SplitPointMlp :23-37, channel shuffle 'b (g d) -> b (d g)', g = 8
 //   [optional] + res                                              (FMBlock `net(x) + x` :130)
 // One thread owns one pixel and keeps its C (8 or 16) channels in registers.  All weights
-// (<= 1.4K floats) and, with the depthwise conv, the 16x16 pixel tile plus its (K-1)/2 halo
+// (<= 1.4K floats) and, with the depthwise conv, the 8x16 pixel tile plus its (K-1)/2 halo
 // are staged in LDS by one batch of loads at kernel start; the math then reads weights as
 // LDS broadcasts (no dependent scalar-load chains).
 #include "common.h"
@@ -13,7 +13,7 @@
 namespace esm {
 namespace {
 
-constexpr int kTileH = 16;
+constexpr int kTileH = 8;
 constexpr int kTileW = 16;
 constexpr int kThreads = kTileH * kTileW;
 
@@ -72,17 +72,17 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict
     for (int c = 0; c < C; ++c) t[c] = o[c];
 }
 
-__device__ __forceinline__ void stage_copy(float* dst, const float* __restrict__ src, int n, int tid) {
-    for (int i = tid; i < n; i += kThreads) dst[i] = src[i];
-}
-
 template <int C, int K>
 __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
     using Lyt = SmixLayout<C>;
     constexpr int R = K / 2;
     constexpr int LH = kTileH + 2 * R;
     constexpr int LW = kTileW + 2 * R;
-    constexpr int NW = ESM_SMIX_MAX_STAGES * Lyt::STAGE + (K > 1 ? C * K * K + C : 0);
+    constexpr int DWO = ESM_SMIX_MAX_STAGES * Lyt::STAGE;
+    constexpr int NW = DWO + (K > 1 ? C * K * K + C : 0);
+    constexpr int NT = (K > 1) ? C * LH * LW : 1;
+    constexpr int NWR = (NW + kThreads - 1) / kThreads;
+    constexpr int NTR = (NT + kThreads - 1) / kThreads;
     __shared__ float wsh[NW];
     __shared__ float tile[(K > 1) ? C : 1][(K > 1) ? LH : 1][(K > 1) ? LW + 1 : 1];
     const int tid = threadIdx.x;
@@ -94,28 +94,61 @@ __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
 
-    // ---- one staging phase: weights of every stage (+ depthwise), the pixel tile with halo
-    for (int s = 0; s < a.nstages; ++s) {
-        float* d = wsh + s * Lyt::STAGE;
-        const esm_smix_stage& st = a.stage[s];
-        stage_copy(d + Lyt::LN, st.ln_w, C, tid);
-        stage_copy(d + Lyt::F0W, st.fc0_w, C * Lyt::H2, tid);
-        stage_copy(d + Lyt::F0B, st.fc0_b, C, tid);
-        stage_copy(d + Lyt::F2W, st.fc2_w, Lyt::H2 * C, tid);
-        stage_copy(d + Lyt::F2B, st.fc2_b, Lyt::H2, tid);
+    // ---- one staging phase: every weight (both stages + depthwise) and the pixel tile with halo,
+    //      all loads in flight together, then the LDS stores
+    // weight element i of the LDS image: stage s (ln | fc0_w | fc0_b | fc2_w | fc2_b), then the
+    // depthwise weights and bias; every pointer is a kernel argument, so the select is scalar
+    auto weight_at = [&](int i) -> float {
+        const float* p = nullptr;
+        int off = 0;
+#pragma unroll
+        for (int st = 0; st < ESM_SMIX_MAX_STAGES; ++st) {
+            const esm_smix_stage& g = a.stage[st];
+            const int j = i - st * Lyt::STAGE;
+            if (st < a.nstages && j >= 0 && j < Lyt::STAGE) {
+                p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
+                off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
+            }
+        }
+        if (K > 1 && i >= DWO) {
+            p = i < DWO + C * K * K ? a.dw_w : a.dw_b;
+            off = i - (i < DWO + C * K * K ? DWO : DWO + C * K * K);
+        }
+        return p ? p[off] : 0.f;
+    };
+    float rw[NWR];
+#pragma unroll
+    for (int k = 0; k < NWR; ++k) {
+        const int i = tid + k * kThreads;
+        rw[k] = i < NW ? weight_at(i) : 0.f;
     }
-    constexpr int DWO = ESM_SMIX_MAX_STAGES * Lyt::STAGE;
-    if (K > 1) {
-        stage_copy(wsh + DWO, a.dw_w, C * K * K, tid);
-        stage_copy(wsh + DWO + C * K * K, a.dw_b, C, tid);
-        for (int i = tid; i < C * LH * LW; i += kThreads) {
+    float rt[NTR];
+    if constexpr (K > 1) {
+#pragma unroll
+        for (int k = 0; k < NTR; ++k) {
+            const int i = tid + k * kThreads;
             const int c = i / (LH * LW);
             const int rem = i - c * LH * LW;
             const int ly = rem / LW, lx = rem - (rem / LW) * LW;
             const int gy = y0 + ly - R, gx = x0 + lx - R;
-            const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const bool ok = i < NT && gy >= 0 && gy < H && gx >= 0 && gx < W;
             const float v = xb[ok ? c * plane + gy * W + gx : 0];
-            tile[c][ly][lx] = ok ? v : 0.f;
+            rt[k] = ok ? v : 0.f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NWR; ++k)
+        if (tid + k * kThreads < NW) wsh[tid + k * kThreads] = rw[k];
+    if constexpr (K > 1) {
+#pragma unroll
+        for (int k = 0; k < NTR; ++k) {
+            const int i = tid + k * kThreads;
+            if (i < NT) {
+                const int c = i / (LH * LW);
+                const int rem = i - c * LH * LW;
+                const int ly = rem / LW, lx = rem - (rem / LW) * LW;
+                tile[c][ly][lx] = rt[k];
+            }
         }
     }
     __syncthreads();

@@ -13,15 +13,17 @@ compiled whole-hot-path plan run the very same kernels with the very same fusion
 from __future__ import annotations
 
 import ctypes
+import json
+import os
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, ACT_SILU, EsmConvDesc, EsmSmixDesc, check, lib
+from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, ACT_SILU, EsmConvDesc, EsmShuffleTailDesc, EsmSmixDesc, check, lib
 
-__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
+__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -224,6 +226,12 @@ class Ctx:
         else:
             check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
 
+    def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
+        else:
+            check(lib.esm_shuffle_tail_f32(ctypes.byref(d), self.stream), "shuffle_tail")
+
     def gwc(self, L, R, att, V, B, C, H, W, D, G) -> None:
         self.meta.append(dict(name="gwc_volume", kind="gwc", flops=2 * B * C * D * H * W,
                               bytes=4 * B * (2 * C * H * W + G * D * H * W + (G * H * W if att is not None else 0)),
@@ -276,6 +284,24 @@ class Ctx:
 
 
 # ----------------------------------------------------------------------------- ops
+
+
+# Measured tile choices (scripts/autotune.py on MI355X, in the hot path's own launch sequence):
+# shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
+TUNED_HINTS: Dict[str, int] = {}
+if os.path.exists(_TUNED_PATH) and not os.environ.get("ESM_NO_TUNED"):
+    with open(_TUNED_PATH) as _f:
+        TUNED_HINTS = {k: int(v) for k, v in json.load(_f).get("hints", {}).items()}
+
+
+def conv_key(d: EsmConvDesc, nd: int) -> str:
+    """Shape key of a conv launch: geometry, source channel split, batch, input extent and the
+    epilogue features that change the store path."""
+    cins = "+".join(str(d.src[i].C) for i in range(d.nsrc))
+    return (f"{nd}d{'T' if d.transposed else ''} k{d.kh}s{d.stride}p{d.ph} {cins}->{d.Cout} B{d.B} "
+            f"{d.Di}x{d.Hi}x{d.Wi} sh{d.shuffle}{'u' if d.up else ''}{'m' if d.mul else ''}"
+            f"{'r' if d.res else ''}{'2' if d.out2 else ''}")
 
 
 def _spatial(t: torch.Tensor, nd: int) -> Tuple[int, int, int]:
@@ -379,13 +405,14 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
         if d.up_h * up_f != Ho or d.up_w * up_f != Wo:
             raise ValueError("conv: bilinear source extent x factor must equal the output extent")
     d.post_scale = float(post_scale)
-    d.hint = int(hint)
     if out2 is not None:
         require_device(out2, "conv out2")
         if out2.stride() != out.stride() or out2.shape != out.shape:
             raise ValueError("conv: out2 must have the output's shape and strides")
         d.out2 = out2.data_ptr()
         d.post_scale2 = float(post_scale2)
+    key = conv_key(d, nd)
+    d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd
     if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap
@@ -398,7 +425,7 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
     ctx.meta.append(dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
                          shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
                                f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
-                         reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2)))
+                         reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint))
     ctx.conv(d)
     return out
 
@@ -447,4 +474,60 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
                          bytes=4 * npix * C * (3 if res is not None else 2), shape=f"C{C} {H}x{W} dw{d.dw_k}",
                          reads=_spans(x, res), writes=_spans(out)))
     ctx.smix(d)
+    return out
+
+
+@dataclass
+class PackedShuffleTail:
+    """``upsampling`` (Conv2d 1x1 + PixelShuffle + SiLU) and ``tail`` (Conv2d 3x3 -> 1) weights."""
+
+    up_w: torch.Tensor
+    up_b: torch.Tensor
+    tail_w: torch.Tensor
+    tail_b: Optional[torch.Tensor]
+    nf: int
+    r: int
+
+
+def pack_shuffle_tail(up: torch.nn.Conv2d, tail: torch.nn.Conv2d, r: int) -> PackedShuffleTail:
+    nf = int(tail.weight.shape[1])
+    if tuple(up.weight.shape) != (nf * r * r, nf, 1, 1) or up.bias is None:
+        raise ValueError("shuffle_tail: upsampling must be Conv2d(nf, nf*r*r, 1) with bias")
+    if tuple(tail.weight.shape) != (1, nf, 3, 3) or tuple(tail.padding) != (1, 1) or tuple(tail.stride) != (1, 1):
+        raise ValueError("shuffle_tail: tail must be Conv2d(nf, 1, 3, 1, 1)")
+    return PackedShuffleTail(up.weight.detach().float().reshape(nf * r * r, nf).contiguous(),
+                             up.bias.detach().float().contiguous(),
+                             tail.weight.detach().float().reshape(nf, 3, 3).contiguous(),
+                             tail.bias.detach().float().contiguous() if tail.bias is not None else None, nf, int(r))
+
+
+def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optional[torch.Tensor] = None,
+                     tag: str = "shuffle_tail") -> torch.Tensor:
+    """``tail(SiLU(PixelShuffle(r)(up(x))))`` as one launch (``esm_shuffle_tail_f32``): the
+    ``upsampling`` + ``tail`` pair of the ESM upsamplers (models/ESMStereo.py:264-271,301-302)."""
+    require_device(x, "shuffle_tail input")
+    B, nf, H, W = (int(v) for v in x.shape)
+    r = p.r
+    if nf != p.nf:
+        raise RuntimeError(f"shuffle_tail: input has {nf} channels, layer expects {p.nf}")
+    if out is None:
+        out = ctx.empty(B, 1, H * r, W * r)
+    require_device(out, "shuffle_tail output")
+    if tuple(out.shape) != (B, 1, H * r, W * r):
+        raise ValueError("shuffle_tail: output must be [B, 1, r*H, r*W]")
+    require_on(x.device, "shuffle_tail", x, out, p.up_w, p.up_b, p.tail_w, p.tail_b)
+    d = EsmShuffleTailDesc()
+    d.x = x.data_ptr()
+    d.xb, d.xc, d.xh = x.stride(0), x.stride(1), x.stride(2)
+    d.up_w, d.up_b, d.tail_w = p.up_w.data_ptr(), p.up_b.data_ptr(), p.tail_w.data_ptr()
+    d.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
+    d.out = out.data_ptr()
+    d.ob, d.oh = out.stride(0), out.stride(2)
+    d.B, d.nf, d.H, d.W, d.r = B, nf, H, W, r
+    ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b)
+    npix = B * H * W * r * r
+    ctx.meta.append(dict(name=tag, kind="shuffle_tail", flops=2 * npix * nf * (1 + 9),
+                         bytes=4 * (B * nf * H * W + npix), shape=f"nf{nf} r{r} in {H}x{W} out {H * r}x{W * r}",
+                         reads=_spans(x), writes=_spans(out)))
+    ctx.shuffle_tail(d)
     return out

@@ -22,6 +22,10 @@
  *   esm_smix_f32              models/shufflemixer.py:23-112 LayerNorm('BiasFree') +
  *                             SplitPointMlp + channel shuffle + residual, optionally preceded
  *                             by the depthwise 7x7 `spatial` conv
+ *   esm_shuffle_tail_f32      models/ESMStereo.py:264-271,290-302,311-312 (and the upsample8 /
+ *                             upsample16 twins): `upsampling` (Conv2d 1x1 nf -> nf*r*r + bias,
+ *                             PixelShuffle(r), SiLU) followed by `tail` (Conv2d 3x3 nf -> 1 +
+ *                             bias) as one kernel; the shuffled map is never materialised
  *   esm_plan_*                the orchestration of models/ESMStereo.py:700-745 as a native
  *                             launch list, optionally replayed as one hipGraph
  */
@@ -92,7 +96,8 @@ typedef struct {
     int64_t ob, oc, od, oh;
     const float* up;
     int32_t up_h, up_w, up_f;
-    int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 12
+    int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 10 |
+                     rows-per-wave << 12 | C1T << 16
                      (tuning sweeps / tests; see conv_impl.h launch_geom) */
     int64_t ub, uh;
     float post_scale;
@@ -126,10 +131,27 @@ typedef struct {
     int32_t B, C, H, W;
 } esm_smix_desc;
 
+/* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,
+ * silu(pixel_shuffle(conv1x1(up_w, x) + up_b, r))), zero padding 1.  (nf, r) in
+ * {(8,2), (8,4), (16,2), (16,4)}.  x: [B, nf, H, W] with strides xb, xc, xh (innermost 1);
+ * out: [B, 1, r*H, r*W] with strides ob, oh.  tail_b may be NULL (no bias). */
+typedef struct {
+    const float* x;
+    int64_t xb, xc, xh;
+    const float* up_w;   /* [nf*r*r][nf] */
+    const float* up_b;   /* [nf*r*r] */
+    const float* tail_w; /* [nf][3][3] */
+    const float* tail_b; /* [1] or NULL */
+    float* out;
+    int64_t ob, oh;
+    int32_t B, nf, H, W, r;
+    int32_t reserved;
+} esm_shuffle_tail_desc;
+
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc; -1 for an unknown id. */
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc; -1 for an unknown id. */
 int esm_struct_size(int which);
 
 int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* V, int B, int C, int H, int W,
@@ -145,6 +167,7 @@ int esm_topk2_regression_f32(const float* cost, const float* samples, float* out
                              void* stream);
 int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
+int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
 
 /* ---- native launch plan (the hot path as one replayable unit) ---- */
 typedef struct esm_plan esm_plan;
@@ -152,6 +175,7 @@ esm_plan* esm_plan_create(void);
 void esm_plan_destroy(esm_plan* plan);
 int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
+int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
@@ -161,8 +185,12 @@ int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float*
 /* kind 0 = disparity_regression, 1 = regression_topk k=2 */
 int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
 int esm_plan_num_ops(const esm_plan* plan);
-/* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression */
+/* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
+ * 7 = shuffle_tail */
 int esm_plan_op_kind(const esm_plan* plan, int index);
+/* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
+ * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */
+int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint);
 int esm_plan_run(esm_plan* plan, void* stream);
 /* Capture the launch list into a hipGraph (instantiated once; replays are cheap). */
 int esm_plan_graph_build(esm_plan* plan, void* stream);

@@ -15,16 +15,17 @@ import re
 
 
 def short(name: str) -> str:
-    m = re.search(r"conv_kernel<(.*?)>\(", name)
+    m = re.search(r"(\w*conv\w*_kernel)<(.*?)>\(", name)
     if m:
-        return "conv<" + m.group(1).replace("true", "1").replace("false", "0").replace(" ", "") + ">"
-    return re.sub(r"\(.*", "", name)[:60]
+        return m.group(1) + "<" + m.group(2).replace("true", "1").replace("false", "0").replace(" ", "") + ">"
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"\(.*", "", name)[:90]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--top", type=int, default=400)
     args = ap.parse_args()
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(args.dir, "**", "*counter_collection.csv"), recursive=True):

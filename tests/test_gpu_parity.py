@@ -264,6 +264,47 @@ def test_conv_c1_hint():
         run_conv(Ctx(DEV), p, [x.to(DEV)], hint=0x3)
 
 
+@pytest.mark.parametrize("nd,cin", [(2, 16), (2, 32), (2, 8), (2, 24), (3, 12), (3, 24), (3, 32), (3, 8)])
+def test_convt_c1_form(nd, cin):
+    """Single-output-channel ConvTranspose k4 s2 p1 on the VALU form (conv_c1.h), automatic and
+    forced (hint 1 << 16), ragged extents (not multiples of the 16 x 64 tile), vs fp64 torch;
+    rel <= 1e-5."""
+    conv, _ = _mk(nd, cin, 1, 4, 2, 1, transposed=True, bn=False, seed=11)
+    shape = (2, cin, 5, 9, 37) if nd == 3 else (2, cin, 13, 45)
+    x = torch.randn(*shape)
+    ref = _ref_conv([x], conv, None, ACT_NONE)
+    p = pk(conv, None, ACT_NONE)
+    for h in (0, 1 << 16):
+        assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
+    if nd == 2:  # the up_refinement epilogue: + bilinear(prev, x2), x4 store, unscaled copy
+        prev = torch.randn(2, 1, 13, 45)
+        cp = torch.empty(2, 1, 26, 90, device=DEV)
+        y = run_conv(Ctx(DEV), p, [x.to(DEV)], up=prev.to(DEV), up_f=2, post_scale=4.0, out2=cp, post_scale2=1.0)
+        r2 = _ref_conv([x], conv, None, ACT_NONE, up=prev, up_f=2)
+        assert rel(y, r2 * 4) < 1e-5 and rel(cp, r2) < 1e-5
+    with pytest.raises(E.EsmError):  # not a single-output-channel transposed layer
+        c2, b2 = _mk(nd, cin, 4, 4, 2, 1, transposed=True, seed=12)
+        run_conv(Ctx(DEV), pk(c2, b2, ACT_GELU), [x.to(DEV)], hint=1 << 16)
+
+
+@pytest.mark.parametrize("nf,r,H,W", [(8, 4, 24, 78), (8, 4, 7, 21), (8, 2, 13, 29), (16, 2, 24, 78), (16, 2, 5, 9),
+                                      (16, 4, 6, 17)])
+def test_shuffle_tail(nf, r, H, W):
+    """upsampling (1x1 + PixelShuffle + SiLU) fused with tail (3x3 -> 1) vs fp64 torch of the
+    reference's two modules (models/ESMStereo.py:264-271,301-302); rel <= 1e-5."""
+    from esmstereo_amd.engine import pack_shuffle_tail, run_shuffle_tail
+    torch.manual_seed(nf * 100 + r)
+    up = torch.nn.Conv2d(nf, nf * r * r, 1, 1, 0)
+    tail = torch.nn.Conv2d(nf, 1, 3, 1, 1)
+    x = torch.randn(2, nf, H, W)
+    ref = F.conv2d(F.silu(F.pixel_shuffle(F.conv2d(x.double(), up.weight.double(), up.bias.double()), r)),
+                   tail.weight.double(), tail.bias.double(), 1, 1).float()
+    p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), r)
+    y = run_shuffle_tail(Ctx(DEV), x.to(DEV), p)
+    assert y.shape == (2, 1, H * r, W * r)
+    assert rel(y, ref) < 1e-5
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
