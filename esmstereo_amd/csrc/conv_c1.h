@@ -87,6 +87,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
         const float v = a.w[ok ? ((static_cast<long long>(cls) * TAPS + tap) * a.cin_pad + c) * a.cout_pad : 0];
         rw[k] = ok ? v : 0.f;
     }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
 #pragma unroll
     for (int k = 0; k < XR; ++k) {
         const int i = tid + k * kC1Threads;

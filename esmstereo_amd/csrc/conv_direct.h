@@ -211,6 +211,9 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
 #pragma unroll
                             for (int mt = 0; mt < MT; ++mt)
                                 av[t][k][mt] = buf_load_s(wrs, wlane, wchunk + 4 * (((td * PT + t) * a.cin_pad + 4 * k) * a.cout_pad + mt * 16));
+                    // every load above the first MFMA: left alone the scheduler sinks each load next
+                    // to its use and the wave pays one memory round trip per load (scripts/isa_waits.py)
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int t = 0; t < PT; ++t)
 #pragma unroll
@@ -253,6 +256,7 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
                             av[tt][k][mt] = buf_load_s(wrs, wlane, wchunk + 4 * ((tap * a.cin_pad + 4 * k) * a.cout_pad + mt * 16));
                     }
                 }
+                __builtin_amdgcn_sched_barrier(0);  // all loads issued before the first MFMA
 #pragma unroll
                 for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll

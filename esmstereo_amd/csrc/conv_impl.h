@@ -243,11 +243,13 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const esm_conv_desc a) {
     };
 
     load_chunk(0);
+    __builtin_amdgcn_sched_barrier(0);
     for (int c0 = 0; c0 < a.Cin; c0 += CC) {
         __syncthreads();  // every wave is done reading the previous chunk
         store_chunk();
         __syncthreads();
         if (c0 + CC < a.Cin) load_chunk(c0 + CC);  // in flight during this chunk's math
+        __builtin_amdgcn_sched_barrier(0);          // ... not sunk below it by the scheduler
         if constexpr (KS == 1) {
             // one row of KT taps per iteration: enough independent LDS reads to cover their latency
             // without hoisting the whole chunk's operands (which would exhaust the VGPRs)

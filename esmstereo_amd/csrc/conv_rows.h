@@ -122,14 +122,26 @@ __global__ void __launch_bounds__(kDirectThreads) rconv_kernel(const esm_conv_de
     float bcur[NB];
     load_row(bcur, y_first, 0);
     const EpiConst<MT> ec = conv_epi_const<MT>(a, cob, lane);
-    // weights of this workgroup's couts -> LDS (once)
+    // weights of this workgroup's couts -> LDS (once): cin_pad is 16 on this form (rows_ok), so the
+    // count is a compile-time constant and every load is issued before the first LDS store
     {
-        const int n4 = TAPS * a.cin_pad * (16 * MT / 4);  // float4 count
-        for (int i = threadIdx.x; i < n4; i += kDirectThreads) {
-            const int row = i / (4 * MT);  // tap * cin_pad + c
+        constexpr int N4 = TAPS * 16 * (16 * MT / 4);  // float4 count
+        constexpr int R4 = (N4 + kDirectThreads - 1) / kDirectThreads;
+        floatx4 rw[R4];
+#pragma unroll
+        for (int k = 0; k < R4; ++k) {
+            const int i = min(static_cast<int>(threadIdx.x) + k * kDirectThreads, N4 - 1);  // clamped: no branch
+            const int row = i / (4 * MT);  // tap * 16 + c
             const int q4 = i - row * (4 * MT);
-            const floatx4 v = *reinterpret_cast<const floatx4*>(a.w + static_cast<long long>(row) * a.cout_pad + cob + 4 * q4);
-            *reinterpret_cast<floatx4*>(wl + row * WROW + 4 * q4) = v;
+            rw[k] = *reinterpret_cast<const floatx4*>(a.w + static_cast<long long>(row) * a.cout_pad + cob + 4 * q4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < R4; ++k) {
+            const int i = threadIdx.x + k * kDirectThreads;
+            const int row = i / (4 * MT);
+            const int q4 = i - row * (4 * MT);
+            if (i < N4) *reinterpret_cast<floatx4*>(wl + row * WROW + 4 * q4) = rw[k];
         }
     }
 
@@ -137,6 +149,9 @@ __global__ void __launch_bounds__(kDirectThreads) rconv_kernel(const esm_conv_de
     for (int ys = y_first; ys < y_end; ys += 4) {
         float bnext[NB];
         load_row(bnext, ys + 4, 0);  // next row's operands in flight during this row's MFMAs
+        // keep every load of the next row above this row's MFMAs: left alone the scheduler sinks
+        // each load next to its use and the wave pays one memory round trip per load
+        __builtin_amdgcn_sched_barrier(0);
 
         floatx4 accs[NC][MT];
 #pragma unroll

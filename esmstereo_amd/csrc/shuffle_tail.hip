@@ -58,9 +58,11 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
         const int i = tid + k * kThreads;
         const float* p = i < NUP * NF ? a.up_w : i < NUP * NF + NUP ? a.up_b : i < WN - 1 ? a.tail_w : a.tail_b;
         const int off = i < NUP * NF ? i : i < NUP * NF + NUP ? i - NUP * NF : i < WN - 1 ? i - NUP * NF - NUP : 0;
-        const bool ok = i < WN && p;
-        const float v = ok ? p[off] : 0.f;
-        rw[k] = v;
+        // unconditional load (clamped offset) then select: a conditional load makes hipcc branch
+        // around it and wait for each one separately
+        const float* q = p ? p : a.up_w;
+        const float v = q[i < WN && p ? off : 0];
+        rw[k] = (i < WN && p) ? v : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < XR; ++k) {
@@ -72,6 +74,7 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
         const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
         rx[k] = ok ? v : 0.f;
     }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
 #pragma unroll
     for (int k = 0; k < WR; ++k)
         if (tid + k * kThreads < WN) wsh[tid + k * kThreads] = rw[k];

@@ -4,18 +4,20 @@
 //              LN = BiasFree_LayerNorm over C (mean IS subtracted) :47-62
 //              SplitPointMlp :23-37, channel shuffle 'b (g d) -> b (d g)', g = 8
 //   [optional] + res                                              (FMBlock `net(x) + x` :130)
-// One thread owns one pixel and keeps its C (8 or 16) channels in registers.  All weights
-// (<= 1.4K floats) and, with the depthwise conv, the 8x16 pixel tile plus its (K-1)/2 halo
-// are staged in LDS by one batch of loads at kernel start; the math then reads weights as
-// LDS broadcasts (no dependent scalar-load chains).
+// A workgroup owns a 4x16 pixel tile (the coarse 1/16-res map is small: many small workgroups
+// spread it over the chip).  All weights (<= 1.4K floats) and, with the depthwise conv, the tile
+// plus its (K-1)/2 halo are staged in LDS by one batch of loads at kernel start.  The depthwise
+// conv runs on all 256 threads (4 channel groups x 64 pixels, weights as LDS broadcasts); the
+// per-pixel LN/MLP chain then runs on one thread per pixel with its C channels in registers.
 #include "common.h"
 
 namespace esm {
 namespace {
 
-constexpr int kTileH = 8;
+constexpr int kTileH = 4;
 constexpr int kTileW = 16;
-constexpr int kThreads = kTileH * kTileW;
+constexpr int kPix = kTileH * kTileW;  // pixels per workgroup
+constexpr int kThreads = 256;          // depthwise: 4 channel groups x 64 pixels; LN/MLP: 64 pixels
 
 template <int C>
 struct SmixLayout {
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
     const int H = a.H, W = a.W;
     const int b = blockIdx.z;
     const int y0 = blockIdx.y * kTileH, x0 = blockIdx.x * kTileW;
-    const int ty = tid / kTileW, tx = tid - (tid / kTileW) * kTileW;
+    const int ty = (tid % kPix) / kTileW, tx = tid % kTileW;  // pixel of the LN/MLP phase (tid < kPix)
     const int y = y0 + ty, x = x0 + tx;
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
@@ -114,7 +116,8 @@ __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
             p = i < DWO + C * K * K ? a.dw_w : a.dw_b;
             off = i - (i < DWO + C * K * K ? DWO : DWO + C * K * K);
         }
-        return p ? p[off] : 0.f;
+        const float v = (p ? p : a.x)[p ? off : 0];  // unconditional load, then select
+        return p ? v : 0.f;
     };
     float rw[NWR];
 #pragma unroll
@@ -136,6 +139,7 @@ __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
             rt[k] = ok ? v : 0.f;
         }
     }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
 #pragma unroll
     for (int k = 0; k < NWR; ++k)
         if (tid + k * kThreads < NW) wsh[tid + k * kThreads] = rw[k];
@@ -152,21 +156,31 @@ __global__ void __launch_bounds__(kThreads) smix_kernel(const esm_smix_desc a) {
         }
     }
     __syncthreads();
-    if (y >= H || x >= W) return;
     float t[C];
-    if (K > 1) {
+    if constexpr (K > 1) {
+        // depthwise KxK: thread = (channel group, pixel); the group (C/4 channels) is wave-uniform,
+        // so the weights are LDS broadcasts; results meet their pixel's thread through LDS
+        __shared__ float dws[C][kPix];
+        const int p = tid % kPix, cg = tid / kPix;
+        const int py = p / kTileW, px = p - (p / kTileW) * kTileW;
         const float* dww = wsh + DWO;
         const float* dwb = wsh + DWO + C * K * K;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
+        for (int cc = 0; cc < C / 4; ++cc) {
+            const int c = cg * (C / 4) + cc;
             float s = 0.f;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) s += dww[(c * K + ky) * K + kx] * tile[c][ty + ky][tx + kx];
-            t[c] = s + dwb[c];
+                for (int kx = 0; kx < K; ++kx) s += dww[(c * K + ky) * K + kx] * tile[c][py + ky][px + kx];
+            dws[c][p] = s + dwb[c];
         }
+        __syncthreads();
+        if (tid >= kPix || y >= H || x >= W) return;
+#pragma unroll
+        for (int c = 0; c < C; ++c) t[c] = dws[c][tid];
     } else {
+        if (tid >= kPix || y >= H || x >= W) return;
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = xb[c * plane + y * W + x];
     }

@@ -24,7 +24,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kPix = 4;                       // pixels per thread
 constexpr int kTile = kThreads * kPix;         // flat pixels per workgroup
-constexpr int kDChunk = 8;                     // disparity planes per workgroup
+constexpr int kDChunk = 16;                    // disparity planes per workgroup
 
 template <int CPG, bool ATT, bool VEC>
 __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__ L, const float* __restrict__ R,
@@ -44,10 +44,19 @@ __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__
     // stage right pixels [p0 - (d0+dn-1), p0 + kTile - d0) for this group's channels
     const int lo = p0 - (d0 + dn - 1);
     const int span = kTile + dn - 1;
+    // every load of the thread (right segment, left pixels, att) issued as one batch with clamped
+    // addresses, then selected and stored: one memory round trip per workgroup
+    constexpr int NR = (kTile + kDChunk - 1 + kThreads - 1) / kThreads;
+    float rr[CPG][NR];
+#pragma unroll
     for (int c = 0; c < CPG; ++c)
-        for (int i = threadIdx.x; i < span; i += kThreads) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const int i = threadIdx.x + k * kThreads;
             const int p = lo + i;
-            rs[c][i] = (p >= 0 && p < HW) ? rb[static_cast<long long>(c) * HW + p] : 0.f;
+            const bool ok = i < span && p >= 0 && p < HW;
+            const float v = rb[static_cast<long long>(c) * HW + (ok ? p : 0)];
+            rr[c][k] = ok ? v : 0.f;
         }
     const int pt = p0 + threadIdx.x * kPix;
     float lv[CPG][kPix];
@@ -59,9 +68,25 @@ __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__
         const bool in = p < HW;
         xs[k] = in ? p % W : -1;
 #pragma unroll
-        for (int c = 0; c < CPG; ++c) lv[c][k] = in ? lb[static_cast<long long>(c) * HW + p] : 0.f;
-        av[k] = (ATT && in) ? att[static_cast<long long>(bg) * HW + p] : 1.f;
+        for (int c = 0; c < CPG; ++c) {
+            const float v = lb[static_cast<long long>(c) * HW + (in ? p : 0)];
+            lv[c][k] = in ? v : 0.f;
+        }
+        if (ATT) {
+            const float v = att[static_cast<long long>(bg) * HW + (in ? p : 0)];
+            av[k] = in ? v : 1.f;
+        } else {
+            av[k] = 1.f;
+        }
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < CPG; ++c)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const int i = threadIdx.x + k * kThreads;
+            if (i < span) rs[c][i] = rr[c][k];
+        }
     __syncthreads();
     float* vb = V + (static_cast<long long>(bg) * D + d0) * HW;
     const float inv = 1.0f / static_cast<float>(CPG);

@@ -13,6 +13,7 @@ pass() {
 pass 1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS &&
 pass 2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE
 rc=$?
-python3 scripts/pmc_summary.py $OUT > $OUT/summary.txt
-head -c 20000 $OUT/summary.txt | grep -A17 "shuffle_tail\|convt_c1\|smix" | head -80
+tail -3 $OUT/p1.log $OUT/p2.log
+python3 scripts/pmc_summary.py $OUT > gpurun_out/pmc_bench_summary.txt
+rm -rf $OUT/p1 $OUT/p2  # raw per-dispatch CSVs: too large to bring back
 exit $rc
