@@ -78,11 +78,13 @@ SIGNATURES = {
     "esm_conv_f32": (c_int, [POINTER(EsmConvDesc), c_void_p]),
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
+    "esm_conv_pair_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_plan_create": (c_void_p, []),
     "esm_plan_destroy": (None, [c_void_p]),
     "esm_plan_add_conv": (c_int, [c_void_p, POINTER(EsmConvDesc)]),
     "esm_plan_add_smix": (c_int, [c_void_p, POINTER(EsmSmixDesc)]),
     "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
+    "esm_plan_add_conv_pair": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),

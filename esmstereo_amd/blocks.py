@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token,
-                     run_conv, run_shuffle_tail)
+                     run_conv, run_conv_pair, run_shuffle_tail)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -99,6 +99,16 @@ def _up(cin: int, cout: int, is_3d: bool, last: bool = False) -> BasicConv:
                      stride=2)
 
 
+def _pair(ctx: Ctx, first: BasicConv, srcs: Sequence[torch.Tensor], second, second_packed: Optional[PackedConv] = None,
+          **kw) -> torch.Tensor:
+    """``second(first(cat(srcs)))`` as one fused launch where the pair has a fused form (2-D,
+    stride 1), else two launches (engine.run_conv_pair)."""
+    n0 = getattr(first, "_esm_name", "BasicConv")
+    n1 = getattr(second, "_esm_name", "conv") if second is not None else "conv"
+    pb = second_packed if second_packed is not None else second.packed()
+    return run_conv_pair(ctx, first.packed(), srcs, pb, tag=f"{n0}+{n1.rsplit('.', 1)[-1]}", tags=(n0, n1), **kw)
+
+
 def _crop_like(t: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
     """``t[..., :ref.D, :ref.H, :ref.W]`` (ESMStereo.py:172,177,230) as a strided view."""
     idx = (slice(None), slice(None)) + tuple(slice(0, n) for n in ref.shape[2:])
@@ -127,8 +137,7 @@ class _Hourglass(nn.Module):
         c2 = self.conv2[1].emit(ctx, [self.conv2[0].emit(ctx, [c1])])
         c3 = self.conv3[1].emit(ctx, [self.conv3[0].emit(ctx, [c2])])
         u3 = self.conv3_up.emit(ctx, [c3])
-        a0 = self.agg_0[0].emit(ctx, [_crop_like(u3, c2), c2, *extra0])
-        a0 = self.agg_0[1].emit(ctx, [a0])
+        a0 = _pair(ctx, self.agg_0[0], [_crop_like(u3, c2), c2, *extra0], self.agg_0[1])
         u2 = self.conv2_up.emit(ctx, [a0])
         if crop1:
             u2 = _crop_like(u2, c1)
@@ -136,8 +145,7 @@ class _Hourglass(nn.Module):
             # the reference concat at ESMStereo.py:234 does not crop and raises here
             raise RuntimeError(f"Sizes of tensors must match except in dimension 1. Expected size "
                                f"{u2.shape[2]} but got size {c1.shape[2]} for tensor number 1 in the list.")
-        a1 = self.agg_1[0].emit(ctx, [u2, c1, *extra1])
-        a1 = self.agg_1[1].emit(ctx, [a1])
+        a1 = _pair(ctx, self.agg_1[0], [u2, c1, *extra1], self.agg_1[1])
         return self.conv1_up.emit(ctx, [a1], **last)
 
 
@@ -242,12 +250,11 @@ class _ESMUpsampler(nn.Module):
         n = len(self.STAGES)
         for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
             dm = getattr(self, f"dm{tag}")
-            d = prev
-            for layer in dm:
-                d = layer.emit(ctx, [d])
+            d = dm[0].emit(ctx, [prev])
+            d = _pair(ctx, dm[1], [d], dm[2])
+            d = dm[3].emit(ctx, [d])
             spx = getattr(self, f"spx_{tag}")
-            c = spx[0].emit(ctx, [d, feats[cat_i]])
-            c = run_conv(ctx, p[f"spx1_{tag}"], [c], tag=f"{me}.spx_{tag}.1")
+            c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c
             if i == 0:
                 x = run_conv(ctx, p["to_feat"], [x], tag=f"{me}.to_feat")

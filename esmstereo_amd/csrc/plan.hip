@@ -16,6 +16,9 @@ int launch_regression(int, const float*, const float*, float*, int, int, int, in
 int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
+namespace conv {
+int launch_conv_pair(const esm_conv_desc*, const esm_conv_desc*, hipStream_t);
+}
 
 namespace {
 thread_local std::string g_error;
@@ -30,7 +33,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8 };
 
 struct VolArgs {
     const float* L;
@@ -51,6 +54,7 @@ struct RegArgs {
 struct Op {
     int kind = 0;
     esm_conv_desc conv{};
+    esm_conv_desc conv2{};
     esm_smix_desc smix{};
     esm_shuffle_tail_desc st{};
     VolArgs vol{};
@@ -62,6 +66,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kConv: return esm::launch_conv(&op.conv, s);
         case kSmix: return esm::launch_smix(&op.smix, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
+        case kConvPair: return esm::conv::launch_conv_pair(&op.conv, &op.conv2, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
                                    op.vol.D, op.vol.G, s);
@@ -222,6 +227,15 @@ int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc)
     Op op;
     op.kind = kShuffleTail;
     op.st = *desc;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b) {
+    if (!a || !b) return esm::arg_error("plan: null conv pair desc");
+    Op op;
+    op.kind = kConvPair;
+    op.conv = *a;
+    op.conv2 = *b;
     return add_op(plan, std::move(op));
 }
 

@@ -23,7 +23,7 @@ import torch
 from . import _lib
 from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, ACT_SILU, EsmConvDesc, EsmShuffleTailDesc, EsmSmixDesc, check, lib
 
-__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
+__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "run_conv_pair", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -226,6 +226,12 @@ class Ctx:
         else:
             check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
 
+    def pair(self, a: EsmConvDesc, b: EsmConvDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_conv_pair(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair")
+        else:
+            check(lib.esm_conv_pair_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair")
+
     def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
         if self.plan:
             check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
@@ -318,33 +324,57 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
     """One implicit-GEMM conv launch; ``srcs`` are concatenated along channels (each may be a
     cropped view), the epilogue applies BN/bias, activation, ``*mul``, ``+res``,
     ``+bilinear(up)``, ``*post_scale`` and an optional PixelShuffle(``shuffle``)."""
+    d, out, meta = _conv_desc(ctx, pc, srcs, out, mul=mul, res=res, up=up, up_f=up_f, post_scale=post_scale,
+                              shuffle=shuffle, out2=out2, post_scale2=post_scale2, tag=tag, hint=hint)
+    ctx.meta.append(meta)
+    ctx.conv(d)
+    return out
+
+
+def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, *,
+               mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
+               up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
+               out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
+               hint: int = 0, alloc_out: bool = True, virtual_in: Optional[Tuple[int, int, int, int]] = None):
+    """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta).
+    ``alloc_out=False`` (first conv of a fused pair) leaves the output pointer NULL."""
     nd = pc.nd
-    if not srcs or len(srcs) > _lib.MAX_SRC:
-        raise ValueError("conv: 1..3 sources")
-    x0 = srcs[0]
-    if x0.dim() != nd + 2:
-        raise ValueError(f"conv: expected a {nd + 2}-D input, got shape {tuple(x0.shape)}")
-    B = int(x0.shape[0])
-    Di, Hi, Wi = _spatial(x0, nd)
     d = EsmConvDesc()
-    cin = 0
-    for i, s in enumerate(srcs):
-        require_device(s, "conv input")
-        if s.dim() != nd + 2 or int(s.shape[0]) != B or _spatial(s, nd) != (Di, Hi, Wi):
-            # torch.cat of mismatching tensors raises RuntimeError in the reference
-            raise RuntimeError(f"Sizes of tensors must match except in dimension 1 (conv sources "
-                               f"{[tuple(t.shape) for t in srcs]})")
-        st = s.stride()
-        d.src[i].ptr = s.data_ptr()
-        d.src[i].C = int(s.shape[1])
-        d.src[i].sb, d.src[i].sc = st[0], st[1]
-        d.src[i].sd = st[2] if nd == 3 else 0
-        d.src[i].sh = st[-2]
-        cin += int(s.shape[1])
+    if virtual_in is not None:  # the on-chip output of the first conv of a fused pair (never dereferenced)
+        B, cin, Hi, Wi = (int(v) for v in virtual_in)
+        Di = 1
+        dev = pc.w.device
+        d.src[0].ptr = None
+        d.src[0].C = cin
+        d.src[0].sb, d.src[0].sc, d.src[0].sh = cin * Hi * Wi, Hi * Wi, Wi
+        srcs = []
+    else:
+        if not srcs or len(srcs) > _lib.MAX_SRC:
+            raise ValueError("conv: 1..3 sources")
+        x0 = srcs[0]
+        if x0.dim() != nd + 2:
+            raise ValueError(f"conv: expected a {nd + 2}-D input, got shape {tuple(x0.shape)}")
+        dev = x0.device
+        B = int(x0.shape[0])
+        Di, Hi, Wi = _spatial(x0, nd)
+        cin = 0
+        for i, s in enumerate(srcs):
+            require_device(s, "conv input")
+            if s.dim() != nd + 2 or int(s.shape[0]) != B or _spatial(s, nd) != (Di, Hi, Wi):
+                # torch.cat of mismatching tensors raises RuntimeError in the reference
+                raise RuntimeError(f"Sizes of tensors must match except in dimension 1 (conv sources "
+                                   f"{[tuple(t.shape) for t in srcs]})")
+            st = s.stride()
+            d.src[i].ptr = s.data_ptr()
+            d.src[i].C = int(s.shape[1])
+            d.src[i].sb, d.src[i].sc = st[0], st[1]
+            d.src[i].sd = st[2] if nd == 3 else 0
+            d.src[i].sh = st[-2]
+            cin += int(s.shape[1])
     if cin != pc.cin:
         raise RuntimeError(f"conv: input has {cin} channels, layer expects {pc.cin}")
-    require_on(x0.device, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2)
-    d.nsrc = len(srcs)
+    require_on(dev, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2)
+    d.nsrc = max(1, len(srcs))
     d.B, d.Cin = B, cin
     d.Di, d.Hi, d.Wi = Di, Hi, Wi
     k, s, p = pc.k, pc.stride, pc.pad
@@ -356,7 +386,7 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
         Ho, Wo = (Hi + 2 * p - k) // s + 1, (Wi + 2 * p - k) // s + 1
         Do = (Di + 2 * p - k) // s + 1 if nd == 3 else 1
     if min(Do, Ho, Wo) <= 0:
-        raise RuntimeError(f"conv: empty output for input {tuple(x0.shape)}")
+        raise RuntimeError(f"conv: empty output for input extent {(B, cin, Di, Hi, Wi)}")
     d.Do, d.Ho, d.Wo = Do, Ho, Wo
     d.kd = k if nd == 3 else 1
     d.kh = d.kw = k
@@ -370,27 +400,28 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
     d.act = pc.act
     r = int(shuffle)
     d.shuffle = r
-    if out is None:
+    if out is None and alloc_out:
         if r > 1:
             if pc.cout % (r * r):
                 raise ValueError("pixel shuffle: Cout not divisible by r^2")
             out = ctx.empty(B, pc.cout // (r * r), Ho * r, Wo * r)
         else:
             out = ctx.empty(B, pc.cout, Do, Ho, Wo) if nd == 3 else ctx.empty(B, pc.cout, Ho, Wo)
-    require_device(out, "conv output")
-    require_on(x0.device, "conv output", out)
-    ost = out.stride()
-    d.out = out.data_ptr()
-    d.ob, d.oc = ost[0], ost[1]
-    d.od = ost[2] if nd == 3 else 0
-    d.oh = ost[-2]
+    if out is not None:
+        require_device(out, "conv output")
+        require_on(dev, "conv output", out)
+        ost = out.stride()
+        d.out = out.data_ptr()
+        d.ob, d.oc = ost[0], ost[1]
+        d.od = ost[2] if nd == 3 else 0
+        d.oh = ost[-2]
     if mul is not None:
         require_device(mul, "conv mul")
         d.mul = mul.data_ptr()
         d.mb, d.mc, d.mh = mul.stride(0), mul.stride(1), mul.stride(-2)
     if res is not None:
         require_device(res, "conv residual")
-        if tuple(res.shape) != tuple(out.shape):
+        if out is None or tuple(res.shape) != tuple(out.shape):
             raise ValueError("conv: residual shape must match the output")
         rs = res.stride()
         d.res = res.data_ptr()
@@ -422,11 +453,61 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
     in_bytes = 4 * B * cin * Di * Hi * Wi
     out_bytes = 4 * B * pc.cout * Do * Ho * Wo * (2 if out2 is not None else 1)
     extra = 4 * (res.numel() if res is not None else 0) + 4 * (mul.numel() if mul is not None else 0)
-    ctx.meta.append(dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
-                         shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
-                               f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
-                         reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint))
-    ctx.conv(d)
+    meta = dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
+                shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
+                      f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
+                reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint)
+    return d, out, meta
+
+
+# Fused pairs (esm_conv_pair_f32) are used unless ESM_NO_PAIR is set (A/B measurements).
+PAIRS_ENABLED = not os.environ.get("ESM_NO_PAIR")
+
+
+def pair_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
+    """Whether esm_conv_pair_f32 has a fused form for conv ``pa`` (over ``srcs``) then ``pb``."""
+    def plain(p):
+        return p.nd == 2 and not p.transposed and p.stride == 1 and p.k in (1, 3) and p.pad == p.k // 2
+    if not (PAIRS_ENABLED and plain(pa) and plain(pb)) or pa.cout > 32 or pb.cout > 32 or pb.cin != pa.cout:
+        return False
+    # measured (MI355X, S-K): a 3x3 -> 3x3 pair recomputes the halo rows of the first conv (each
+    # wave walks a short run of rows to keep the grid wide) and loses to two launches; 1x1 -> 3x3
+    # (cheap first conv) and 3x3 -> 1x1 (no row halo) win
+    if pa.k == 3 and pb.k == 3:
+        return False
+    cins = [int(t.shape[1]) for t in srcs]
+    if len(cins) > 1 and any(c % 4 for c in cins):
+        return False
+    n = sum(cins)
+    nk = (n + 3) // 4
+    if pa.k == 1:
+        ok_nk = nk <= 24
+    else:
+        ok_nk = nk <= 12
+    ma, mb = (2 if pa.cout > 16 else 1), (2 if pb.cout > 16 else 1)
+    taps_a, taps_b = pa.k * pa.k, pb.k * pb.k
+    nka = next(v for v in ((8, 16, 24) if pa.k == 1 else (2, 4, 8, 12)) + (999,) if v >= nk)
+    wra, wrb = (16 if ma == 1 else 48), (16 if mb == 1 else 48)
+    lds = 4 * (taps_a * 4 * nka * wra + taps_b * 16 * ma * wrb)
+    return ok_nk and lds <= 64 * 1024
+
+
+def run_conv_pair(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
+                  out: Optional[torch.Tensor] = None, *, res: Optional[torch.Tensor] = None, tag: str = "conv_pair",
+                  tags: Tuple[str, str] = ("", "")) -> torch.Tensor:
+    """``pb(pa(cat(srcs)))`` (+ ``res``) as ONE launch when a fused form exists
+    (``esm_conv_pair_f32``: the intermediate never leaves the chip), else two ``run_conv`` launches."""
+    if not pair_supported(pa, pb, srcs):
+        mid = run_conv(ctx, pa, srcs, tag=tags[0] or tag + ".a")
+        return run_conv(ctx, pb, [mid], out, res=res, tag=tags[1] or tag + ".b")
+    da, _, ma = _conv_desc(ctx, pa, srcs, alloc_out=False, tag=tag)
+    B, _, H, W = (int(v) for v in srcs[0].shape)
+    db, out, mb = _conv_desc(ctx, pb, [], out, res=res, tag=tag, virtual_in=(B, pa.cout, H, W))
+    ctx.meta.append(dict(name=tag, kind="conv_pair", flops=ma["flops"] + mb["flops"],
+                         bytes=ma["bytes"] - 4 * B * pa.cout * H * W + mb["bytes"] - 4 * B * pb.cin * H * W,
+                         shape=f"pair {ma['shape']} + {mb['shape']}", reads=ma["reads"] + _spans(res),
+                         writes=mb["writes"], key=ma["key"] + " | " + mb["key"], hint=0))
+    ctx.pair(da, db)
     return out
 
 

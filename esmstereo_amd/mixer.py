@@ -2,13 +2,13 @@
 
 Parameter names match the reference state dict (``net.0.norm1.body.weight``,
 ``net.0.mlp1.fc.0.weight``, ``net.0.spatial.weight``, ``conv.0.weight`` ...).  The forward
-of an ``FMBlock`` is five HIP launches:
+of an ``FMBlock`` is four HIP launches:
 
 1. ``smix``:  t1 = mlp1(LN1(x)) + x                                  (SMLayer 0, first half)
 2. ``smix``:  t2 = dw7(t1) -> mlp2(LN2(.)) + . -> SMLayer 1's mlp1(LN1(.)) + .
 3. ``smix``:  t3 = dw7(t2) -> mlp2(LN2(.)) + . ; t3 += x               (``net(x) + x``)
-4. ``conv``:  h  = SiLU(conv3x3(t3) + b)
-5. ``conv``:  y  = conv1x1(h) + b + t3                                (``conv(x) + x``)
+4. ``conv pair``: y = conv1x1(SiLU(conv3x3(t3) + b)) + b + t3          (``conv(x) + x``; one launch,
+   the 24-channel hidden map stays on chip)
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ from typing import List
 import torch
 import torch.nn as nn
 
-from .engine import ACT_NONE, ACT_SILU, Ctx, SmixStage, pack_conv, param_token, run_conv, run_smix
+from .engine import ACT_NONE, ACT_SILU, Ctx, SmixStage, pack_conv, param_token, run_conv_pair, run_smix
 
 __all__ = ["BiasFree_LayerNorm", "LayerNorm", "SplitPointMlp", "SMLayer", "FMBlock"]
 
@@ -119,8 +119,9 @@ class FMBlock(nn.Module):
         t1 = run_smix(ctx, x, [p["a1"]], tag=f"{me}.net.0.mlp1")
         t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"], tag=f"{me}.net.0.spatial+mlp2+net.1.mlp1")
         t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x, tag=f"{me}.net.1.spatial+mlp2+res")
-        h = run_conv(ctx, p["c0"], [t3], tag=f"{me}.conv.0")
-        return run_conv(ctx, p["c2"], [h], res=t3, tag=f"{me}.conv.2")
+        # conv.0 (3x3 + SiLU) and conv.2 (1x1) + residual: one fused launch (esm_conv_pair_f32)
+        return run_conv_pair(ctx, p["c0"], [t3], p["c2"], res=t3, tag=f"{me}.conv.0+2",
+                             tags=(f"{me}.conv.0", f"{me}.conv.2"))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.emit(Ctx(x.device), x.contiguous())

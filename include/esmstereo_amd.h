@@ -26,6 +26,10 @@
  *                             upsample16 twins): `upsampling` (Conv2d 1x1 nf -> nf*r*r + bias,
  *                             PixelShuffle(r), SiLU) followed by `tail` (Conv2d 3x3 nf -> 1 +
  *                             bias) as one kernel; the shuffled map is never materialised
+ *   esm_conv_pair_f32         two stride-1 2-D convs in one launch, the intermediate kept on chip:
+ *                             agg_0 / agg_1 of up_refinement (models/ESMStereo.py:214-218,228-235),
+ *                             spx_* (:256-259,283-286 and twins), dmNx.1 -> dmNx.2 (:250-253),
+ *                             FMBlock.conv (models/shufflemixer.py:124-131)
  *   esm_plan_*                the orchestration of models/ESMStereo.py:700-745 as a native
  *                             launch list, optionally replayed as one hipGraph
  */
@@ -168,6 +172,14 @@ int esm_topk2_regression_f32(const float* cost, const float* samples, float* out
 int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
+/* out_b = epilogue_b(conv_b(epilogue_a(conv_a(src_a)))): `a` describes the first conv (its sources,
+ * weights, BN/bias, activation; a->out is not written, a->res must be NULL), `b` the second (its
+ * src[] is ignored: its input is a's output; weights, BN/bias, activation, optional residual and
+ * post_scale, output).  Both stride 1, k in {1, 3} with same padding, 2-D, Cout <= 32 each,
+ * a->Cin <= 96 (split on 4-channel boundaries when a has several sources), no shuffle / mul / up /
+ * out2.  Returns ESM_ERR_UNSUPPORTED (no launch) for a pair without a fused form: run the two convs
+ * with esm_conv_f32 instead. */
+int esm_conv_pair_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
 
 /* ---- native launch plan (the hot path as one replayable unit) ---- */
 typedef struct esm_plan esm_plan;
@@ -176,6 +188,7 @@ void esm_plan_destroy(esm_plan* plan);
 int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
+int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
@@ -186,7 +199,7 @@ int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float*
 int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail */
+ * 7 = shuffle_tail, 8 = conv_pair */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

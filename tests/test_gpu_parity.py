@@ -305,6 +305,39 @@ def test_shuffle_tail(nf, r, H, W):
     assert rel(y, ref) < 1e-5
 
 
+@pytest.mark.parametrize("ka,kb,cins,cm,cout,act_a,act_b,res,H,W", [
+    (1, 3, (16, 16, 24), 16, 16, ACT_GELU, ACT_GELU, False, 23, 70),   # ref4x.agg_1
+    (1, 3, (16, 16, 32), 16, 16, ACT_GELU, ACT_GELU, False, 13, 29),   # ref2x.agg_0
+    (3, 3, (16, 24), 16, 8, ACT_GELU, ACT_GELU, False, 21, 45),        # spx_4x
+    (3, 3, (16,), 16, 16, ACT_GELU, ACT_GELU, False, 17, 40),          # dm.1 -> dm.2
+    (3, 1, (8,), 24, 8, ACT_SILU, ACT_NONE, True, 9, 33),              # FMBlock.conv (+ residual)
+    (1, 3, (32, 32, 32), 32, 32, ACT_GELU, ACT_GELU, False, 11, 37),   # L widths: no fused form (LDS) -> two launches
+])
+def test_conv_pair(ka, kb, cins, cm, cout, act_a, act_b, res, H, W):
+    """Fused pair (esm_conv_pair_f32) vs fp64 torch of the two layers; rel <= 1e-5.  Ragged
+    extents (tiles of 12-14 valid columns, rows not a multiple of the wave's run)."""
+    from esmstereo_amd.engine import run_conv_pair, pair_supported
+    bias_a = act_a == ACT_SILU
+    ca, ba = _mk(2, sum(cins), cm, ka, 1, ka // 2, bias=bias_a, bn=not bias_a, seed=21)
+    cb, bb = _mk(2, cm, cout, kb, 1, kb // 2, bias=res, bn=not res, seed=22)
+    xs = [torch.randn(2, c, H, W) for c in cins]
+    mid = _ref_conv(xs, ca, ba, act_a)
+    resid = torch.randn(2, cout, H, W) if res else None
+    ref = _ref_conv([mid], cb, bb, act_b, res=resid)
+    pa, pb = pk(ca, ba, act_a), pk(cb, bb, act_b)
+    assert pair_supported(pa, pb, [x.to(DEV) for x in xs]) == ((cm <= 16 or cout <= 16) and (ka == 1 or kb == 1))
+    y = run_conv_pair(Ctx(DEV), pa, [x.to(DEV) for x in xs], pb, res=resid.to(DEV) if res else None)
+    assert rel(y, ref) < 1e-5
+    if ka == 3 and kb == 3:  # the kernel itself (the host prefers two launches for this shape)
+        from esmstereo_amd.engine import _conv_desc
+        ctx = Ctx(DEV)
+        xd = [x.to(DEV) for x in xs]
+        da, _, _ = _conv_desc(ctx, pa, xd, alloc_out=False)
+        db, out, _ = _conv_desc(ctx, pb, [], virtual_in=(2, cm, H, W))
+        ctx.pair(da, db)
+        assert rel(out, ref) < 1e-5
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
