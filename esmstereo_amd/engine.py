@@ -475,6 +475,11 @@ def pair_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor])
     # (cheap first conv) and 3x3 -> 1x1 (no row halo) win
     if pa.k == 3 and pb.k == 3:
         return False
+    # 1x1 -> 3x3 wins only on the full-resolution map (ref4x.agg_1, 192x624: -3 us); on the smaller
+    # ones the pair's shorter row runs leave too few waves and it loses 1.6-2.3 us to two launches
+    B, _, H, W = (int(v) for v in srcs[0].shape)
+    if pa.k == 1 and B * H * W < 65536:
+        return False
     cins = [int(t.shape[1]) for t in srcs]
     if len(cins) > 1 and any(c % 4 for c in cins):
         return False

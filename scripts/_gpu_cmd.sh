@@ -1,1 +1,1 @@
-bash scripts/gpu_iter.sh && timeout -k 10 600 python -u scripts/autotune.py --variants S --out gpurun_out/tuned_hints.json > gpurun_out/autotune.log 2>&1; tail -2 gpurun_out/autotune.log
+timeout -k 10 300 python scripts/probe_epilogue.py --steps 50 --warmup 10 --no-cpu-baseline --no-extra > gpurun_out/probe_noact.log 2>&1; tail -3 gpurun_out/probe_noact.log | cut -c1-300
