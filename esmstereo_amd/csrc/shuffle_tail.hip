@@ -25,7 +25,11 @@ template <int NF, int R, int TH, int kTW>
 struct StGeo {
     static constexpr int LRH = TH / R + 2;  // low-res rows under tile + halo
     static constexpr int LRW = kTW / R + 2;
-    static constexpr int MH = TH + 2, MW = kTW + 2, MWP = MW + 2;  // shuffled tile (+halo); 16-B aligned rows
+    // nf = 8, r = 4 (ESMStereo-S) builds the shuffled tile with MFMA: each low-res pixel's 4x4
+    // sub-pixels land as 4 aligned columns, so its tile spans the whole low-res window (origin X0 - 4)
+    static constexpr bool MF = NF == 8 && R == 4;
+    static constexpr int MX0 = MF ? 4 : 1;  // tile column 0 = output column X0 - MX0
+    static constexpr int MH = TH + 2, MW = MF ? LRW * R : kTW + 2, MWP = MF ? MW : MW + 2;  // 16-B aligned rows
     static constexpr int NUP = NF * R * R;
     static constexpr int WN = NUP * NF + NUP + NF * 9 + 1;  // up_w, up_b, tail_w, tail_b
     static constexpr int XN = NF * LRH * LRW;
@@ -37,6 +41,7 @@ template <int NF, int R, int TH, int kTW>
 __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffle_tail_desc a) {
     using G = StGeo<NF, R, TH, kTW>;
     constexpr int LRH = G::LRH, LRW = G::LRW, MH = G::MH, MW = G::MW, MWP = G::MWP, PIX = G::PIX, PIXP = G::PIXP;
+    constexpr int MX0 = G::MX0;
     constexpr int NUP = G::NUP, WN = G::WN, XN = G::XN;
     constexpr int WR = (WN + kThreads - 1) / kThreads;
     constexpr int XR = (XN + kThreads - 1) / kThreads;
@@ -89,6 +94,50 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
     const float* upb = wsh + NUP * NF;
     const float* tw = wsh + NUP * NF + NUP;
     const float tb = a.tail_b ? wsh[WN - 1] : 0.f;
+    if constexpr (G::MF) {
+        // 1x1 conv as MFMA: M = the 16 sub-pixels (sy, sx) of one channel c, N = 16 low-res pixels,
+        // K = the 8 input channels (2 k-steps).  Lane (g, n) gets sub-pixel row sy = g, columns
+        // sx = 0..3 of low-res pixel n: one 16-byte LDS store per lane.  Wave w: channels 2w, 2w+1.
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+        float av[2][2], bias[2][4];
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) {
+            const int c = 2 * wave + ci;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) av[ci][kk] = upw[(c * 16 + n) * NF + 4 * kk + g];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bias[ci][j] = upb[c * 16 + 4 * g + j];
+        }
+        const float* lrf = &lr[0][0][0];
+#pragma unroll 1
+        for (int nt = 0; nt < (PIX + 15) / 16; ++nt) {
+            const int p = nt * 16 + n;
+            const bool pin = p < PIX;
+            const int py = p / LRW, px = p - (p / LRW) * LRW;
+            float bk[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) bk[kk] = lrf[(4 * kk + g) * PIX + (pin ? p : 0)];
+            const int Y = (ly0 + py) * R + g;
+            const int my = Y - (Y0 - 1);
+            const bool yok = Y >= 0 && Y < HO;
+            const int X = (lx0 + px) * R;  // sub-pixel column 0
+#pragma unroll
+            for (int ci = 0; ci < 2; ++ci) {
+                conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ci][0], bk[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ci][1], bk[1], acc, 0, 0, 0);
+                conv::floatx4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = silu_fast(acc[j] + bias[ci][j]);
+                    o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+                }
+                if (pin && my >= 0 && my < MH)
+                    *reinterpret_cast<conv::floatx4*>(&mid[2 * wave + ci][my][px * R]) = o;
+            }
+        }
+    } else {
     for (int i = tid; i < NF * PIXP; i += kThreads) {
         const int c = __builtin_amdgcn_readfirstlane(i / PIXP);
         const int rem = i - c * PIXP;
@@ -103,7 +152,7 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
             for (int sx = 0; sx < R; ++sx) {
                 // shuffled output position, in tile coordinates (tile row 0 = output row Y0 - 1)
                 const int Y = (ly0 + py) * R + sy, X = (lx0 + px) * R + sx;
-                const int my = Y - (Y0 - 1), mx = X - (X0 - 1);
+                const int my = Y - (Y0 - 1), mx = X - (X0 - MX0);
                 if (my < 0 || my >= MH || mx < 0 || mx >= MW) continue;
                 float v = 0.f;  // zero padding of the 3x3 conv outside the shuffled map
                 if (Y >= 0 && Y < HO && X >= 0 && X < WO) {
@@ -115,6 +164,7 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
                 }
                 mid[c][my][mx] = v;
             }
+    }
     }
     __syncthreads();
 
@@ -130,7 +180,7 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
             for (int ky = 0; ky < 3; ++ky) {
                 float v[6];
 #pragma unroll
-                for (int j = 0; j < 6; ++j) v[j] = mid[c][r + ky][4 * g + j];
+                for (int j = 0; j < 6; ++j) v[j] = mid[c][r + ky][4 * g + j + MX0 - 1];
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
                     const float w = tw[(c * 3 + ky) * 3 + kx];

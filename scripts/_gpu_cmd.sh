@@ -1,1 +1,2 @@
-timeout -k 10 300 python scripts/probe_epilogue.py --steps 50 --warmup 10 --no-cpu-baseline --no-extra > gpurun_out/probe_noact.log 2>&1; tail -3 gpurun_out/probe_noact.log | cut -c1-300
+export PYTEST_ARGS='-k shuffle_tail'
+bash scripts/gpu_iter.sh
