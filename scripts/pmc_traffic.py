@@ -22,7 +22,7 @@ import os
 import sys
 from collections import defaultdict
 
-OURS = ("conv_kernel", "smix_kernel", "gwc_kernel", "concat_kernel", "normcorr_kernel", "l2norm_kernel",
+OURS = ("esm::", "conv_kernel", "smix_kernel", "gwc_kernel", "concat_kernel", "normcorr_kernel", "l2norm_kernel",
         "dispreg_kernel", "topk2_kernel")
 
 
