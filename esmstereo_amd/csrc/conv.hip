@@ -6,6 +6,13 @@ namespace esm {
 
 int launch_conv2d(const esm_conv_desc& a, hipStream_t s);
 int launch_conv3d(const esm_conv_desc& a, hipStream_t s);
+namespace conv {
+bool stem_ok(const esm_conv_desc& a);                    // conv_stem.hip
+int launch_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
+}  // namespace conv
+
+constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
+constexpr int kHintNoStem = 1 << 18;  // automatic choice among the other forms
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -45,6 +52,14 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         (d3 && a.Do != (a.Di + 2 * a.pd - a.kd) / S + 1))
         return arg_error("conv: output extent inconsistent with kernel/stride/padding");
     if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
+    if (a.hint & kHintStem) return conv::launch_stem(a, s);
+    if (a.hint & kHintNoStem) {
+        esm_conv_desc d = a;
+        d.hint &= ~kHintNoStem;
+        return d3 ? launch_conv3d(d, s) : launch_conv2d(d, s);
+    }
+    // 8 / 12 output channels, 3x3(x3) stride 1: the 16-block MFMA form wastes no tile rows
+    if (a.hint == 0 && conv::stem_ok(a)) return conv::launch_stem(a, s);
     return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
 }
 

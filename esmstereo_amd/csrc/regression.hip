@@ -15,6 +15,7 @@ namespace esm {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kRegChunk = 16;  // cost planes loaded per round trip
 
 __global__ void __launch_bounds__(kThreads) dispreg_kernel(const float* __restrict__ cost, float* __restrict__ out,
                                                            int D, int HW, int npix) {
@@ -24,7 +25,15 @@ __global__ void __launch_bounds__(kThreads) dispreg_kernel(const float* __restri
     const int p = i - b * HW;
     const float* c = cost + static_cast<long long>(b) * D * HW + p;
     float acc = 0.f;
-    for (int d = 0; d < D; ++d) acc = acc + c[static_cast<long long>(d) * HW] * static_cast<float>(d);
+    // kRegChunk loads in flight per round trip, then the adds in d order (reference order)
+    for (int d0 = 0; d0 < D; d0 += kRegChunk) {
+        float v[kRegChunk];
+#pragma unroll
+        for (int k = 0; k < kRegChunk; ++k) v[k] = d0 + k < D ? c[static_cast<long long>(d0 + k) * HW] : 0.f;
+#pragma unroll
+        for (int k = 0; k < kRegChunk; ++k)
+            if (d0 + k < D) acc = acc + v[k] * static_cast<float>(d0 + k);
+    }
     out[i] = acc;
 }
 
@@ -40,13 +49,21 @@ __global__ void __launch_bounds__(kThreads) topk2_kernel(const float* __restrict
     float v0 = -INFINITY, v1 = -INFINITY;
     int i0 = 0, i1 = 1;
     bool have0 = false, have1 = false;
-    for (int d = 0; d < D; ++d) {
-        const float v = c[static_cast<long long>(d) * HW];
-        if (!have0 || v > v0) {
-            if (have0) { v1 = v0; i1 = i0; have1 = true; }
-            v0 = v; i0 = d; have0 = true;
-        } else if (!have1 || v > v1) {
-            v1 = v; i1 = d; have1 = true;
+    for (int d0 = 0; d0 < D; d0 += kRegChunk) {
+        float vs[kRegChunk];
+#pragma unroll
+        for (int k = 0; k < kRegChunk; ++k) vs[k] = d0 + k < D ? c[static_cast<long long>(d0 + k) * HW] : 0.f;
+#pragma unroll
+        for (int k = 0; k < kRegChunk; ++k) {
+            if (d0 + k >= D) break;
+            const float v = vs[k];
+            const int d = d0 + k;
+            if (!have0 || v > v0) {
+                if (have0) { v1 = v0; i1 = i0; have1 = true; }
+                v0 = v; i0 = d; have0 = true;
+            } else if (!have1 || v > v1) {
+                v1 = v; i1 = d; have1 = true;
+            }
         }
     }
     // softmax over (v0, v1): max is v0

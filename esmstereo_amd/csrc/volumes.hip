@@ -171,76 +171,106 @@ __global__ void __launch_bounds__(kThreads) concat_kernel(const float* __restric
     }
 }
 
-// Per-pixel L2 normalisation over channels: out[c] = x[c] / (sqrt(sum x^2) + 1e-5).
-__global__ void __launch_bounds__(kThreads) l2norm_kernel(const float* __restrict__ X, float* __restrict__ Y, int C,
-                                                          int HW, int npix) {
-    const int i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= npix) return;
-    const int b = i / HW;
-    const int p = i - b * HW;
-    const float* xb = X + static_cast<long long>(b) * C * HW + p;
-    float* yb = Y + static_cast<long long>(b) * C * HW + p;
-    float ss = 0.f;
-    for (int c = 0; c < C; ++c) {
-        const float v = xb[static_cast<long long>(c) * HW];
-        ss = ss + v * v;
-    }
-    const float n = sqrtf(ss) + 1e-05f;
-    for (int c = 0; c < C; ++c) yb[static_cast<long long>(c) * HW] = xb[static_cast<long long>(c) * HW] / n;
-}
+// Norm-correlation in one launch.  A workgroup owns one row segment [x0, x0+kNcW) of (b, y)
+// and a chunk of kNcD disparities.  It stages the left segment and the right segment
+// [x0-d0-kNcD+1, x0+kNcW-d0) of all C channels in LDS (every load of the tile in flight at
+// once), computes each staged pixel's L2 norm over C (hoisted out of the d loop: the reference
+// recomputes it per d), normalises in place, and writes kNcD planes of the row segment.
+// The norm is summed in channel order and the eps is added after the sqrt, as
+// torch.norm(., 2, 1) + 1e-5 (submodule.py:188-189); the mean is sum_c / C (submodule.py:190).
+constexpr int kNcW = 64;   // output pixels per workgroup (one per lane of a wave)
+constexpr int kNcD = 16;   // disparities per workgroup (ESMStereo's D is 12-64: little idle work)
+constexpr int kNcSpan = kNcW + kNcD - 1;
 
-// Correlation of normalised features: one thread per pixel, kNcD disparities in registers,
-// right rows staged in LDS in channel chunks of 16.
-constexpr int kNcPix = 256;
-constexpr int kNcD = 16;
-constexpr int kNcC = 16;
-
-__global__ void __launch_bounds__(kThreads) normcorr_kernel(const float* __restrict__ Ln, const float* __restrict__ Rn,
+template <int CT>  // CT: channel capacity of the LDS tile (C <= CT)
+__global__ void __launch_bounds__(kThreads) normcorr_kernel(const float* __restrict__ L, const float* __restrict__ R,
                                                             float* __restrict__ V, int C, int H, int W, int D) {
-    __shared__ float rs[kNcC][kNcPix + kNcD];
-    const int HW = H * W;
-    const int b = blockIdx.y;
-    const int p0 = blockIdx.x * kNcPix;
+    __shared__ float ls[CT][kNcW + 1];
+    __shared__ float rs[CT][kNcSpan + 1];
+    const int x0 = blockIdx.x * kNcW;
+    const int y = blockIdx.y % H;
+    const int b = blockIdx.y / H;
     const int d0 = blockIdx.z * kNcD;
-    const int dn = min(kNcD, D - d0);
-    const int p = p0 + threadIdx.x;
-    const bool in = p < HW;
-    const int x = in ? p % W : -1;
-    const int lo = p0 - (d0 + dn - 1);
-    const int span = kNcPix + dn - 1;
-    float acc[kNcD];
+    const int r0 = x0 - d0 - (kNcD - 1);  // right x of rs[.][0]
+    const long long HW = static_cast<long long>(H) * W;
+    const float* lrow = L + static_cast<long long>(b) * C * HW + static_cast<long long>(y) * W;
+    const float* rrow = R + static_cast<long long>(b) * C * HW + static_cast<long long>(y) * W;
+    const int t = threadIdx.x;
+
+    // stage: all loads of the tile issued before the first LDS store
+    constexpr int NL = (CT * kNcW + kThreads - 1) / kThreads;
+    constexpr int NR = (CT * kNcSpan + kThreads - 1) / kThreads;
+    float lv[NL], rv[NR];
 #pragma unroll
-    for (int k = 0; k < kNcD; ++k) acc[k] = 0.f;
-    const float* lb = Ln + static_cast<long long>(b) * C * HW;
-    const float* rb = Rn + static_cast<long long>(b) * C * HW;
-    for (int c0 = 0; c0 < C; c0 += kNcC) {
-        const int cn = min(kNcC, C - c0);
-        __syncthreads();
-        for (int i = threadIdx.x; i < cn * span; i += kThreads) {
-            const int cc = i / span;
-            const int j = i - cc * span;
-            const int q = lo + j;
-            rs[cc][j] = (q >= 0 && q < HW) ? rb[static_cast<long long>(c0 + cc) * HW + q] : 0.f;
+    for (int k = 0; k < NL; ++k) {
+        const int i = t + k * kThreads;
+        const int c = i / kNcW, j = i - c * kNcW, x = x0 + j;
+        lv[k] = (i < C * kNcW && x < W) ? lrow[c * HW + x] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int i = t + k * kThreads;
+        const int c = i / kNcSpan, j = i - c * kNcSpan, x = r0 + j;
+        rv[k] = (i < C * kNcSpan && x >= 0 && x < W) ? rrow[c * HW + x] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = t + k * kThreads;
+        if (i < C * kNcW) ls[i / kNcW][i % kNcW] = lv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int i = t + k * kThreads;
+        if (i < C * kNcSpan) rs[i / kNcSpan][i % kNcSpan] = rv[k];
+    }
+    __syncthreads();
+    // per-pixel norms (one staged pixel per thread), then normalise in place
+    float n = 1.f;
+    if (t < kNcW + kNcSpan) {
+        float ss = 0.f;
+        if (t < kNcW) {
+#pragma unroll 8
+            for (int c = 0; c < C; ++c) ss = ss + ls[c][t] * ls[c][t];
+        } else {
+#pragma unroll 8
+            for (int c = 0; c < C; ++c) ss = ss + rs[c][t - kNcW] * rs[c][t - kNcW];
         }
-        __syncthreads();
-        for (int cc = 0; cc < cn; ++cc) {
-            const float lv = in ? lb[static_cast<long long>(c0 + cc) * HW + p] : 0.f;
+        n = sqrtf(ss) + 1e-05f;
+    }
+    __syncthreads();
+    if (t < kNcW) {
+#pragma unroll 8
+        for (int c = 0; c < C; ++c) ls[c][t] = ls[c][t] / n;
+    } else if (t < kNcW + kNcSpan) {
+#pragma unroll 8
+        for (int c = 0; c < C; ++c) rs[c][t - kNcW] = rs[c][t - kNcW] / n;
+    }
+    __syncthreads();
+    // correlation: lane = pixel, wave w takes disparities d0 + w, d0 + w + 4, ...
+    const int j = t & (kNcW - 1);
+    const int x = x0 + j;
+    const int w = t / kNcW;
+    constexpr int PER = kNcD / (kThreads / kNcW);
+    float acc[PER];
 #pragma unroll
-            for (int k = 0; k < kNcD; ++k) {
-                if (k < dn) {
-                    const int d = d0 + k;
-                    const int j = p - d - lo;
-                    acc[k] = acc[k] + lv * rs[cc][j];
-                }
-            }
+    for (int k = 0; k < PER; ++k) acc[k] = 0.f;
+#pragma unroll 4
+    for (int c = 0; c < C; ++c) {
+        const float l = ls[c][j];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int dd = w + 4 * k;  // x - (d0 + dd) - r0 = j + kNcD - 1 - dd
+            acc[k] = acc[k] + l * rs[c][j + kNcD - 1 - dd];
         }
     }
-    if (!in) return;
-    float* vb = V + (static_cast<long long>(b) * D + d0) * HW + p;
+    if (x >= W) return;
+    float* vrow = V + static_cast<long long>(b) * D * HW + static_cast<long long>(y) * W + x;
     const float invC = 1.0f / static_cast<float>(C);
 #pragma unroll
-    for (int k = 0; k < kNcD; ++k)
-        if (k < dn) vb[static_cast<long long>(k) * HW] = (x >= d0 + k) ? acc[k] * invC : 0.f;
+    for (int k = 0; k < PER; ++k) {
+        const int d = d0 + w + 4 * k;
+        if (d < D) vrow[d * HW] = x >= d ? acc[k] * invC : 0.f;
+    }
 }
 
 }  // namespace
@@ -288,16 +318,18 @@ int launch_concat(const float* L, const float* R, float* V, int B, int C, int H,
 
 int launch_normcorr(const float* L, const float* R, float* V, float* work, int B, int C, int H, int W, int D,
                     hipStream_t s) {
-    if (!L || !R || !V || !work) return arg_error("normcorr: null pointer");
+    (void)work;  // kept in the ABI; the fused kernel normalises in LDS
+    if (!L || !R || !V) return arg_error("normcorr: null pointer");
     if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || D <= 0) return arg_error("normcorr: non-positive size");
-    const int HW = H * W;
-    const int npix = B * HW;
-    float* Ln = work;
-    float* Rn = work + static_cast<long long>(B) * C * HW;
-    hipLaunchKernelGGL(l2norm_kernel, dim3(ceil_div(npix, kThreads)), dim3(kThreads), 0, s, L, Ln, C, HW, npix);
-    hipLaunchKernelGGL(l2norm_kernel, dim3(ceil_div(npix, kThreads)), dim3(kThreads), 0, s, R, Rn, C, HW, npix);
-    dim3 grid(ceil_div(HW, kNcPix), B, ceil_div(D, kNcD));
-    hipLaunchKernelGGL(normcorr_kernel, grid, dim3(kThreads), 0, s, Ln, Rn, V, C, H, W, D);
+    dim3 grid(ceil_div(W, kNcW), B * H, ceil_div(D, kNcD));
+    if (C <= 16)
+        hipLaunchKernelGGL(normcorr_kernel<16>, grid, dim3(kThreads), 0, s, L, R, V, C, H, W, D);
+    else if (C <= 64)
+        hipLaunchKernelGGL(normcorr_kernel<64>, grid, dim3(kThreads), 0, s, L, R, V, C, H, W, D);
+    else {
+        set_error("normcorr: C must be <= 64");
+        return ESM_ERR_UNSUPPORTED;
+    }
     return check_launch("normcorr");
 }
 

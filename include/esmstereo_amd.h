@@ -162,7 +162,7 @@ int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* 
                        int D, int G, void* stream);
 int esm_concat_volume_f32(const float* L, const float* R, float* V, int B, int C, int H, int W, int D,
                           void* stream);
-/* work: caller-owned scratch of 2*B*C*H*W floats (normalised features). */
+/* work: unused since the single-launch kernel (normalises in LDS); may be NULL.  C <= 64. */
 int esm_normcorr_volume_f32(const float* L, const float* R, float* V, float* work, int B, int C, int H, int W,
                             int D, void* stream);
 int esm_disp_regression_f32(const float* cost, float* out, int B, int D, int H, int W, void* stream);

@@ -210,6 +210,38 @@ def test_conv_every_tile_variant(nd, cin, cout, k, s, tr):
         assert rel(run_conv(Ctx(DEV), p, xs, hint=0x114), ref) < 1e-5
 
 
+HINT_STEM, HINT_NO_STEM = 1 << 17, 1 << 18
+STEM_CASES = [(3, 32, 8, (6, 9, 21)), (3, 1, 8, (5, 7, 30)), (3, 8, 8, (7, 5, 29)), (3, 12, 12, (4, 6, 15)),
+              (3, 32, 8, (2, 3, 10)), (3, 3, 8, (9, 4, 44)), (2, 16, 8, (23, 37)), (2, 8, 12, (17, 50)),
+              (2, 64, 8, (33, 15))]
+
+
+@pytest.mark.parametrize("nd,cin,cout,shape", STEM_CASES)
+def test_conv_stem_form(nd, cin, cout, shape):
+    """16-block MFMA narrow-output form (conv_stem.hip), forced and automatic, vs fp64 torch and
+    vs the other forms (1e-5 relative)."""
+    conv, bn = _mk(nd, cin, cout, 3, 1, 1, seed=4)
+    x = torch.randn(2, cin, *shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    xs = [x.to(DEV)]
+    for h in (HINT_STEM, 0, HINT_NO_STEM):
+        assert rel(run_conv(Ctx(DEV), p, xs, hint=h), ref) < 1e-5, hex(h)
+
+
+def test_conv_stem_form_epilogues():
+    """`corr_stem(volume) * att` (ESMStereo.py:703) and a residual through the stem form."""
+    conv, bn = _mk(3, 1, 8, 3, 1, 1, seed=5)
+    x = torch.randn(2, 1, 6, 10, 33)
+    att = torch.randn(2, 8, 10, 33)
+    res = torch.randn(2, 8, 6, 10, 33)
+    p = pk(conv, bn, ACT_GELU)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], mul=att.to(DEV), hint=HINT_STEM)
+    assert rel(y, _ref_conv([x], conv, bn, ACT_GELU, mul=att)) < 1e-5
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), post_scale=2.0, hint=HINT_STEM)
+    assert rel(y, _ref_conv([x], conv, bn, ACT_GELU, res=res, post=2.0)) < 1e-5
+
+
 ROWS_CASES = [(2, 16, 16, 3, 1, 37, 70), (2, 8, 16, 3, 1, 9, 29), (2, 1, 16, 5, 1, 24, 78), (2, 1, 16, 5, 2, 24, 78),
               (2, 16, 8, 1, 0, 11, 33), (2, 16, 32, 3, 1, 13, 45), (2, 16, 24, 3, 1, 6, 17), (2, 4, 1, 3, 1, 20, 50),
               (3, 16, 16, 3, 1, (5, 9, 37), None), (3, 8, 8, 3, 1, (6, 7, 19), None), (3, 16, 24, 1, 0, (3, 6, 20), None)]
@@ -517,7 +549,11 @@ def _full_inputs(model, B, H, W, seed):
 
 
 @pytest.mark.parametrize("var,cv,B,H,W,maxdisp", [("S", "gwc", 1, 384, 1248, 192), ("S", "nc", 2, 384, 1248, 192),
-                                                  ("L", "gwc", 1, 384, 1248, 192), ("M", "gwc", 1, 256, 512, 192)])
+                                                  ("L", "gwc", 1, 384, 1248, 192), ("M", "gwc", 1, 256, 512, 192),
+                                                  # BASELINE configs[2] (SceneFlow 540x960 padded to 544, B=8) and
+                                                  # configs[4] (Middlebury ~1500x1000 padded to 1504x1024, md256)
+                                                  ("L", "gwc", 8, 544, 960, 192), ("L", "gwc", 1, 1024, 1504, 256),
+                                                  ("L", "nc", 1, 384, 1248, 192)])
 def test_hot_path_full_size_vs_oracle(var, cv, B, H, W, maxdisp):
     model, sd, m = _model_from_manifest(f"hot_{var}_{cv}.npz", maxdisp=maxdisp)
     ml, mr, att, up = _full_inputs(model, B, H, W, 11)
