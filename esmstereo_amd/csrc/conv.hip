@@ -8,6 +8,7 @@ int launch_conv2d(const esm_conv_desc& a, hipStream_t s);
 int launch_conv3d(const esm_conv_desc& a, hipStream_t s);
 namespace conv {
 bool stem_ok(const esm_conv_desc& a);                    // conv_stem.hip
+bool stem_auto(const esm_conv_desc& a);                  // conv_stem.hip
 int launch_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 }  // namespace conv
 
@@ -58,8 +59,8 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         d.hint &= ~kHintNoStem;
         return d3 ? launch_conv3d(d, s) : launch_conv2d(d, s);
     }
-    // 8 / 12 output channels, 3x3(x3) stride 1: the 16-block MFMA form wastes no tile rows
-    if (a.hint == 0 && conv::stem_ok(a)) return conv::launch_stem(a, s);
+    // 8 / 12 / 24 output channels, 3x3(x3) stride 1: the 16-block MFMA form wastes no tile rows
+    if (a.hint == 0 && conv::stem_auto(a)) return conv::launch_stem(a, s);
     return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
 }
 

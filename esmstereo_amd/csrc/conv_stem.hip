@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
     constexpr int K = 3;
     constexpr int KDT = D3 ? 3 : 1;
     constexpr int TAPS = KDT * 9;
-    constexpr int CGP = CG == 3 ? 4 : CG;  // LDS entry width (power of two)
+    constexpr int CGP = CG == 3 ? 4 : CG;  // LDS entry width (even: float2 / float4 reads)
     constexpr int VALID = 14;
     constexpr int NB = CK * KDT * K;        // B values of one chunk
     extern __shared__ float wl[];           // [cin_stage][TAPS][4][CGP]
@@ -162,18 +162,22 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
                         const int tap = (td * K + th) * K + tw;
                         const float* wp = wl + (((cc + k) * TAPS + tap) * 4 + q) * CGP;
                         float av[CGP];
-                        if constexpr (CGP == 2) {
-                            const float2 w2 = *reinterpret_cast<const float2*>(wp);
-                            av[0] = w2.x;
-                            av[1] = w2.y;
-                        } else if constexpr (CGP == 4) {
-                            const float4 w4 = *reinterpret_cast<const float4*>(wp);
-                            av[0] = w4.x;
-                            av[1] = w4.y;
-                            av[2] = w4.z;
-                            av[3] = w4.w;
+                        if constexpr (CGP % 4 == 0) {
+#pragma unroll
+                            for (int j = 0; j < CGP / 4; ++j) {
+                                const float4 w4 = *reinterpret_cast<const float4*>(wp + 4 * j);
+                                av[4 * j] = w4.x;
+                                av[4 * j + 1] = w4.y;
+                                av[4 * j + 2] = w4.z;
+                                av[4 * j + 3] = w4.w;
+                            }
                         } else {
-                            av[0] = wp[0];
+#pragma unroll
+                            for (int j = 0; j < CGP / 2; ++j) {
+                                const float2 w2 = *reinterpret_cast<const float2*>(wp + 2 * j);
+                                av[2 * j] = w2.x;
+                                av[2 * j + 1] = w2.y;
+                            }
                         }
                         const int ch = tw & 1;  // two independent chains per group
 #pragma unroll
@@ -263,23 +267,46 @@ int launch_sconv(const esm_conv_desc& a, hipStream_t s) {
 
 }  // namespace
 
-// Layers this form takes: stride-1 3x3(x3) convs with "same" padding, one source, 8 or 12
-// output channels, no pixel shuffle, a weight slab that fits 64 KiB of LDS.
+// Layers this form takes: stride-1 3x3(x3) convs with "same" padding, one source, 8, 12, 16,
+// 24 or 32 output channels, no pixel shuffle, a weight slab that fits 64 KiB of LDS.
 bool stem_ok(const esm_conv_desc& a) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
     if (a.transposed || a.stride != 1 || a.kh != 3 || a.kw != 3 || (d3 && a.kd != 3)) return false;
     if (a.ph != 1 || a.pw != 1 || (d3 && a.pd != 1) || a.nsrc != 1 || a.shuffle > 1) return false;
-    if (a.Cout != 8 && a.Cout != 12) return false;
-    const long long lds = static_cast<long long>((a.Cin + 3) / 4 * 4) * (d3 ? 27 : 9) * 4 *
-                          (a.Cout == 12 ? 4 : 2) * 4;
+    if (a.Cout != 8 && a.Cout != 12 && a.Cout != 16 && a.Cout != 24 && a.Cout != 32) return false;
+    const int cgp = a.Cout == 12 ? 4 : a.Cout / 4;
+    const long long lds = static_cast<long long>((a.Cin + 3) / 4 * 4) * (d3 ? 27 : 9) * 4 * cgp * 4;
     return lds <= 64 * 1024 && direct_ok(a);
+}
+
+template <bool D3>
+int launch_stem_d(const esm_conv_desc& a, hipStream_t s) {
+    switch (a.Cout) {
+        case 8: return launch_sconv<D3, 2>(a, s);
+        case 12: return launch_sconv<D3, 3>(a, s);
+        case 16: return launch_sconv<D3, 4>(a, s);
+        case 24: return launch_sconv<D3, 6>(a, s);
+        default: return launch_sconv<D3, 8>(a, s);
+    }
 }
 
 int launch_stem(const esm_conv_desc& a, hipStream_t s) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
     if (!stem_ok(a)) return arg_error("conv: stem form not applicable");
-    if (d3) return a.Cout == 8 ? launch_sconv<true, 2>(a, s) : launch_sconv<true, 3>(a, s);
-    return a.Cout == 8 ? launch_sconv<false, 2>(a, s) : launch_sconv<false, 3>(a, s);
+    return d3 ? launch_stem_d<true>(a, s) : launch_stem_d<false>(a, s);
+}
+
+// Automatic choice, from scripts/probes/stem_sweep.py on MI355X (profiles/r01_stem_sweep.txt):
+// 3-D 8-cout stems at every size; otherwise only large maps (>= 64k output voxels), where the
+// per-workgroup weight staging is amortised: 12 / 24 couts (the 16x16 tile pads them) and 16 / 32
+// couts over >= 32 input channels (more B reuse per load than the direct form).
+bool stem_auto(const esm_conv_desc& a) {
+    if (!stem_ok(a)) return false;
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    const long long vox = static_cast<long long>(a.B) * (d3 ? a.Do : 1) * a.Ho * a.Wo;
+    if (a.Cout == 8 && d3) return true;
+    if (vox < 65536) return false;
+    return a.Cout == 8 || a.Cout == 12 || a.Cout == 24 || ((a.Cout == 16 || a.Cout == 32) && a.Cin >= 32);
 }
 
 }  // namespace conv

@@ -213,7 +213,8 @@ def test_conv_every_tile_variant(nd, cin, cout, k, s, tr):
 HINT_STEM, HINT_NO_STEM = 1 << 17, 1 << 18
 STEM_CASES = [(3, 32, 8, (6, 9, 21)), (3, 1, 8, (5, 7, 30)), (3, 8, 8, (7, 5, 29)), (3, 12, 12, (4, 6, 15)),
               (3, 32, 8, (2, 3, 10)), (3, 3, 8, (9, 4, 44)), (2, 16, 8, (23, 37)), (2, 8, 12, (17, 50)),
-              (2, 64, 8, (33, 15))]
+              (2, 64, 8, (33, 15)), (3, 24, 24, (5, 9, 31)), (3, 16, 16, (3, 6, 20)), (2, 32, 32, (19, 47)),
+              (2, 16, 16, (12, 39)), (3, 12, 24, (2, 3, 10)), (2, 40, 16, (9, 30))]
 
 
 @pytest.mark.parametrize("nd,cin,cout,shape", STEM_CASES)
