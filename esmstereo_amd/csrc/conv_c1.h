@@ -9,8 +9,8 @@
 // Why not the MFMA forms: with one output channel a 16x16 MFMA tile uses 1/16 of its rows, and
 // a per-parity-class grid re-reads every input pixel for each of the 4 (8) classes.  Here a
 // workgroup owns a 16 x (16*QW) output tile of one output plane (all parity classes), stages
-// the Cin x 10 x (8*QW+2) input tile it needs (x2 planes in 3-D) and the weights in LDS with
-// one batch of loads (one memory round trip); every thread computes QW consecutive output
+// the weights and, channel chunk by channel chunk, the CC x 10 x (8*QW+2) input tile it needs
+// (x2 planes in 3-D) in LDS, the next chunk's loads in flight during the current chunk's FMAs; every thread computes QW consecutive output
 // columns of one row.  The 4 waves take rows of one parity each (rows 2i + p), so a wave's
 // weights are LDS broadcasts, laid out [qz][qy][c][qx][tap] for two 16-byte reads per channel;
 // input rows are 8-byte aligned for 64-bit reads.  QW = 4 stores one 16-byte vector per thread.
@@ -29,7 +29,7 @@ namespace conv {
 constexpr int kC1Threads = 256;
 constexpr int kC1TH = 16;  // output rows per tile
 
-template <bool D3, int CP, int QW>
+template <bool D3, int CC, int QW>
 __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_desc a) {
     constexpr int TW = 16 * QW;               // output columns per tile
     constexpr int IR = kC1TH / 2 + 2;         // input rows of the tile
@@ -37,13 +37,14 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     constexpr int ICP = (IC + 3) / 4 * 4;     // padded LDS row (16-B aligned rows)
     constexpr int NP = D3 ? 2 : 1;            // input planes per output plane
     constexpr int NQZ = D3 ? 2 : 1;
-    constexpr int XN = NP * CP * IR * IC;     // staged input elements
+    constexpr int CPM = 32;                   // channel capacity of the weight table
+    constexpr int XN = NP * CC * IR * IC;     // staged input elements of one channel chunk
     constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
-    constexpr int WN = NQZ * 2 * CP * 2 * 4 * NP;  // staged weights [qz][qy][c][qx][tz][ty][tx]
+    constexpr int WN = NQZ * 2 * CPM * 2 * 4 * NP;  // staged weights [qz][qy][c][qx][tz][ty][tx]
     constexpr int WR = (WN + kC1Threads - 1) / kC1Threads;
     constexpr int TAPS = D3 ? 8 : 4;
-    __shared__ __attribute__((aligned(16))) float xs[NP][CP][IR][ICP];
-    __shared__ __attribute__((aligned(16))) float ws[NQZ][2][CP][2][NP][4];
+    __shared__ __attribute__((aligned(16))) float xs[NP][CC][IR][ICP];
+    __shared__ __attribute__((aligned(16))) float ws[NQZ][2][CPM][2][NP][4];
 
     const int tid = threadIdx.x;
     const int Ho = a.Ho, Wo = a.Wo, Do = D3 ? a.Do : 1;
@@ -55,56 +56,51 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
     const esm_src& sr = a.src[0];
     const float* xb = sr.ptr + b * sr.sb;
+    const int nch = (a.Cin + CC - 1) / CC;
 
-    // ---- stage: every load of the thread in flight together, then the LDS stores
-    float rx[XR], rw[WR];
+    // one channel chunk of the input tile: every load of the thread in flight together
+    auto load_chunk = [&](float (&rx)[XR], int c0) {
 #pragma unroll
-    for (int k = 0; k < XR; ++k) {
-        const int i = tid + k * kC1Threads;
-        const int col = i % IC;
-        const int row = (i / IC) % IR;
-        const int c = (i / (IC * IR)) % CP;
-        const int p = i / (IC * IR * CP);
-        const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
-        const bool ok = i < XN && c < a.Cin && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi &&
-                        (!D3 || (iz >= 0 && iz < a.Di));
-        const float v = xb[ok ? c * sr.sc + (D3 ? iz * sr.sd : 0) + iy * sr.sh + ix : 0];
-        rx[k] = ok ? v : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < WR; ++k) {
-        // LDS index (qz, qy, c, qx, tz, ty, tx) <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
-        const int i = tid + k * kC1Threads;
-        const int tyx = i & 3;
-        const int tz = (i >> 2) % NP;
-        const int qx = (i / (4 * NP)) & 1;
-        const int c = (i / (8 * NP)) % CP;
-        const int qy = (i / (8 * NP * CP)) & 1;
-        const int qzz = i / (16 * NP * CP);
-        const int cls = D3 ? (qzz << 2 | qy << 1 | qx) : (qy << 1 | qx);
-        const int tap = D3 ? (tz << 2 | tyx) : tyx;
-        const bool ok = i < WN && c < a.cin_pad;
-        const float v = a.w[ok ? ((static_cast<long long>(cls) * TAPS + tap) * a.cin_pad + c) * a.cout_pad : 0];
-        rw[k] = ok ? v : 0.f;
-    }
-    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
-#pragma unroll
-    for (int k = 0; k < XR; ++k) {
-        const int i = tid + k * kC1Threads;
-        if (i < XN) {
+        for (int k = 0; k < XR; ++k) {
+            const int i = tid + k * kC1Threads;
             const int col = i % IC;
             const int row = (i / IC) % IR;
-            const int c = (i / (IC * IR)) % CP;
-            const int p = i / (IC * IR * CP);
-            xs[p][c][row][col] = rx[k];
+            const int c = c0 + (i / (IC * IR)) % CC;
+            const int p = i / (IC * IR * CC);
+            const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
+            const bool ok = i < XN && c < a.Cin && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi &&
+                            (!D3 || (iz >= 0 && iz < a.Di));
+            const float v = xb[ok ? c * sr.sc + (D3 ? iz * sr.sd : 0) + iy * sr.sh + ix : 0];
+            rx[k] = ok ? v : 0.f;
+        }
+    };
+    float rx[XR];
+    load_chunk(rx, 0);
+    {
+        float rw[WR];
+#pragma unroll
+        for (int k = 0; k < WR; ++k) {
+            // LDS index (qz, qy, c, qx, tz, ty, tx) <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
+            const int i = tid + k * kC1Threads;
+            const int tyx = i & 3;
+            const int tz = (i >> 2) % NP;
+            const int qx = (i / (4 * NP)) & 1;
+            const int c = (i / (8 * NP)) % CPM;
+            const int qy = (i / (8 * NP * CPM)) & 1;
+            const int qzz = i / (16 * NP * CPM);
+            const int cls = D3 ? (qzz << 2 | qy << 1 | qx) : (qy << 1 | qx);
+            const int tap = D3 ? (tz << 2 | tyx) : tyx;
+            const bool ok = i < WN && c < a.Cin;
+            const float v = a.w[ok ? ((static_cast<long long>(cls) * TAPS + tap) * a.cin_pad + c) * a.cout_pad : 0];
+            rw[k] = ok ? v : 0.f;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
+#pragma unroll
+        for (int k = 0; k < WR; ++k) {
+            const int i = tid + k * kC1Threads;
+            if (i < WN) (&ws[0][0][0][0][0][0])[i] = rw[k];
         }
     }
-#pragma unroll
-    for (int k = 0; k < WR; ++k) {
-        const int i = tid + k * kC1Threads;
-        if (i < WN) (&ws[0][0][0][0][0][0])[i] = rw[k];
-    }
-    __syncthreads();
 
     // ---- thread: output row Y0 + r (wave w: rows of parity w & 1), columns X0 + QW*g ...
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -119,25 +115,42 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     float acc[QW];
 #pragma unroll
     for (int j = 0; j < QW; ++j) acc[j] = 0.f;
+    for (int ch = 0; ch < nch; ++ch) {
+        if (ch) __syncthreads();  // the previous chunk's reads of xs are done
 #pragma unroll
-    for (int tz = 0; tz < NP; ++tz) {
-        const int p = D3 ? 1 - tz : 0;  // plane tap t = tz sits at tile plane 1 - t
+        for (int k = 0; k < XR; ++k) {
+            const int i = tid + k * kC1Threads;
+            if (i < XN) {
+                const int col = i % IC;
+                const int row = (i / IC) % IR;
+                const int c = (i / (IC * IR)) % CC;
+                const int p = i / (IC * IR * CC);
+                xs[p][c][row][col] = rx[k];
+            }
+        }
+        __syncthreads();
+        if (ch + 1 < nch) load_chunk(rx, (ch + 1) * CC);  // next chunk in flight during this one's FMAs
+#pragma unroll
+        for (int tz = 0; tz < NP; ++tz) {
+            const int p = D3 ? 1 - tz : 0;  // plane tap t = tz sits at tile plane 1 - t
 #pragma unroll 4
-        for (int c = 0; c < CP; ++c) {
-            float v[2][NV];
-#pragma unroll
-            for (int ty = 0; ty < 2; ++ty)
-#pragma unroll
-                for (int j = 0; j < NV; ++j) v[ty][j] = xs[p][c][lr - ty][lc + j];
-#pragma unroll
-            for (int j = 0; j < QW; ++j) {
-                const int qx = j & 1;
-                // input m + qx - tx of output column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
+            for (int c = 0; c < CC; ++c) {
+                const int cw = ch * CC + c;
+                float v[2][NV];
 #pragma unroll
                 for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
-                    for (int tx = 0; tx < 2; ++tx)
-                        acc[j] += ws[qz][qy][c][qx][tz][ty * 2 + tx] * v[ty][1 + (j >> 1) + qx - tx];
+                    for (int j = 0; j < NV; ++j) v[ty][j] = xs[p][c][lr - ty][lc + j];
+#pragma unroll
+                for (int j = 0; j < QW; ++j) {
+                    const int qx = j & 1;
+                    // input m + qx - tx of output column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
+#pragma unroll
+                    for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+                        for (int tx = 0; tx < 2; ++tx)
+                            acc[j] += ws[qz][qy][cw][qx][tz][ty * 2 + tx] * v[ty][1 + (j >> 1) + qx - tx];
+                }
             }
         }
     }
@@ -172,10 +185,11 @@ int launch_convt_c1_q(const esm_conv_desc& a, hipStream_t s) {
     const int Do = D3 ? a.Do : 1;
     dim3 grid(ceil_div(a.Wo, 16 * QW), ceil_div(a.Ho, kC1TH), static_cast<unsigned>(a.B) * Do);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-    if (a.Cin <= 16)
-        hipLaunchKernelGGL((convt_c1_kernel<D3, 16, QW>), grid, dim3(kC1Threads), 0, s, a);
+    // channel chunks: 8 at a time in 3-D (two input planes per output plane), 16 in 2-D
+    if constexpr (D3)
+        hipLaunchKernelGGL((convt_c1_kernel<D3, 8, QW>), grid, dim3(kC1Threads), 0, s, a);
     else
-        hipLaunchKernelGGL((convt_c1_kernel<D3, 32, QW>), grid, dim3(kC1Threads), 0, s, a);
+        hipLaunchKernelGGL((convt_c1_kernel<D3, 16, QW>), grid, dim3(kC1Threads), 0, s, a);
     return check_launch("conv(c1 transposed)");
 }
 
