@@ -79,6 +79,8 @@ SIGNATURES = {
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
     "esm_conv_pair_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
+    "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
+    "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "esm_plan_create": (c_void_p, []),
     "esm_plan_destroy": (None, [c_void_p]),
     "esm_plan_add_conv": (c_int, [c_void_p, POINTER(EsmConvDesc)]),

@@ -32,6 +32,11 @@
  *                             FMBlock.conv (models/shufflemixer.py:124-131)
  *   esm_plan_*                the orchestration of models/ESMStereo.py:700-745 as a native
  *                             launch list, optionally replayed as one hipGraph
+ *   esm_preprocess_u8         the input side: pad to /32 + ToTensor +
+ *                             Normalize of test_kitti.py:93-106 (pad before normalising) or
+ *                             datasets/kitti_dataset.py:151-170 (pad after), datasets/data_io.py:7-16
+ *   esm_disp_to_u16           the output side: crop of the padded disparity (test_kitti.py:115,
+ *                             save_disp.py:81) + np.round(d * 256).astype(np.uint16) (save_disp.py:85)
  */
 #ifndef ESMSTEREO_AMD_H
 #define ESMSTEREO_AMD_H
@@ -101,7 +106,8 @@ typedef struct {
     const float* up;
     int32_t up_h, up_w, up_f;
     int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 10 |
-                     rows-per-wave << 12 | C1T << 16
+                     rows-per-wave << 12 | C1T << 16 | STEM << 17 (16-block 4x4x1 MFMA form for
+                     3x3(x3) s1 convs with 8/12/16/24/32 couts) | NO_STEM << 18 (automatic, without it)
                      (tuning sweeps / tests; see conv_impl.h launch_geom) */
     int64_t ub, uh;
     float post_scale;
@@ -180,6 +186,15 @@ int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
  * out2.  Returns ESM_ERR_UNSUPPORTED (no launch) for a pair without a fused form: run the two convs
  * with esm_conv_f32 instead. */
 int esm_conv_pair_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
+
+/* img: [B, H, W, 3] uint8 RGB (PIL order); out: [B, 3, Hp, Wp] fp32.  The image lands at rows
+ * [top, top+H), columns [left, left+W); pad_normalized = 1 fills the rest with normalised zeros
+ * (test_kitti.py: top = Hp-H, left = Wp-W), 0 with 0.0 (kitti_dataset.py: top = Hp-H, left = 0). */
+int esm_preprocess_u8(const uint8_t* img, float* out, int B, int H, int W, int Hp, int Wp, int top, int left,
+                      int pad_normalized, void* stream);
+/* disp: [B, Hp, Wp] fp32; out: [B, h, w] uint16 = round_half_even(disp[b, top+y, left+x] * 256). */
+int esm_disp_to_u16(const float* disp, uint16_t* out, int B, int Hp, int Wp, int top, int left, int h, int w,
+                    void* stream);
 
 /* ---- native launch plan (the hot path as one replayable unit) ---- */
 typedef struct esm_plan esm_plan;
