@@ -139,9 +139,13 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
         }
     __syncthreads();
 
-    floatx4 acc[2][CG];
+    // independent accumulation chains: a 4x4x1 MFMA issues every 8 cycles but its result is ready
+    // later (PMC: 58% of group_stem's wave cycles were issue stalls with 2 chains), so consecutive
+    // MFMAs of one group go to different chains
+    constexpr int NCH = CG <= 3 ? 4 : 2;
+    floatx4 acc[NCH][CG];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int g = 0; g < CG; ++g) acc[c][g] = floatx4{0.f, 0.f, 0.f, 0.f};
 
@@ -179,7 +183,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
                                 av[2 * j + 1] = w2.y;
                             }
                         }
-                        const int ch = tw & 1;  // two independent chains per group
+                        const int ch = (((k * KDT + td) * K + th) * K + tw) % NCH;
 #pragma unroll
                         for (int g = 0; g < CG; ++g) acc[ch][g] = mfma4(av[g], bs, acc[ch][g]);
                     }
@@ -194,7 +198,12 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
 #pragma unroll
     for (int g = 0; g < CG; ++g)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sum[g][i] = acc[0][g][i] + acc[1][g][i];
+        for (int i = 0; i < 4; ++i) {
+            float t = acc[0][g][i];
+#pragma unroll
+            for (int c = 1; c < NCH; ++c) t += acc[c][g][i];  // fixed order (deterministic)
+            sum[g][i] = t;
+        }
     if constexpr (KS) {  // fixed-order reduction of the 4 waves' partial sums
         __shared__ float red[3][CG * 4][64];
         if (wave > 0) {

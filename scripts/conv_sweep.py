@@ -36,6 +36,7 @@ LAYERS = [
     ("conv3.0 3d k3s2 16->24 3x6x20", 3, [16], 24, 3, 2, False, (3, 6, 20), ACT_GELU, 1),
     ("L group_stem 3d k3 32->8 48x96x312", 3, [32], 8, 3, 1, False, (48, 96, 312), ACT_GELU, 1),
     ("L conv1.1 3d k3 24->24 24x48x156", 3, [24], 24, 3, 1, False, (24, 48, 156), ACT_GELU, 1),
+    ("L dm4x.1 2d k3 32->32 192x624", 2, [32], 32, 3, 1, False, (1, 192, 624), ACT_GELU, 1),
 ]
 
 HINTS = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x44, 0x114, 0x211, 0x212, 0x241, 0x242]

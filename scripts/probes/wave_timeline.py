@@ -3,7 +3,7 @@
     python esmstereo_amd/build.py --diag
     ESM_LIB=esmstereo_amd/_build_diag/libesmstereo_amd.so python scripts/probes/wave_timeline.py [--h 192]
 
-Each wave of the 2-D direct kernel records s_memrealtime (100 MHz, chip-wide) at entry and
+Each wave of the 2-D / 3-D direct kernel records s_memrealtime (100 MHz, chip-wide) at entry and
 exit and s_memtime (shader clock) at entry, after setup, after its first K loop and at exit.
 Prints the kernel span, the phases of a wave, and how many waves were resident over time.
 """
@@ -29,15 +29,20 @@ def main():
     ap.add_argument("--cin", type=int, default=16)
     ap.add_argument("--cout", type=int, default=16)
     ap.add_argument("--hint", default="0")
+    ap.add_argument("--nd", type=int, default=2)
+    ap.add_argument("--d", type=int, default=1, help="depth (3-D)")
+    ap.add_argument("--stride", type=int, default=1)
     args = ap.parse_args()
     fn = _lib.lib.esm_diag_stamps
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda")
-    conv = torch.nn.Conv2d(args.cin, args.cout, 3, 1, 1, bias=False).to(dev)
-    bn = torch.nn.BatchNorm2d(args.cout).eval().to(dev)
+    C, BN = (torch.nn.Conv3d, torch.nn.BatchNorm3d) if args.nd == 3 else (torch.nn.Conv2d, torch.nn.BatchNorm2d)
+    conv = C(args.cin, args.cout, 3, args.stride, 1, bias=False).to(dev)
+    bn = BN(args.cout).eval().to(dev)
     pc = pack_conv(conv, bn, ACT_GELU)
-    x = torch.randn(1, args.cin, args.h, args.w, device=dev)
+    shape = (args.d, args.h, args.w) if args.nd == 3 else (args.h, args.w)
+    x = torch.randn(1, args.cin, *shape, device=dev)
     out = None
     maxw = (1 << 20) // 8
     buf = np.zeros(8 * maxw, dtype=np.uint64)
