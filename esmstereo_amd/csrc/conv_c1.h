@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     constexpr int ICP = (IC + 3) / 4 * 4;     // padded LDS row (16-B aligned rows)
     constexpr int NP = D3 ? 2 : 1;            // input planes per output plane
     constexpr int NQZ = D3 ? 2 : 1;
-    constexpr int CPM = 32;                   // channel capacity of the weight table
+    constexpr int CPM = D3 ? 32 : CC;         // channel capacity of the weight table (2-D: one chunk)
     constexpr int XN = NP * CC * IR * IC;     // staged input elements of one channel chunk
     constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
     constexpr int WN = NQZ * 2 * CPM * 2 * 4 * NP;  // staged weights [qz][qy][c][qx][tz][ty][tx]
@@ -185,11 +185,14 @@ int launch_convt_c1_q(const esm_conv_desc& a, hipStream_t s) {
     const int Do = D3 ? a.Do : 1;
     dim3 grid(ceil_div(a.Wo, 16 * QW), ceil_div(a.Ho, kC1TH), static_cast<unsigned>(a.B) * Do);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-    // channel chunks: 8 at a time in 3-D (two input planes per output plane), 16 in 2-D
+    // channel chunks: 8 at a time in 3-D (two input planes per output plane); 2-D stages all
+    // channels at once (one chunk of 16 or 32)
     if constexpr (D3)
         hipLaunchKernelGGL((convt_c1_kernel<D3, 8, QW>), grid, dim3(kC1Threads), 0, s, a);
-    else
+    else if (a.Cin <= 16)
         hipLaunchKernelGGL((convt_c1_kernel<D3, 16, QW>), grid, dim3(kC1Threads), 0, s, a);
+    else
+        hipLaunchKernelGGL((convt_c1_kernel<D3, 32, QW>), grid, dim3(kC1Threads), 0, s, a);
     return check_launch("conv(c1 transposed)");
 }
 

@@ -299,6 +299,18 @@ int esm_plan_run(esm_plan* plan, void* stream) {
     return plan->launch_all(esm::as_stream(stream), next_slot(plan));
 }
 
+int esm_plan_run_op(esm_plan* plan, int index, int reps, void* stream) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (index < 0 || index >= static_cast<int>(plan->ops.size())) return esm::arg_error("plan: op index out of range");
+    if (reps < 1) return esm::arg_error("plan: reps must be >= 1");
+    const hipStream_t s = esm::as_stream(stream);
+    for (int r = 0; r < reps; ++r) {
+        const int rc = run_op(plan->ops[index], s);
+        if (rc != ESM_OK) return rc;
+    }
+    return ESM_OK;
+}
+
 int esm_plan_graph_build(esm_plan* plan, void* stream) {
     if (!plan) return esm::arg_error("plan: null");
     (void)stream;

@@ -128,6 +128,11 @@ class HotPath:
         n = check(lib.esm_plan_probe_read(self.ctx.plan, buf, max_n), "probe_read")
         return [buf[i] for i in range(n)]
 
+    def run_op(self, index: int, reps: int = 1, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Launch op ``index`` of the plan alone, ``reps`` times back to back (kernel timing)."""
+        s = _lib.c_void_p((stream or torch.cuda.current_stream(self.device)).cuda_stream)
+        check(lib.esm_plan_run_op(self.ctx.plan, index, reps, s), "plan_run_op")
+
     def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = _lib.c_void_p((stream or torch.cuda.current_stream(self.device)).cuda_stream)
         if self.graph:

@@ -220,6 +220,9 @@ int esm_plan_op_kind(const esm_plan* plan, int index);
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */
 int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint);
 int esm_plan_run(esm_plan* plan, void* stream);
+/* Launch op `index` alone, `reps` times back to back on `stream` (timing one kernel of the
+ * path with a single hipEvent pair around the batch; the op's buffers are the plan's own). */
+int esm_plan_run_op(esm_plan* plan, int index, int reps, void* stream);
 /* Capture the launch list into a hipGraph (instantiated once; replays are cheap). */
 int esm_plan_graph_build(esm_plan* plan, void* stream);
 int esm_plan_graph_launch(esm_plan* plan, void* stream);

@@ -52,12 +52,23 @@ def assign(seq, n):
     return {i: sum(v) / len(v) for i, v in acc.items()}
 
 
+def trailing(ops_json: str) -> int:
+    """Dispatches bench.py issued after its last whole step (written next to the op table)."""
+    meta = ops_json + ".meta.json"
+    if not os.path.exists(meta):
+        return 0
+    with open(meta) as f:
+        return int(json.load(f).get("trailing_dispatches", 0))
+
+
 def main():
     fdir, wdir, ops_json, workload, out = sys.argv[1:6]
     ops = json.load(open(ops_json))
     n = len(ops)
-    fetch = assign(per_dispatch(fdir, "FETCH_SIZE"), n)
-    write = assign(per_dispatch(wdir, "WRITE_SIZE"), n)
+    tr = trailing(ops_json)
+    fs, ws = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
+    fetch = assign(fs[:len(fs) - tr], n)
+    write = assign(ws[:len(ws) - tr], n)
     tab = json.load(open(out)) if os.path.exists(out) else {}
     rows = {}
     for i, op in enumerate(ops):

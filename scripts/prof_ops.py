@@ -35,11 +35,21 @@ def load_trace(d: str):
     return rows
 
 
+def trailing(ops_json: str) -> int:
+    """Dispatches bench.py issued after its last whole step (written next to the op table)."""
+    meta = ops_json + ".meta.json"
+    if not os.path.exists(meta):
+        return 0
+    with open(meta) as f:
+        return int(json.load(f).get("trailing_dispatches", 0))
+
+
 def main():
     d, ops_json = sys.argv[1], sys.argv[2]
     ops = json.load(open(ops_json))
     n = len(ops)
     rows = [r for r in load_trace(d) if any(s in (r.get("Kernel_Name") or r.get("kernel_name") or "") for s in OURS)]
+    rows = rows[:len(rows) - trailing(ops_json)]
     steps = len(rows) // n
     if steps == 0:
         raise SystemExit("trace shorter than one step")
