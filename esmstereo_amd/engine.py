@@ -460,6 +460,53 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     return d, out, meta
 
 
+HINT_GWC_STEM = 1 << 19  # esm_conv_desc.hint: input = the virtual gwc volume of src[0..2]
+
+# build_gwc_volume fused into group_stem: opt-in (ESM_GWC_STEM=1).  Bitwise equal to the two-launch
+# path, but measured slower on MI355X (L-K: 503 us fused vs 36 + 306 us; S-K: even), because every
+# disparity tap re-fetches its shifted right-feature operands (3x the loads of reading the
+# volume); staging the right rows in LDS per workgroup is the next step.
+GWC_STEM_ENABLED = os.environ.get("ESM_GWC_STEM") == "1"
+
+
+def gwc_stem_supported(pc: PackedConv, C: int, G: int) -> bool:
+    return pc.nd == 3 and not pc.transposed and pc.k == 3 and pc.stride == 1 and pc.pad == 1 and pc.cout == 8 and \
+        pc.cin == G and C == 2 * G
+
+
+def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, att: Optional[torch.Tensor], D: int,
+                 G: int, out: Optional[torch.Tensor] = None, tag: str = "gwc+group_stem") -> torch.Tensor:
+    """``group_stem(build_gwc_volume(L, R, D, G) [* att])`` (models/ESMStereo.py:708-711) in one launch:
+    the conv reads the volume's voxels computed from the features in registers (conv_stem.hip),
+    bitwise equal to the two-launch path, and the [B, G, D, h, w] volume is never stored."""
+    B, C, h, w = (int(v) for v in L.shape)
+    if not gwc_stem_supported(pc, C, G):
+        raise ValueError("gwc_stem: needs a 3x3x3 stride-1 stem with 8 couts over 2-channel groups")
+    for t in (L, R) + ((att,) if att is not None else ()):
+        require_device(t, "gwc_stem input")
+        if t.stride(-1) != 1:
+            raise ValueError("gwc_stem: inputs must be contiguous along W")
+    virt = L.as_strided((B, G, D, h, w), (0, 0, 0, 0, 1))  # geometry only: the sources are replaced below
+    d, out, meta = _conv_desc(ctx, pc, [virt], out, tag=tag, hint=HINT_GWC_STEM)
+    for i, t in enumerate((L, R, att)):
+        if t is None:
+            d.src[i].ptr, d.src[i].C = None, 0
+            d.src[i].sb = d.src[i].sc = d.src[i].sd = d.src[i].sh = 0
+            continue
+        st = t.stride()
+        d.src[i].ptr = t.data_ptr()
+        d.src[i].C = int(t.shape[1])
+        d.src[i].sb, d.src[i].sc, d.src[i].sd, d.src[i].sh = st[0], st[1], 0, st[2]
+    d.nsrc = 3 if att is not None else 2
+    d.hint = HINT_GWC_STEM
+    ctx.hold(L, R, att)
+    meta.update(bytes=4 * B * (2 * C * h * w + (G * h * w if att is not None else 0) + pc.cout * D * h * w) +
+                4 * pc.w.numel(), reads=_spans(L, R, att), shape="gwc+" + meta["shape"])
+    ctx.meta.append(meta)
+    ctx.conv(d)
+    return out
+
+
 # Fused pairs (esm_conv_pair_f32) are used unless ESM_NO_PAIR is set (A/B measurements).
 PAIRS_ENABLED = not os.environ.get("ESM_NO_PAIR")
 

@@ -29,7 +29,7 @@ from . import _lib
 from ._lib import check, lib
 from .backbone import StubFeature
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
-from .engine import Ctx, require_device
+from .engine import Ctx, GWC_STEM_ENABLED, gwc_stem_supported, require_device, run_gwc_stem
 
 __all__ = ["ESMStereo", "FeatUp", "HotPath"]
 
@@ -246,10 +246,16 @@ class ESMStereo(nn.Module):
         D = self.maxdisp // self.vol_size
         vs = self.vol_size
         if self.gwc:
-            V = ctx.empty(B, self.num_groups, D, h, w)
             a = att.reshape(B, self.num_groups, h, w) if (vs == 16 and att is not None) else None
-            ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
-            vol = self.group_stem.emit(ctx, [V])
+            pc = self.group_stem.packed()
+            if GWC_STEM_ENABLED and gwc_stem_supported(pc, C, self.num_groups):
+                # build_gwc_volume (+ `* att`) fused into group_stem: the volume never reaches HBM
+                vol = run_gwc_stem(ctx, pc, ml, mr, a, D, self.num_groups,
+                                   tag=getattr(self.group_stem, "_esm_name", "group_stem"))
+            else:
+                V = ctx.empty(B, self.num_groups, D, h, w)
+                ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
+                vol = self.group_stem.emit(ctx, [V])
         elif self.norm_correlation:
             V = ctx.empty(B, 1, D, h, w)
             work = ctx.empty(2, B, C, h, w)

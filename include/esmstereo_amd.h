@@ -107,7 +107,12 @@ typedef struct {
     int32_t up_h, up_w, up_f;
     int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 10 |
                      rows-per-wave << 12 | C1T << 16 | STEM << 17 (16-block 4x4x1 MFMA form for
-                     3x3(x3) s1 convs with 8/12/16/24/32 couts) | NO_STEM << 18 (automatic, without it)
+                     3x3(x3) s1 convs with 8/12/16/24/32 couts) | NO_STEM << 18 (automatic, without it) |
+                     GWC_STEM << 19: the input is the VIRTUAL gwc volume (build_gwc_volume, 2 channels per
+                     group, models/submodule.py:151-161; `* att` of ESMStereo.py:711) of src[0] = L and
+                     src[1] = R ([B, 2*Cin, h, w]) and src[2] = att ([B, Cin, h, w] or ptr NULL); Di/Hi/Wi =
+                     D/h/w; a 3x3x3 s1 p1 stem with 8 couts; bitwise equal to esm_gwc_volume_f32 followed
+                     by esm_conv_f32 on the volume, without storing the volume
                      (tuning sweeps / tests; see conv_impl.h launch_geom) */
     int64_t ub, uh;
     float post_scale;

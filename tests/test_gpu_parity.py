@@ -599,3 +599,27 @@ def test_expected_raises():
         with pytest.raises(RuntimeError):
             with torch.no_grad():
                 model(left, left, False)
+
+
+@pytest.mark.parametrize("B,G,D,h,w,att", [(1, 32, 12, 24, 78, True), (2, 32, 5, 7, 13, False), (1, 32, 48, 20, 60, False),
+                                           (1, 4, 6, 9, 31, True)])
+def test_gwc_stem_fused(B, G, D, h, w, att):
+    """build_gwc_volume (+ `* att`) fused into group_stem (conv_stem.hip, GV form) vs the oracle volume
+    through an fp64 conv (1e-5 relative), and bitwise vs the two-launch path."""
+    from esmstereo_amd.engine import run_gwc_stem
+
+    L, R = feature_pair(B, 2 * G, h, w, 9, max(D, 2))
+    a = torch.rand(B, G, h, w) + 0.5 if att else None
+    conv, bn = _mk(3, G, 8, 3, 1, 1, seed=6)
+    p = pk(conv, bn, ACT_GELU)
+    V = O.gwc_volume(L, R, D, G)
+    if a is not None:
+        V = V * a.unsqueeze(2)
+    ref = _ref_conv([V], conv, bn, ACT_GELU)
+    ctx = Ctx(DEV)
+    y = run_gwc_stem(ctx, p, L.to(DEV), R.to(DEV), a.to(DEV) if a is not None else None, D, G)
+    assert rel(y, ref) < 1e-5
+    V2 = torch.empty(B, G, D, h, w, device=DEV)
+    ctx.gwc(L.to(DEV), R.to(DEV), a.to(DEV) if a is not None else None, V2, B, 2 * G, h, w, D, G)
+    # same voxel values, same chunking and accumulation order: bitwise equal to volume -> stem
+    assert torch.equal(y, run_conv(ctx, p, [V2]))
