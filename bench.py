@@ -22,7 +22,10 @@ Printed (rank 0, one JSON line): the contract fields, plus
                 (the north_star headline: HBM fraction of the volume kernel);
   cpu_baseline  the CPU oracle (oracle/esm_oracle.py, PyTorch fp32 on the host cores) timed
                 on a bounded sample of the same workload, rank 0 at N = 1 only;
-  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input.
+  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input;
+  concurrent    (N = 1) serving-style side measurement: --streams independent hot-path instances
+                (own buffers and graphs, same batch per instance) replayed concurrently on as many
+                HIP streams.  `value` stays the single-stream rate.
 """
 from __future__ import annotations
 
@@ -159,6 +162,40 @@ def cost_volume_roofline(device, reps: int = 20) -> dict:
             "min_us": round(ms[0] * 1e3, 2)}
 
 
+def concurrent_streams(model, ml, mr, att, up, n: int, steps: int, warmup: int, device) -> dict:
+    """Serving-style throughput at batch 1: ``n`` independent hot-path instances (own buffers, own
+    hipGraph) replayed concurrently on ``n`` HIP streams, so one pair's latency-bound small launches
+    overlap another's.  Reported beside the contract value, which stays the single-stream B=1 rate."""
+    B, C, h, w = (int(v) for v in ml.shape)
+    paths = []
+    for _ in range(n):
+        hp = E.HotPath(model, B, h, w, 0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], device,
+                       graph=True, channels=C)
+        hp.load_inputs(ml, mr, att, up)
+        paths.append(hp)
+    streams = [torch.cuda.Stream(device) for _ in range(n)]
+    main = torch.cuda.current_stream(device)
+
+    def round_():
+        for hp, st in zip(paths, streams):
+            st.wait_stream(main)
+            hp.launch(st)
+        for st in streams:
+            main.wait_stream(st)
+
+    for _ in range(warmup):
+        round_()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        round_()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    same = all(torch.equal(hp.outputs[0], paths[0].outputs[0]) for hp in paths[1:])
+    return {"streams": n, "value": round(n * B * steps / el, 2), "unit": "pairs/s", "batch_per_stream": B,
+            "ms_per_round": round(el / steps * 1e3, 4), "outputs_identical": bool(same)}
+
+
 def cpu_baseline(model, ml, mr, att, up, args, budget_s: float) -> tuple:
     from oracle import esm_oracle as O
 
@@ -199,6 +236,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the cost-volume roofline side measurement")
     ap.add_argument("--kernel-table", default="", help="write the per-op probe table (json) here")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="side measurement: independent B-pair instances on this many concurrent streams")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -315,6 +354,9 @@ def main() -> None:
         }
         if not args.no_extra:
             line["roofline_cost_volume"] = cost_volume_roofline(dev)
+            if world == 1 and args.streams > 1:
+                line["concurrent"] = concurrent_streams(model, ml, mr, att, up, args.streams, args.steps, args.warmup,
+                                                        dev)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref = cpu_baseline(model, ml, mr, att, up, args, args.cpu_seconds)
             line["cpu_baseline"] = cb
