@@ -284,10 +284,10 @@ int launch_pair_t(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s)
     const int H = b.Ho, W = b.Wo;
     const long long tiles_w = (W + G::VALID - 1) / G::VALID;
     const long long rows = static_cast<long long>(a.B) * H * tiles_w;
-    // rows per wave: enough waves to fill the chip (about 2 per SIMD), 2..8 rows each (each A row
-    // is computed once and reused by KB output rows; the first KB-1 are the wave's warm-up)
-    const long long want = rows / 2048;
-    const int rw = static_cast<int>(want < 2 ? 2 : (want > 8 ? 8 : want));
+    // rows per wave (each A row is computed once and reused by KB output rows; the first KB-1 are
+    // the wave's warm-up).  Swept on MI355X in the S-K launch sequence: the 192x624 agg_1 pair is
+    // fastest at 3 (31.1 us vs 35.9 at 4, 37.5 at 2), the 24x78 FMBlock pairs at 1 (10.4 vs 12.6 at 2)
+    const int rw = rows >= 6144 ? 3 : (rows >= 2048 ? 2 : 1);
     const long long nwg = tiles_w * ((H + 4 * rw - 1) / (4 * rw)) * a.B;
     if (nwg > 0x7fffffffLL) return arg_error("conv pair: grid too large");
     hipLaunchKernelGGL((pair_kernel<KA, KB, MA, MB, NKA>), dim3(static_cast<unsigned>(nwg)), dim3(kPairThreads),
