@@ -29,6 +29,140 @@ namespace conv {
 constexpr int kC1Threads = 256;
 constexpr int kC1TH = 16;  // output rows per tile
 
+// 2-D: the input tile of all channels (<= 32) and the weights staged with one batch of loads.
+template <bool D3, int CP, int QW>
+__global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_conv_desc a) {
+    constexpr int TW = 16 * QW;               // output columns per tile
+    constexpr int IR = kC1TH / 2 + 2;         // input rows of the tile
+    constexpr int IC = TW / 2 + 2;            // input columns of the tile
+    constexpr int ICP = (IC + 3) / 4 * 4;     // padded LDS row (16-B aligned rows)
+    constexpr int NP = D3 ? 2 : 1;            // input planes per output plane
+    constexpr int NQZ = D3 ? 2 : 1;
+    constexpr int XN = NP * CP * IR * IC;     // staged input elements
+    constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
+    constexpr int WN = NQZ * 2 * CP * 2 * 4 * NP;  // staged weights [qz][qy][c][qx][tz][ty][tx]
+    constexpr int WR = (WN + kC1Threads - 1) / kC1Threads;
+    constexpr int TAPS = D3 ? 8 : 4;
+    __shared__ __attribute__((aligned(16))) float xs[NP][CP][IR][ICP];
+    __shared__ __attribute__((aligned(16))) float ws[NQZ][2][CP][2][NP][4];
+
+    const int tid = threadIdx.x;
+    const int Ho = a.Ho, Wo = a.Wo, Do = D3 ? a.Do : 1;
+    const int Y0 = blockIdx.y * kC1TH, X0 = blockIdx.x * TW;
+    const int b = blockIdx.z / Do;
+    const int oz = blockIdx.z - b * Do;
+    const int qz = D3 ? (oz & 1) : 0;
+    const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
+    const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
+    const esm_src& sr = a.src[0];
+    const float* xb = sr.ptr + b * sr.sb;
+
+    // ---- stage: every load of the thread in flight together, then the LDS stores
+    float rx[XR], rw[WR];
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int i = tid + k * kC1Threads;
+        const int col = i % IC;
+        const int row = (i / IC) % IR;
+        const int c = (i / (IC * IR)) % CP;
+        const int p = i / (IC * IR * CP);
+        const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
+        const bool ok = i < XN && c < a.Cin && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi &&
+                        (!D3 || (iz >= 0 && iz < a.Di));
+        const float v = xb[ok ? c * sr.sc + (D3 ? iz * sr.sd : 0) + iy * sr.sh + ix : 0];
+        rx[k] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        // LDS index (qz, qy, c, qx, tz, ty, tx) <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
+        const int i = tid + k * kC1Threads;
+        const int tyx = i & 3;
+        const int tz = (i >> 2) % NP;
+        const int qx = (i / (4 * NP)) & 1;
+        const int c = (i / (8 * NP)) % CP;
+        const int qy = (i / (8 * NP * CP)) & 1;
+        const int qzz = i / (16 * NP * CP);
+        const int cls = D3 ? (qzz << 2 | qy << 1 | qx) : (qy << 1 | qx);
+        const int tap = D3 ? (tz << 2 | tyx) : tyx;
+        const bool ok = i < WN && c < a.cin_pad;
+        const float v = a.w[ok ? ((static_cast<long long>(cls) * TAPS + tap) * a.cin_pad + c) * a.cout_pad : 0];
+        rw[k] = ok ? v : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int i = tid + k * kC1Threads;
+        if (i < XN) {
+            const int col = i % IC;
+            const int row = (i / IC) % IR;
+            const int c = (i / (IC * IR)) % CP;
+            const int p = i / (IC * IR * CP);
+            xs[p][c][row][col] = rx[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        const int i = tid + k * kC1Threads;
+        if (i < WN) (&ws[0][0][0][0][0][0])[i] = rw[k];
+    }
+    __syncthreads();
+
+    // ---- thread: output row Y0 + r (wave w: rows of parity w & 1), columns X0 + QW*g ...
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int qy = wave & 1;
+    const int g = lane % 16;
+    const int r = 2 * ((wave >> 1) * 4 + lane / 16) + qy;
+    const int oy = Y0 + r;
+    const int lr = r / 2 + 1 + qy;  // tile row of input m + q (row tap t = 0); t = 1 is lr - 1
+    const int lc = QW / 2 * g;      // first tile column the thread reads (QW = 1: see below)
+    constexpr int NV = QW / 2 + 2;  // tile columns per row the thread reads
+    float acc[QW];
+#pragma unroll
+    for (int j = 0; j < QW; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int tz = 0; tz < NP; ++tz) {
+        const int p = D3 ? 1 - tz : 0;  // plane tap t = tz sits at tile plane 1 - t
+#pragma unroll 4
+        for (int c = 0; c < CP; ++c) {
+            float v[2][NV];
+#pragma unroll
+            for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+                for (int j = 0; j < NV; ++j) v[ty][j] = xs[p][c][lr - ty][lc + j];
+#pragma unroll
+            for (int j = 0; j < QW; ++j) {
+                const int qx = j & 1;
+                // input m + qx - tx of output column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
+#pragma unroll
+                for (int ty = 0; ty < 2; ++ty)
+#pragma unroll
+                    for (int tx = 0; tx < 2; ++tx)
+                        acc[j] += ws[qz][qy][c][qx][tz][ty * 2 + tx] * v[ty][1 + (j >> 1) + qx - tx];
+            }
+        }
+    }
+    if (oy >= Ho) return;
+    const int ox0 = X0 + QW * g;
+    const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;
+    if constexpr (QW == 4) {
+        const bool plain = !a.mul && !a.res && !a.out2;
+        if (plain && ox0 + 3 < Wo && ((o | a.oh) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0) {
+            floatx4 v4;
+            v4.x = conv_finish(a, acc[0], b, 0, oz, oy, ox0 + 0) * a.post_scale;
+            v4.y = conv_finish(a, acc[1], b, 0, oz, oy, ox0 + 1) * a.post_scale;
+            v4.z = conv_finish(a, acc[2], b, 0, oz, oy, ox0 + 2) * a.post_scale;
+            v4.w = conv_finish(a, acc[3], b, 0, oz, oy, ox0 + 3) * a.post_scale;
+            *reinterpret_cast<floatx4*>(a.out + o) = v4;
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < QW; ++j)
+        if (ox0 + j < Wo) conv_put(a, conv_finish(a, acc[j], b, 0, oz, oy, ox0 + j), b, 0, oz, oy, ox0 + j);
+}
+
+// 3-D: channel chunks of CC, the next chunk's loads in flight during the current one's FMAs.
 template <bool D3, int CC, int QW>
 __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_desc a) {
     constexpr int TW = 16 * QW;               // output columns per tile
@@ -185,14 +319,14 @@ int launch_convt_c1_q(const esm_conv_desc& a, hipStream_t s) {
     const int Do = D3 ? a.Do : 1;
     dim3 grid(ceil_div(a.Wo, 16 * QW), ceil_div(a.Ho, kC1TH), static_cast<unsigned>(a.B) * Do);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-    // channel chunks: 8 at a time in 3-D (two input planes per output plane); 2-D stages all
-    // channels at once (one chunk of 16 or 32)
+    // 3-D: channel chunks of 8 (two input planes per output plane); 2-D: every channel in one
+    // batch (the chunked kernel with one chunk measured 1.8 us slower at S-K ref4x.conv1_up)
     if constexpr (D3)
         hipLaunchKernelGGL((convt_c1_kernel<D3, 8, QW>), grid, dim3(kC1Threads), 0, s, a);
     else if (a.Cin <= 16)
-        hipLaunchKernelGGL((convt_c1_kernel<D3, 16, QW>), grid, dim3(kC1Threads), 0, s, a);
+        hipLaunchKernelGGL((convt_c1_batch_kernel<D3, 16, QW>), grid, dim3(kC1Threads), 0, s, a);
     else
-        hipLaunchKernelGGL((convt_c1_kernel<D3, 32, QW>), grid, dim3(kC1Threads), 0, s, a);
+        hipLaunchKernelGGL((convt_c1_batch_kernel<D3, 32, QW>), grid, dim3(kC1Threads), 0, s, a);
     return check_launch("conv(c1 transposed)");
 }
 
