@@ -15,6 +15,7 @@ int launch_normcorr(const float*, const float*, float*, float*, int, int, int, i
 int launch_regression(int, const float*, const float*, float*, int, int, int, int, hipStream_t);
 int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
+int launch_fmnet(const esm_fmnet_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 namespace conv {
 int launch_conv_pair(const esm_conv_desc*, const esm_conv_desc*, hipStream_t);
@@ -33,7 +34,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8, kFmnet = 9 };
 
 struct VolArgs {
     const float* L;
@@ -56,6 +57,7 @@ struct Op {
     esm_conv_desc conv{};
     esm_conv_desc conv2{};
     esm_smix_desc smix{};
+    esm_fmnet_desc fm{};
     esm_shuffle_tail_desc st{};
     VolArgs vol{};
     RegArgs reg{};
@@ -65,6 +67,7 @@ int run_op(const Op& op, hipStream_t s) {
     switch (op.kind) {
         case kConv: return esm::launch_conv(&op.conv, s);
         case kSmix: return esm::launch_smix(&op.smix, s);
+        case kFmnet: return esm::launch_fmnet(&op.fm, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
         case kConvPair: return esm::conv::launch_conv_pair(&op.conv, &op.conv2, s);
         case kGwc:
@@ -191,6 +194,7 @@ int esm_struct_size(int which) {
         case 2: return static_cast<int>(sizeof(esm_smix_stage));
         case 3: return static_cast<int>(sizeof(esm_smix_desc));
         case 4: return static_cast<int>(sizeof(esm_shuffle_tail_desc));
+        case 5: return static_cast<int>(sizeof(esm_fmnet_desc));
         default: return -1;
     }
 }
@@ -219,6 +223,14 @@ int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc) {
     Op op;
     op.kind = kSmix;
     op.smix = *desc;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc) {
+    if (!desc) return esm::arg_error("plan: null fmnet desc");
+    Op op;
+    op.kind = kFmnet;
+    op.fm = *desc;
     return add_op(plan, std::move(op));
 }
 

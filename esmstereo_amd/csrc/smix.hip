@@ -210,6 +210,124 @@ int launch_c(const esm_smix_desc& a, hipStream_t s) {
     return check_launch("smix");
 }
 
+// The whole `net` of an FMBlock (two SMLayers, models/shufflemixer.py:100-112,129-130) in one
+// launch instead of three smix launches (mlp1 | dw0 -> mlp2 -> mlp1 | dw1 -> mlp2, + x), with halo
+// recomputation.  A workgroup owns a kFTH x kFTW output tile: it computes t1 on the tile plus a 2R
+// halo and t2 on the tile plus an R halo (each zero outside the image: the depthwise convs' zero
+// padding), then the output.  Per pixel and channel the operations and their order are those of
+// smix_kernel (equal to the three-launch chain up to the compiler's FMA contraction choices).
+constexpr int kFTH = 4;
+constexpr int kFTW = 16;
+
+template <int C, int K>
+__global__ void __launch_bounds__(kThreads) fmnet_kernel(const esm_fmnet_desc a) {
+    using Lyt = SmixLayout<C>;
+    constexpr int R = K / 2;
+    constexpr int AH = kFTH + 4 * R, AW = kFTW + 4 * R, AP = AH * AW;  // t1 region
+    constexpr int BH = kFTH + 2 * R, BW = kFTW + 2 * R, BP = BH * BW;  // t2 region
+    constexpr int CP = kFTH * kFTW;                                      // output tile
+    constexpr int AWP = AW + 1, BWP = BW + 1;
+    constexpr int DW0 = 4 * Lyt::STAGE, DW1 = DW0 + C * K * K + C;
+    constexpr int NW = DW1 + C * K * K + C;
+    __shared__ float wsh[NW];
+    __shared__ float s1[C * AH * AWP];  // t1 image, then t2 image ([C][BH][BWP])
+    __shared__ float s2[C * BP];        // depthwise results: region B, then the tile
+    const int tid = threadIdx.x;
+    const int H = a.H, W = a.W;
+    const int b = blockIdx.z;
+    const int y0 = blockIdx.y * kFTH, x0 = blockIdx.x * kFTW;
+    const long long plane = static_cast<long long>(H) * W;
+    const float* xb = a.x + static_cast<long long>(b) * C * plane;
+
+    // weights: stage s (ln | fc0_w | fc0_b | fc2_w | fc2_b) for s = 0..3, then dw0 w, b, dw1 w, b
+    for (int i = tid; i < NW; i += kThreads) {
+        const float* p;
+        int off;
+        if (i < DW0) {
+            const esm_smix_stage& g = a.stage[i / Lyt::STAGE];
+            const int j = i % Lyt::STAGE;
+            p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
+            off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
+        } else {
+            const int l = i < DW1 ? 0 : 1;
+            const int j = i - (l ? DW1 : DW0);
+            p = j < C * K * K ? a.dw_w[l] : a.dw_b[l];
+            off = j < C * K * K ? j : j - C * K * K;
+        }
+        wsh[i] = p[off];
+    }
+    __syncthreads();
+    // t1 = SMLayer0.mlp1 (x) on region A
+    for (int q = tid; q < AP; q += kThreads) {
+        const int ly = q / AW, lx = q - (q / AW) * AW;
+        const int gy = y0 - 2 * R + ly, gx = x0 - 2 * R + lx;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        float t[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) t[c] = in ? xb[c * plane + gy * W + gx] : 0.f;
+        if (in) mix_stage<C>(t, wsh);
+#pragma unroll
+        for (int c = 0; c < C; ++c) s1[(c * AH + ly) * AWP + lx] = in ? t[c] : 0.f;
+    }
+    __syncthreads();
+    // dw0 (t1) on region B
+    for (int i = tid; i < C * BP; i += kThreads) {
+        const int c = i / BP, p = i - (i / BP) * BP;
+        const int py = p / BW, px = p - (p / BW) * BW;
+        const float* w = wsh + DW0 + c * K * K;
+        float sacc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) sacc += w[ky * K + kx] * s1[(c * AH + py + ky) * AWP + px + kx];
+        s2[c * BP + p] = sacc + wsh[DW0 + C * K * K + c];
+    }
+    __syncthreads();
+    // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
+    for (int p = tid; p < BP; p += kThreads) {
+        const int py = p / BW, px = p - (p / BW) * BW;
+        const int gy = y0 - R + py, gx = x0 - R + px;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        float t[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) t[c] = s2[c * BP + p];
+        if (in) {
+            mix_stage<C>(t, wsh + Lyt::STAGE);
+            mix_stage<C>(t, wsh + 2 * Lyt::STAGE);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
+    }
+    __syncthreads();
+    // dw1 (t2) on the tile
+    for (int i = tid; i < C * CP; i += kThreads) {
+        const int c = i / CP, p = i - (i / CP) * CP;
+        const int py = p / kFTW, px = p - (p / kFTW) * kFTW;
+        const float* w = wsh + DW1 + c * K * K;
+        float sacc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) sacc += w[ky * K + kx] * s1[(c * BH + py + ky) * BWP + px + kx];
+        s2[c * CP + p] = sacc + wsh[DW1 + C * K * K + c];
+    }
+    __syncthreads();
+    // out = SMLayer1.mlp2 (dw1) + x on the tile
+    if (tid >= CP) return;
+    const int py = tid / kFTW, px = tid - (tid / kFTW) * kFTW;
+    const int y = y0 + py, x = x0 + px;
+    if (y >= H || x >= W) return;
+    float t[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
+    mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
+    const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
+#pragma unroll
+    for (int c = 0; c < C; ++c) a.out[pix + c * plane] = t[c];
+}
+
 }  // namespace
 
 int launch_smix(const esm_smix_desc* d, hipStream_t s) {
@@ -230,7 +348,37 @@ int launch_smix(const esm_smix_desc* d, hipStream_t s) {
     return ESM_ERR_UNSUPPORTED;
 }
 
+int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
+    if (!d) return arg_error("fmnet: null descriptor");
+    const esm_fmnet_desc& a = *d;
+    if (!a.x || !a.out || !a.dw_w[0] || !a.dw_b[0] || !a.dw_w[1] || !a.dw_b[1]) return arg_error("fmnet: null pointer");
+    if (a.x == a.out) return arg_error("fmnet: cannot run in place");
+    if (a.B <= 0 || a.H <= 0 || a.W <= 0) return arg_error("fmnet: bad size");
+    for (int i = 0; i < 4; ++i) {
+        const esm_smix_stage& st = a.stage[i];
+        if (!st.ln_w || !st.fc0_w || !st.fc0_b || !st.fc2_w || !st.fc2_b) return arg_error("fmnet: null stage weights");
+    }
+    if (a.dw_k != 7) {
+        set_error("fmnet: depthwise kernel must be 7 (FMBlock kernel_size)");
+        return ESM_ERR_UNSUPPORTED;
+    }
+    const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, kFTH), a.B);
+    if (a.C == 8)
+        hipLaunchKernelGGL((fmnet_kernel<8, 7>), grid, dim3(kThreads), 0, s, a);
+    else if (a.C == 16)
+        hipLaunchKernelGGL((fmnet_kernel<16, 7>), grid, dim3(kThreads), 0, s, a);
+    else {
+        set_error("fmnet: C must be 8 or 16");
+        return ESM_ERR_UNSUPPORTED;
+    }
+    return check_launch("fmnet");
+}
+
 }  // namespace esm
+
+extern "C" int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream) {
+    return esm::launch_fmnet(desc, esm::as_stream(stream));
+}
 
 extern "C" int esm_smix_f32(const esm_smix_desc* desc, void* stream) {
     return esm::launch_smix(desc, esm::as_stream(stream));

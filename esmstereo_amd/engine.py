@@ -232,6 +232,12 @@ class Ctx:
         else:
             check(lib.esm_conv_pair_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair")
 
+    def fmnet(self, d) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_fmnet(self.plan, ctypes.byref(d)), "plan_add_fmnet")
+        else:
+            check(lib.esm_fmnet_f32(ctypes.byref(d), self.stream), "fmnet")
+
     def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
         if self.plan:
             check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
@@ -607,6 +613,50 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
                          bytes=4 * npix * C * (3 if res is not None else 2), shape=f"C{C} {H}x{W} dw{d.dw_k}",
                          reads=_spans(x, res), writes=_spans(out)))
     ctx.smix(d)
+    return out
+
+
+# FMBlock.net as one launch (esm_fmnet_f32): opt-in (ESM_FMNET=1).  Measured on MI355X it saves no
+# time (S-K 1916 vs 1914 pairs/s) and loses at L (397 vs 404): the fused kernel's four
+# barrier-separated phases on a 4x16 tile plus a 6-pixel halo run longer than the launches they
+# replace.
+FMNET_ENABLED = os.environ.get("ESM_FMNET") == "1"
+
+
+def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
+              dw1: Tuple[torch.Tensor, torch.Tensor], out: Optional[torch.Tensor] = None,
+              tag: str = "fmnet") -> torch.Tensor:
+    """``FMBlock.net(x) + x`` (shufflemixer.py:129-130) in one launch: stages = SMLayer0.mlp1, .mlp2,
+    SMLayer1.mlp1, .mlp2; dw0 / dw1 = the two SMLayers' depthwise convs (weight, bias)."""
+    require_device(x, "fmnet input")
+    if not x.is_contiguous():
+        raise ValueError("fmnet: input must be contiguous")
+    if len(stages) != 4:
+        raise ValueError("fmnet: four mlp stages")
+    B, C, H, W = (int(v) for v in x.shape)
+    if out is None:
+        out = ctx.empty(B, C, H, W)
+    d = _lib.EsmFmnetDesc()
+    d.x, d.out = x.data_ptr(), out.data_ptr()
+    d.dw_w[0], d.dw_b[0] = dw0[0].data_ptr(), dw0[1].data_ptr()
+    d.dw_w[1], d.dw_b[1] = dw1[0].data_ptr(), dw1[1].data_ptr()
+    d.dw_k = int(dw0[0].shape[-1])
+    if int(dw1[0].shape[-1]) != d.dw_k:
+        raise ValueError("fmnet: both SMLayers need the same depthwise kernel")
+    require_on(x.device, "fmnet", x, out, *dw0, *dw1,
+               *[t for st in stages for t in (st.ln_w, st.fc0_w, st.fc0_b, st.fc2_w, st.fc2_b)])
+    for i, st in enumerate(stages):
+        d.stage[i].ln_w = st.ln_w.data_ptr()
+        d.stage[i].fc0_w, d.stage[i].fc0_b = st.fc0_w.data_ptr(), st.fc0_b.data_ptr()
+        d.stage[i].fc2_w, d.stage[i].fc2_b = st.fc2_w.data_ptr(), st.fc2_b.data_ptr()
+        ctx.hold(st.ln_w, st.fc0_w, st.fc0_b, st.fc2_w, st.fc2_b)
+    d.B, d.C, d.H, d.W = B, C, H, W
+    ctx.hold(x, out, *dw0, *dw1)
+    npix = B * H * W
+    ctx.meta.append(dict(name=tag, kind="fmnet", flops=npix * (2 * C * C * 4 + 2 * 2 * C * d.dw_k ** 2),
+                         bytes=4 * npix * C * 2, shape=f"C{C} {H}x{W} dw{d.dw_k} x2",
+                         reads=_spans(x), writes=_spans(out)))
+    ctx.fmnet(d)
     return out
 
 

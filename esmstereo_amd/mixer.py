@@ -18,7 +18,8 @@ from typing import List
 import torch
 import torch.nn as nn
 
-from .engine import ACT_NONE, ACT_SILU, Ctx, SmixStage, pack_conv, param_token, run_conv_pair, run_smix
+from .engine import (ACT_NONE, ACT_SILU, FMNET_ENABLED, Ctx, SmixStage, pack_conv, param_token, run_conv_pair,
+                     run_fmnet, run_smix)
 
 __all__ = ["BiasFree_LayerNorm", "LayerNorm", "SplitPointMlp", "SMLayer", "FMBlock"]
 
@@ -116,9 +117,13 @@ class FMBlock(nn.Module):
     def emit(self, ctx: Ctx, x: torch.Tensor) -> torch.Tensor:
         p = self._packed()
         me = getattr(self, "_esm_name", "FMBlock")
-        t1 = run_smix(ctx, x, [p["a1"]], tag=f"{me}.net.0.mlp1")
-        t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"], tag=f"{me}.net.0.spatial+mlp2+net.1.mlp1")
-        t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x, tag=f"{me}.net.1.spatial+mlp2+res")
+        if FMNET_ENABLED and int(x.shape[1]) in (8, 16) and int(p["dw0"][0].shape[-1]) == 7:
+            # the two SMLayers + x as one launch (the same operations as the three below)
+            t3 = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], tag=f"{me}.net")
+        else:
+            t1 = run_smix(ctx, x, [p["a1"]], tag=f"{me}.net.0.mlp1")
+            t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"], tag=f"{me}.net.0.spatial+mlp2+net.1.mlp1")
+            t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x, tag=f"{me}.net.1.spatial+mlp2+res")
         # conv.0 (3x3 + SiLU) and conv.2 (1x1) + residual: one fused launch (esm_conv_pair_f32)
         return run_conv_pair(ctx, p["c0"], [t3], p["c2"], res=t3, tag=f"{me}.conv.0+2",
                              tags=(f"{me}.conv.0", f"{me}.conv.2"))

@@ -19,6 +19,7 @@
  *                             129-509 with their fused neighbours (crop+cat :172,177,230,234;
  *                             PixelShuffle+SiLU :265-268; bilinear-upsample + add :307,316;
  *                             `* att` :703; residual adds of models/shufflemixer.py:130-131)
+ *   esm_fmnet_f32             models/shufflemixer.py:100-112,129-130 FMBlock.net (two SMLayers) + x
  *   esm_smix_f32              models/shufflemixer.py:23-112 LayerNorm('BiasFree') +
  *                             SplitPointMlp + channel shuffle + residual, optionally preceded
  *                             by the depthwise 7x7 `spatial` conv
@@ -146,6 +147,22 @@ typedef struct {
     int32_t B, C, H, W;
 } esm_smix_desc;
 
+/* The whole `net` of an FMBlock (two SMLayers, models/shufflemixer.py:100-112,129-130) in one launch:
+ * out = SMLayer1(SMLayer0(x)) + x, where SMLayer(t) = mlp2(dw(mlp1(t))) with mlp = the per-pixel
+ * LN -> SplitPointMlp -> shuffle -> residual chain of esm_smix_desc.  stage[] = SMLayer0.mlp1,
+ * SMLayer0.mlp2, SMLayer1.mlp1, SMLayer1.mlp2; dw_w/dw_b[l] = SMLayer l's depthwise K x K conv
+ * (K = 7); C in {8, 16}.  The three esm_smix_f32 launches it replaces, in one (same operations). */
+typedef struct {
+    const float* x;
+    float* out;
+    const float* dw_w[2];
+    const float* dw_b[2];
+    int32_t dw_k;
+    int32_t reserved;
+    esm_smix_stage stage[4];
+    int32_t B, C, H, W;
+} esm_fmnet_desc;
+
 /* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,
  * silu(pixel_shuffle(conv1x1(up_w, x) + up_b, r))), zero padding 1.  (nf, r) in
  * {(8,2), (8,4), (16,2), (16,4)}.  x: [B, nf, H, W] with strides xb, xc, xh (innermost 1);
@@ -166,7 +183,7 @@ typedef struct {
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc; -1 for an unknown id. */
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc; -1 for an unknown id. */
 int esm_struct_size(int which);
 
 int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* V, int B, int C, int H, int W,
@@ -182,6 +199,7 @@ int esm_topk2_regression_f32(const float* cost, const float* samples, float* out
                              void* stream);
 int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
+int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
 /* out_b = epilogue_b(conv_b(epilogue_a(conv_a(src_a)))): `a` describes the first conv (its sources,
  * weights, BN/bias, activation; a->out is not written, a->res must be NULL), `b` the second (its
@@ -207,6 +225,7 @@ esm_plan* esm_plan_create(void);
 void esm_plan_destroy(esm_plan* plan);
 int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
+int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
 int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
@@ -219,7 +238,7 @@ int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float*
 int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 8 = conv_pair */
+ * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

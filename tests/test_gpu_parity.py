@@ -623,3 +623,25 @@ def test_gwc_stem_fused(B, G, D, h, w, att):
     ctx.gwc(L.to(DEV), R.to(DEV), a.to(DEV) if a is not None else None, V2, B, 2 * G, h, w, D, G)
     # same voxel values, same chunking and accumulation order: bitwise equal to volume -> stem
     assert torch.equal(y, run_conv(ctx, p, [V2]))
+
+
+@pytest.mark.parametrize("C,H,W", [(8, 24, 78), (8, 7, 13), (16, 96, 312), (16, 5, 40), (8, 1, 1)])
+def test_fmnet_fused_bitwise(C, H, W):
+    """FMBlock.net + x in one launch (esm_fmnet_f32, halo recomputation) vs the three smix launches:
+    the same per-pixel operations in the same order, up to the compiler's FMA contraction choices in
+    the two kernels (relative 1e-6)."""
+    from esmstereo_amd.engine import run_fmnet, run_smix
+
+    torch.manual_seed(C * 100 + H)
+    blk = E.FMBlock(C, 7).to(DEV).eval()
+    with torch.no_grad():
+        for prm in blk.parameters():
+            prm.uniform_(-0.5, 0.5)
+    p = blk._packed()
+    x = torch.randn(2, C, H, W, device=DEV)
+    ctx = Ctx(DEV)
+    fused = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"])
+    t1 = run_smix(ctx, x, [p["a1"]])
+    t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"])
+    t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x)
+    assert rel(fused, t3) < 1e-6
