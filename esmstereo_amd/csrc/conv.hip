@@ -11,11 +11,14 @@ bool stem_ok(const esm_conv_desc& a);                    // conv_stem.hip
 bool stem_auto(const esm_conv_desc& a);                  // conv_stem.hip
 int launch_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 int launch_gwc_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
+bool c1in_ok(const esm_conv_desc& a);                    // conv_stem.hip
+int launch_c1in(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
 constexpr int kHintNoStem = 1 << 18;  // automatic choice among the other forms
 constexpr int kHintGwcStem = 1 << 19;  // input = the virtual gwc volume of src[0..2] (conv_stem.hip)
+constexpr int kHintC1in = 1 << 20;     // force the VALU single-input-channel form (conv_stem.hip)
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -57,6 +60,12 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return arg_error("conv: output extent inconsistent with kernel/stride/padding");
     if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
+    if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
+    // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).
+    // Measured (scripts/probes/c1in_sweep.py, profiles/r01_c1in_sweep.txt): 1->16 k3s2 at 192x624
+    // output 8.6 us; on small maps the MFMA direct form wins (4.8 vs 11.6 us at 24x78)
+    if (a.hint == 0 && conv::c1in_ok(a) && static_cast<long long>(a.B) * a.Ho * a.Wo >= 65536)
+        return conv::launch_c1in(a, s);
     if (a.hint & kHintNoStem) {
         esm_conv_desc d = a;
         d.hint &= ~kHintNoStem;

@@ -397,6 +397,81 @@ int launch_gwc_stem(const esm_conv_desc& a, hipStream_t s) {
     return launch_sconv<true, 2, true>(a, s);
 }
 
+// Single-input-channel 2-D convs on the VALU: the refinement heads' first layer (BasicConv(1, C,
+// 3, s2, p1), models/ESMStereo.py:190-191) and the disparity feature heads dmNx.0 (BasicConv(1, C,
+// 5, p0), :247-248 and twins).  An MFMA tile pads the single channel to a 4-deep k-step (75% of
+// every MFMA wasted) and these layers are bandwidth-sized (K*K MACs per output), so one thread per
+// output pixel does all couts: K*K loads, K*K*Cout FMAs (weights as LDS broadcasts), Cout
+// coalesced stores.
+namespace {
+constexpr int kC1inTW = 64, kC1inTH = 4;
+
+template <int K, int S, int CO>
+__global__ void __launch_bounds__(256) c1in_kernel(const esm_conv_desc a) {
+    __shared__ float ws[K * K * CO + 2 * CO];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < K * K * CO; i += 256) {
+        const int tap = i / CO, co = i - (i / CO) * CO;
+        ws[i] = co < a.Cout ? a.w[static_cast<long long>(tap) * a.cin_pad * a.cout_pad + co] : 0.f;
+    }
+    if (tid < CO) {
+        const int co = min(tid, a.Cout - 1);
+        ws[K * K * CO + tid] = a.scale ? a.scale[co] : 1.f;
+        ws[K * K * CO + CO + tid] = a.shift ? a.shift[co] : 0.f;
+    }
+    const int b = blockIdx.z;
+    const int ox = blockIdx.x * kC1inTW + (tid & (kC1inTW - 1));
+    const int oy = blockIdx.y * kC1inTH + tid / kC1inTW;
+    const esm_src& s0 = a.src[0];
+    const float* xb = s0.ptr + b * s0.sb;
+    float xv[K * K];
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+            const int yi = oy * S - a.ph + ky, xi = ox * S - a.pw + kx;
+            const bool ok = oy < a.Ho && ox < a.Wo && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+            const float v = xb[ok ? static_cast<long long>(yi) * s0.sh + xi : 0];
+            xv[ky * K + kx] = ok ? v : 0.f;
+        }
+    __syncthreads();
+    if (oy >= a.Ho || ox >= a.Wo) return;
+    const long long o = b * a.ob + static_cast<long long>(oy) * a.oh + ox;
+#pragma unroll 4
+    for (int co = 0; co < CO; ++co) {
+        if (co >= a.Cout) break;
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < K * K; ++t) acc += ws[t * CO + co] * xv[t];
+        const float v = a.scale ? acc * ws[K * K * CO + co] + ws[K * K * CO + CO + co] : acc + ws[K * K * CO + CO + co];
+        a.out[o + co * a.oc] = apply_act(v, a.act) * a.post_scale;
+    }
+}
+
+template <int K, int S>
+int launch_c1in_k(const esm_conv_desc& a, hipStream_t s) {
+    const dim3 grid(ceil_div(a.Wo, kC1inTW), ceil_div(a.Ho, kC1inTH), a.B);
+    if (a.Cout <= 16)
+        hipLaunchKernelGGL((c1in_kernel<K, S, 16>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((c1in_kernel<K, S, 32>), grid, dim3(256), 0, s, a);
+    return check_launch("conv(1-channel input)");
+}
+}  // namespace
+
+bool c1in_ok(const esm_conv_desc& a) {
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    return !d3 && !a.transposed && a.Cin == 1 && a.nsrc == 1 && a.Cout <= 32 && a.shuffle <= 1 && !a.mul && !a.res &&
+           !a.up && !a.out2 && ((a.kh == 3 && (a.stride == 1 || a.stride == 2)) || (a.kh == 5 && a.stride == 1)) &&
+           a.src[0].ptr != nullptr;
+}
+
+int launch_c1in(const esm_conv_desc& a, hipStream_t s) {
+    if (!c1in_ok(a)) return arg_error("conv: 1-channel-input form not applicable");
+    if (a.kh == 5) return launch_c1in_k<5, 1>(a, s);
+    return a.stride == 2 ? launch_c1in_k<3, 2>(a, s) : launch_c1in_k<3, 1>(a, s);
+}
+
 // Layers this form takes: stride-1 3x3(x3) convs with "same" padding, one source, 8, 12, 16,
 // 24 or 32 output channels, no pixel shuffle, a weight slab that fits 64 KiB of LDS.
 bool stem_ok(const esm_conv_desc& a) {

@@ -113,7 +113,8 @@ typedef struct {
                      group, models/submodule.py:151-161; `* att` of ESMStereo.py:711) of src[0] = L and
                      src[1] = R ([B, 2*Cin, h, w]) and src[2] = att ([B, Cin, h, w] or ptr NULL); Di/Hi/Wi =
                      D/h/w; a 3x3x3 s1 p1 stem with 8 couts; bitwise equal to esm_gwc_volume_f32 followed
-                     by esm_conv_f32 on the volume, without storing the volume
+                     by esm_conv_f32 on the volume, without storing the volume |
+                     C1IN << 20: force the VALU form for 2-D convs with one input channel
                      (tuning sweeps / tests; see conv_impl.h launch_geom) */
     int64_t ub, uh;
     float post_scale;

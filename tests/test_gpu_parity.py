@@ -645,3 +645,15 @@ def test_fmnet_fused_bitwise(C, H, W):
     t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"])
     t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x)
     assert rel(fused, t3) < 1e-6
+
+
+@pytest.mark.parametrize("cout,k,s,p,H,W", [(16, 3, 2, 1, 384, 1248), (16, 5, 1, 0, 96, 312), (32, 5, 1, 0, 37, 50),
+                                            (16, 3, 2, 1, 9, 13), (32, 3, 2, 1, 96, 312), (8, 3, 1, 1, 20, 33)])
+def test_conv_c1in_form(cout, k, s, p, H, W):
+    """VALU single-input-channel 2-D form (conv_stem.hip c1in_kernel), forced and automatic, vs fp64."""
+    conv, bn = _mk(2, 1, cout, k, s, p, seed=7)
+    x = torch.randn(2, 1, H, W)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    pc = pk(conv, bn, ACT_GELU)
+    for h in (1 << 20, 0):
+        assert rel(run_conv(Ctx(DEV), pc, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
