@@ -30,8 +30,9 @@ from esmstereo_amd._lib import check, lib  # noqa: E402
 
 # 0 = automatic; LDS-staged NT|KS<<4; direct 0x200 (+ rows/wave << 12); rows 0x400; C1 0x114;
 # VALU transposed C1 0x10000
+# narrow-output 16-block form 1 << 17, automatic without it 1 << 18, VALU 1-input-channel form 1 << 20
 CANDIDATES = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x211, 0x212, 0x241, 0x242, 0x1211, 0x2211, 0x4211, 0x1212,
-              0x2212, 0x400, 0x114, 0x10000]
+              0x2212, 0x400, 0x114, 0x10000, 1 << 17, 1 << 18, 1 << 20]
 
 
 def op_time(hp, i: int, reps: int) -> float:
@@ -118,6 +119,9 @@ def main():
         with open(args.out) as f:
             table = json.load(f)
     for r in reports:
+        for op in r["ops"]:  # a key whose best is now the automatic choice drops its old hint
+            if op["best"] == "0x0":
+                table["hints"].pop(op["key"], None)
         table["hints"].update(r["hints"])
     table["source"] = ("scripts/autotune.py on " + torch.cuda.get_device_name(0) + ": " +
                        ", ".join(f"{r['variant']} {r['step_auto_us']}->{r['step_tuned_us']} us/step" for r in reports))
