@@ -221,6 +221,9 @@ int launch_nr(const esm_shuffle_tail_desc& a, hipStream_t s) {
     if constexpr (NF == 8 && R == 4) {
         if (big >= 256) return launch_tile<NF, R, 16, 32>(a, s);
     }
+    // nf = 16 (ESMStereo-L heads): 8 x 32 tiles (4x head at 384x1248: 38.9 vs 48.2 us for 8 x 64;
+    // 2x head equal)
+    if constexpr (NF == 16) return launch_tile<NF, R, 8, 32>(a, s);
     return big >= 256 ? launch_tile<NF, R, TH, 64>(a, s) : launch_tile<NF, R, 8, 32>(a, s);
 }
 
