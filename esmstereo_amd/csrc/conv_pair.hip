@@ -286,8 +286,9 @@ int launch_pair_t(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s)
     const long long rows = static_cast<long long>(a.B) * H * tiles_w;
     // rows per wave (each A row is computed once and reused by KB output rows; the first KB-1 are
     // the wave's warm-up).  Swept on MI355X in the S-K launch sequence: the 192x624 agg_1 pair is
-    // fastest at 3 (31.1 us vs 35.9 at 4, 37.5 at 2), the 24x78 FMBlock pairs at 1 (10.4 vs 12.6 at 2)
-    const int rw = rows >= 6144 ? 3 : (rows >= 2048 ? 2 : 1);
+    // fastest at 3 (31.1 us vs 35.9 at 4, 37.5 at 2), the 24x78 FMBlock pairs at 1 (10.4 vs 12.6 at 2),
+    // and in the L sequence the 96x312 FMBlock pairs at 1 too (15.9 vs 18.8 us at 2)
+    const int rw = rows >= 6144 ? 3 : 1;
     const long long nwg = tiles_w * ((H + 4 * rw - 1) / (4 * rw)) * a.B;
     if (nwg > 0x7fffffffLL) return arg_error("conv pair: grid too large");
     hipLaunchKernelGGL((pair_kernel<KA, KB, MA, MB, NKA>), dim3(static_cast<unsigned>(nwg)), dim3(kPairThreads),
