@@ -26,18 +26,18 @@ constexpr int kPix = 4;                       // pixels per thread
 constexpr int kTile = kThreads * kPix;         // flat pixels per workgroup
 constexpr int kDChunk = 16;                    // disparity planes per workgroup
 
-template <int CPG, bool ATT, bool VEC>
+template <int CPG, bool ATT, bool VEC, int DCH = kDChunk>
 __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__ L, const float* __restrict__ R,
                                                        const float* __restrict__ att, float* __restrict__ V, int G,
                                                        int H, int W, int D) {
-    __shared__ float rs[CPG][kTile + kDChunk];
+    __shared__ float rs[CPG][kTile + DCH];
     const int HW = H * W;
     const int bg = blockIdx.y;  // b*G + g
     const int b = bg / G;
     const int g = bg - b * G;
     const int p0 = blockIdx.x * kTile;
-    const int d0 = blockIdx.z * kDChunk;
-    const int dn = min(kDChunk, D - d0);
+    const int d0 = blockIdx.z * DCH;
+    const int dn = min(DCH, D - d0);
     const int C = G * CPG;
     const float* lb = L + (static_cast<long long>(b) * C + g * CPG) * HW;
     const float* rb = R + (static_cast<long long>(b) * C + g * CPG) * HW;
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__
     const int span = kTile + dn - 1;
     // every load of the thread (right segment, left pixels, att) issued as one batch with clamped
     // addresses, then selected and stored: one memory round trip per workgroup
-    constexpr int NR = (kTile + kDChunk - 1 + kThreads - 1) / kThreads;
+    constexpr int NR = (kTile + DCH - 1 + kThreads - 1) / kThreads;
     float rr[CPG][NR];
 #pragma unroll
     for (int c = 0; c < CPG; ++c)
@@ -282,16 +282,21 @@ int launch_gwc(const float* L, const float* R, const float* att, float* V, int B
     if (C % G) return arg_error("gwc: C must be divisible by num_groups");
     const int cpg = C / G;
     const int HW = H * W;
-    dim3 grid(ceil_div(HW, kTile), B * G, ceil_div(D, kDChunk));
+    // small volumes (the S variant at 1/16 resolution: 2 pixel tiles x 32 groups) get 4-plane
+    // disparity chunks, i.e. 4x the workgroups; the values are the same (per-voxel arithmetic)
+    const bool small = static_cast<long long>(ceil_div(HW, kTile)) * B * G * ceil_div(D, kDChunk) < 512;
+    const int dch = small ? 4 : kDChunk;
+    dim3 grid(ceil_div(HW, kTile), B * G, ceil_div(D, dch));
     const bool vec = (HW % 4) == 0;
+#define ESM_GWC_L(CP, AT, VC)                                                                                      \
+    if (small) hipLaunchKernelGGL((gwc_kernel<CP, AT, VC, 4>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D); \
+    else hipLaunchKernelGGL((gwc_kernel<CP, AT, VC>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D);
 #define ESM_GWC(CP)                                                                                          \
     if (cpg == CP) {                                                                                         \
         if (att) {                                                                                           \
-            if (vec) hipLaunchKernelGGL((gwc_kernel<CP, true, true>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D); \
-            else hipLaunchKernelGGL((gwc_kernel<CP, true, false>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D); \
+            if (vec) { ESM_GWC_L(CP, true, true) } else { ESM_GWC_L(CP, true, false) }                      \
         } else {                                                                                             \
-            if (vec) hipLaunchKernelGGL((gwc_kernel<CP, false, true>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D); \
-            else hipLaunchKernelGGL((gwc_kernel<CP, false, false>), grid, dim3(kThreads), 0, s, L, R, att, V, G, H, W, D); \
+            if (vec) { ESM_GWC_L(CP, false, true) } else { ESM_GWC_L(CP, false, false) }                     \
         }                                                                                                    \
         return check_launch("gwc");                                                                          \
     }
@@ -300,6 +305,7 @@ int launch_gwc(const float* L, const float* R, const float* att, float* V, int B
     ESM_GWC(4)
     ESM_GWC(8)
 #undef ESM_GWC
+#undef ESM_GWC_L
     set_error("gwc: channels per group must be 1, 2, 4 or 8");
     return ESM_ERR_UNSUPPORTED;
 }
