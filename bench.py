@@ -137,29 +137,69 @@ def find_dominant(hp: E.HotPath, reps: int = 3) -> tuple:
     return dom, times
 
 
-def cost_volume_roofline(device, reps: int = 20) -> dict:
-    """gwc kernel alone at ESMStereo-L KITTI full res (B=1, C=64, 96x312, D=48, G=32)."""
-    B, C, H, W, D, G = 1, 64, 96, 312, 48, 32
-    L = torch.randn(B, C, H, W, device=device)
-    R = torch.randn(B, C, H, W, device=device)
-    V = torch.empty(B, G, D, H, W, device=device)
+INFINITY_CACHE_BYTES = 256 << 20  # MI355X die-level L3 (MI355X_MICROARCH.md)
+
+
+def cost_volume_roofline(device, reps: int = 24, B: int = 1, H: int = 96, W: int = 312, D: int = 48) -> dict:
+    """gwc kernel alone at ESMStereo-L KITTI full res (B=1, C=64, 96x312, D=48, G=32), cache-proof:
+    every launch writes the next buffer of a ring of output volumes (and reads the next of a ring of
+    feature pairs) whose total exceeds the 256 MiB Infinity Cache, so no launch finds its output
+    lines or its inputs resident from the previous one.  Timed as ``reps`` back-to-back launches
+    between one hipEvent pair (per-launch event pairs add their own overhead)."""
+    C, G = 64, 32
+    vol = 4 * B * G * D * H * W
+    feat = 4 * B * 2 * C * H * W
+    nbuf = max(2, -(-(2 * INFINITY_CACHE_BYTES) // (vol + feat)))  # footprint >= 2x the Infinity Cache
+    Ls = [torch.randn(B, C, H, W, device=device) for _ in range(nbuf)]
+    Rs = [torch.randn(B, C, H, W, device=device) for _ in range(nbuf)]
+    Vs = [torch.empty(B, G, D, H, W, device=device) for _ in range(nbuf)]
     ctx = E.engine.Ctx(device)
-    for _ in range(3):
-        ctx.gwc(L, R, None, V, B, C, H, W, D, G)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in evs:
-        a.record()
-        ctx.gwc(L, R, None, V, B, C, H, W, D, G)
-        b.record()
+    for i in range(nbuf):
+        ctx.gwc(Ls[i], Rs[i], None, Vs[i], B, C, H, W, D, G)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for r in range(reps):
+        i = r % nbuf
+        ctx.gwc(Ls[i], Rs[i], None, Vs[i], B, C, H, W, D, G)
+    ev1.record()
     torch.cuda.synchronize()
-    ms = sorted(a.elapsed_time(b) for a, b in evs)
-    avg = sum(ms) / len(ms)
+    avg = ev0.elapsed_time(ev1) / reps
     byts = 4 * B * (2 * C * H * W + G * D * H * W)
     ach = byts / (avg * 1e-3) / 1e9
-    return {"kernel": "gwc_volume", "config": "ESMStereo-L KITTI 384x1248 md192: B=1 C=64 96x312 D=48 G=32",
+    out = {"kernel": "gwc_volume", "config": f"ESMStereo-L B={B} C=64 {H}x{W} D={D} G=32",
+           "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2),
+           "ring_buffers": nbuf, "footprint_bytes": nbuf * (vol + feat), "timing": f"{reps} launches, one event pair",
+           "traffic": pmc_traffic("gwc_volume", f"gwc ring B{B} {H}x{W} D{D}")}
+    del Ls, Rs, Vs
+    torch.cuda.empty_cache()
+    return out
+
+
+def concat_volume_roofline(device, reps: int = 6, B: int = 8, H: int = 136, W: int = 240, D: int = 48) -> dict:
+    """build_concat_volume (submodule.py:129-140) at BASELINE configs[2]'s size: [8, 128, 48, 136, 240]
+    = 6.4 GB written per launch, two output buffers alternating (12.8 GB, far past the Infinity Cache)."""
+    C = 64
+    L = torch.randn(B, C, H, W, device=device)
+    R = torch.randn(B, C, H, W, device=device)
+    Vs = [torch.empty(B, 2 * C, D, H, W, device=device) for _ in range(2)]
+    ctx = E.engine.Ctx(device)
+    for V in Vs:
+        ctx.concat(L, R, V, B, C, H, W, D)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for r in range(reps):
+        ctx.concat(L, R, Vs[r % 2], B, C, H, W, D)
+    ev1.record()
+    torch.cuda.synchronize()
+    avg = ev0.elapsed_time(ev1) / reps
+    byts = 4 * B * (2 * C * H * W + 2 * C * D * H * W)
+    ach = byts / (avg * 1e-3) / 1e9
+    del Vs
+    torch.cuda.empty_cache()
+    return {"kernel": "concat_volume", "config": f"ESMStereo-L B={B} C=64 {H}x{W} D={D} (BASELINE configs[2])",
             "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2),
-            "min_us": round(ms[0] * 1e3, 2)}
+            "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2)}
 
 
 def concurrent_streams(model, ml, mr, att, up, n: int, steps: int, warmup: int, device) -> dict:
@@ -196,27 +236,110 @@ def concurrent_streams(model, ml, mr, att, up, n: int, steps: int, warmup: int, 
             "ms_per_round": round(el / steps * 1e3, 4), "outputs_identical": bool(same)}
 
 
+def host_cores() -> tuple:
+    """(cores this process may use, CPUs the host reports).  On the GPU box os.cpu_count() is the
+    whole machine while the job gets a share of it (its affinity mask and cgroup CPU quota): the
+    baseline runs one thread per core of that share."""
+    total = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n), total
+
+
 def cpu_baseline(model, ml, mr, att, up, args, budget_s: float) -> tuple:
+    """The oracle (PyTorch fp32 CPU restatement) on every core of the job's host share, one pair
+    (the first of the batch) per forward; value = 1 / (min over >= 3 forwards) pairs/s."""
     from oracle import esm_oracle as O
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, host_total = host_cores()
     torch.set_num_threads(threads)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    ins = (ml.cpu(), mr.cpu(), None if att is None else att.cpu(), [u.cpu() for u in up])
-    backbone, cvs = VARIANTS[args.variant]
-    reps, t0, out = 0, time.perf_counter(), None
+    one = lambda t: None if t is None else t[:1].cpu()  # noqa: E731
+    ins = (one(ml), one(mr), one(att), [one(u) for u in up])
+    _, cvs = VARIANTS[args.variant]
+    times, t0, out = [], time.perf_counter(), None
     with torch.no_grad():
-        while True:
+        while len(times) < 3 or (time.perf_counter() - t0 < budget_s and len(times) < 50):
+            t1 = time.perf_counter()
             out = O.hot_path(sd, cvs, args.maxdisp, args.cv == "gwc", *ins)
-            reps += 1
-            if time.perf_counter() - t0 >= budget_s and reps >= 2:
-                break
+            times.append(time.perf_counter() - t1)
     el = time.perf_counter() - t0
-    B = ml.shape[0]
-    return ({"value": round(B * reps / el, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
-             "sample": f"{reps} hot-path forwards of the same {B}x{args.height}x{args.width} md{args.maxdisp} "
-                       f"ESMStereo-{args.variant} {args.cv} input, oracle/esm_oracle.py (PyTorch fp32 CPU), "
-                       f"{el:.1f} s"}, out["disp_0"])
+    best = min(times)
+    return ({"value": round(1.0 / best, 3), "unit": "pairs/s", "cores": threads, "host_cpus": host_total,
+             "kind": "port", "timing": f"min of {len(times)} forwards (mean {sum(times) / len(times) * 1e3:.1f} ms)",
+             "sample": f"{len(times)} hot-path forwards of one {args.height}x{args.width} md{args.maxdisp} "
+                       f"ESMStereo-{args.variant} {args.cv} pair, oracle/esm_oracle.py (PyTorch fp32 CPU, "
+                       f"{threads} threads = the job's CPU share of {host_total} host CPUs), {el:.1f} s"},
+            out["disp_0"])
+
+
+# BASELINE.json configs (configs[0] is the reference's CPU plumbing case: tests/test_gpu_parity.py
+# test_expected_raises pins its error).  Default: configs[1], the headline metric.
+CONFIGS = {
+    1: dict(variant="S", cv="gwc", height=384, width=1248, maxdisp=192, batch=1, scaling="weak",
+            name="ESMStereo-S KITTI 384x1248 maxdisp=192 batch=1 per GPU"),
+    2: dict(variant="L", cv="gwc", height=544, width=960, maxdisp=192, batch=8, scaling="weak",
+            name="ESMStereo-L SceneFlow 540x960 (padded to 544x960) maxdisp=192 batch=8 per GPU"),
+    3: dict(variant="L", cv="gwc", height=384, width=1248, maxdisp=192, global_batch=32, scaling="strong",
+            name="ESMStereo-L KITTI 384x1248 maxdisp=192, global batch 32 split over the GPUs"),
+    4: dict(variant="L", cv="gwc", height=1024, width=1504, maxdisp=256, batch=1, scaling="weak",
+            name="Middlebury ~1500x1000 (padded to 1504x1024) maxdisp=256 batch=1 per GPU"),
+}
+WEIGHT_SEED = {("S", "gwc"): 11, ("S", "nc"): 12, ("M", "gwc"): 13, ("M", "nc"): 14, ("L", "gwc"): 15, ("L", "nc"): 16}
+
+
+def load_seeded_weights(model: torch.nn.Module, variant: str, cv: str) -> None:
+    """The hot path's weights from the seeded generator the reference fixtures were made with
+    (tests/helpers.py seeded_state over the reference's state-dict spec): random-init weights of the
+    architecture, and the same network the full-size reference fixture ran, so the benchmark can
+    report its EPE against the reference.  The backbone keeps its own random init."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import load_spec, seeded_state
+
+    sd = seeded_state(load_spec(f"spec_{variant}_{cv}.json"), WEIGHT_SEED[(variant, cv)])
+    missing, unexpected = model.load_state_dict({k: v for k, v in sd.items() if not k.startswith("feature.")},
+                                                strict=False)
+    assert not unexpected and all(k.startswith("feature.") for k in missing), (missing, unexpected)
+
+
+def epe_vs_reference(model, args, dev):
+    """The plan on the seeded inputs of the reference's full-size fixture for this configuration
+    (tests/golden/full_*.npz, made by running the reference itself), EPE of disp_0 at every 4th row and
+    column; ESMStereo-L flip-masked (tests/parity.py).  None when no fixture matches."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import check_fullsize, fullsize_case, fullsize_manifest
+
+    for name, m in sorted(fullsize_manifest().items()):
+        if (m["variant"], m["cv"], m["H"], m["W"], m["maxdisp"]) == (args.variant, args.cv, args.height, args.width,
+                                                                      args.maxdisp):
+            break
+    else:
+        return None
+    m, g, (ml, mr, att, up) = fullsize_case(name)
+    T = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
+    ml, mr, att, up = T(ml), T(mr), T(att), [T(u) for u in up]
+    D = m["maxdisp"] // m["cv_scale"]
+    with torch.no_grad():
+        V = E.build_gwc_volume(ml, mr, D, 32, att=att) if args.cv == "gwc" else E.build_norm_correlation_volume(ml, mr, D)
+        if args.cv == "gwc":
+            vol = model.group_stem(V)
+        else:
+            vol = model.corr_stem.emit(E.engine.Ctx(dev), [V], mul=None if att is None else att)
+        cost = model.aggregation_out(model.agg(vol))[:, 0]
+        init = E.regression_topk(cost, None, 2) if m["cv_scale"] == 4 else \
+            E.disparity_regression(cost, D).unsqueeze(1)
+        disp0 = model.hot_path(ml, mr, att, up)[0]
+    rep = check_fullsize(name, m, g, cost, init, disp0)
+    d = rep.get("disp0")
+    epe = d["epe_outside_mask"] if d else rep["disp0_sub_epe"]
+    return {"epe_px": epe, "fixture": "tests/golden/" + name, "pixels": "every 4th row and column of disp_0",
+            "top2_flips": None if d is None else d["flips"], "cost_rel": max(rep["cost_sample_rel"], rep["cost_l2_rel"])}
 
 
 def main() -> None:
@@ -224,21 +347,32 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--variant", default="S", choices=sorted(VARIANTS))
-    ap.add_argument("--cv", default="gwc", choices=["gwc", "nc"])
-    ap.add_argument("--batch", type=int, default=1, help="pairs per GPU per step")
-    ap.add_argument("--height", type=int, default=384)
-    ap.add_argument("--width", type=int, default=1248)
-    ap.add_argument("--maxdisp", type=int, default=192)
+    ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i] preset (default 1, the headline); the flags below override it")
+    ap.add_argument("--variant", default=None, choices=sorted(VARIANTS))
+    ap.add_argument("--cv", default=None, choices=["gwc", "nc"])
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None, help="pairs per step over all GPUs (strong scaling)")
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--maxdisp", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the cost-volume roofline side measurement")
+    ap.add_argument("--no-extra", action="store_true", help="skip the side measurements (cost-volume rooflines, "
+                    "concurrent streams, EPE vs the reference fixture)")
     ap.add_argument("--kernel-table", default="", help="write the per-op probe table (json) here")
     ap.add_argument("--streams", type=int, default=2,
                     help="side measurement: independent B-pair instances on this many concurrent streams")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("variant", "cv", "height", "width", "maxdisp"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
+    if args.global_batch is None and args.batch is None:
+        args.global_batch = cfg.get("global_batch")
+        args.batch = cfg.get("batch")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -247,10 +381,21 @@ def main() -> None:
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.global_batch is not None:  # strong scaling: the global batch is split over the ranks
+        from esmstereo_amd.dist import shard_range
+
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} must split evenly over {world} GPUs")
+        lo, hi = shard_range(args.global_batch, world, rank)
+        args.batch = hi - lo
+        scaling = "strong"
+    else:
+        scaling = "weak"
 
     backbone, cvs = VARIANTS[args.variant]
     model = E.ESMStereo(args.maxdisp, args.cv == "gwc", args.cv == "nc", backbone, cvs)
     seeded_init(model, 1234)
+    load_seeded_weights(model, args.variant, args.cv)
     model = model.eval().to(dev)
     left, right = synthetic_pair(args.batch, args.height, args.width, args.maxdisp, 100 + rank, dev)
     with torch.no_grad():
@@ -330,7 +475,7 @@ def main() -> None:
                      "avg_us_event_pair_per_launch": round(pair_kms * 1e3, 2),
                      "algorithmic_flops_per_launch": meta[dom]["flops"],
                      "algorithmic_bytes_per_launch": meta[dom]["bytes"]})
-        total = args.batch * world * args.steps
+        total = args.batch * world * args.steps  # every rank holds the same batch (even split)
         line = {
             "metric": METRIC,
             "value": round(total / elapsed, 2),
@@ -340,12 +485,14 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (sinusoid-texture stereo pair, planar disparity; random-init weights)",
+            "data": "synthetic (sinusoid-texture stereo pair, planar disparity; seeded random-init weights, "
+                    "tests/helpers.py seeded_state)",
             "config": {"workload": "hot path: cost volume -> 3D stems -> 3D hourglass -> regression -> "
                                    "ESM upsampler (models/ESMStereo.py:700-745), " + workload,
+                       "baseline_config": f"configs[{args.config}]: {cfg['name']}",
                        "variant": args.variant, "cv": args.cv, "global_batch": args.batch * world,
                        "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                        "parallelism": f"dp{world}", "graph": hp.graph,
@@ -353,14 +500,18 @@ def main() -> None:
             "roofline": roof,
         }
         if not args.no_extra:
+            line["epe_vs_reference"] = epe_vs_reference(model, args, dev)
             line["roofline_cost_volume"] = cost_volume_roofline(dev)
+            # BASELINE configs[2]'s volumes: gwc and build_concat_volume at L-SF B=8 (1.74 / 6.4 GB per launch)
+            line["roofline_cost_volume_configs2"] = cost_volume_roofline(dev, reps=8, B=8, H=136, W=240, D=48)
+            line["roofline_concat_volume_configs2"] = concat_volume_roofline(dev)
             if world == 1 and args.streams > 1:
                 line["concurrent"] = concurrent_streams(model, ml, mr, att, up, args.streams, args.steps, args.warmup,
                                                         dev)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref = cpu_baseline(model, ml, mr, att, up, args, args.cpu_seconds)
             line["cpu_baseline"] = cb
-            got = hp.outputs[0].detach().cpu()
+            got = hp.outputs[0][:1].detach().cpu()  # the oracle ran the batch's first pair
             line["epe_vs_oracle"] = float((got - ref).abs().mean())
         else:
             line["cpu_baseline"] = None

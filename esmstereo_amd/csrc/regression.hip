@@ -37,6 +37,10 @@ __global__ void __launch_bounds__(kThreads) dispreg_kernel(const float* __restri
     out[i] = acc;
 }
 
+// Order of torch.sort(descending=True): NaN ranks above every number; on equal keys the lower
+// index stays first (the scan visits d in increasing order and only a strictly earlier key moves).
+__device__ __forceinline__ bool desc_before(float v, float w) { return (v != v && w == w) || v > w; }
+
 __global__ void __launch_bounds__(kThreads) topk2_kernel(const float* __restrict__ cost,
                                                          const float* __restrict__ samples, float* __restrict__ out,
                                                          int D, int HW, int npix) {
@@ -58,10 +62,10 @@ __global__ void __launch_bounds__(kThreads) topk2_kernel(const float* __restrict
             if (d0 + k >= D) break;
             const float v = vs[k];
             const int d = d0 + k;
-            if (!have0 || v > v0) {
+            if (!have0 || desc_before(v, v0)) {
                 if (have0) { v1 = v0; i1 = i0; have1 = true; }
                 v0 = v; i0 = d; have0 = true;
-            } else if (!have1 || v > v1) {
+            } else if (!have1 || desc_before(v, v1)) {
                 v1 = v; i1 = d; have1 = true;
             }
         }

@@ -62,6 +62,9 @@ def sharded_forward(model, left: torch.Tensor, right: torch.Tensor, group=None) 
     slice through ``model`` and receives the full ``[B, H, W]`` disparity batch."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     lo, hi = shard_range(int(left.shape[0]), world, rank)
-    with torch.no_grad():
-        disp = model(left[lo:hi], right[lo:hi], False)[0]
+    if hi == lo:  # fewer pairs than ranks: nothing to run here, but every rank joins the gather
+        disp = left.new_empty((0,) + tuple(left.shape[-2:]))
+    else:
+        with torch.no_grad():
+            disp = model(left[lo:hi], right[lo:hi], False)[0]
     return gather_disparities(disp, int(left.shape[0]), group)

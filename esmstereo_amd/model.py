@@ -3,8 +3,13 @@
 Same constructor ``ESMStereo(maxdisp, gwc=False, norm_correlation=True,
 backbone="efficientnet_b2", cv_scale=4)``, same ``forward(left, right, train_status)``
 returning ``[disp]`` in eval (``[disp_1, disp_2(, disp_4)]`` with ``train_status``), same
-state-dict keys for every hot-path module, so ``test_kitti.py`` / ``save_disp.py`` run
-unchanged with ``from esmstereo_amd import __models__``.
+state-dict keys for every module (the backbone with timm's key layout, ``backbone.Feature``),
+so ``test_kitti.py`` / ``save_disp.py`` run unchanged with ``from esmstereo_amd import
+__models__`` and load a reference checkpoint.  The backbone starts from random weights (the
+reference's ``pretrained=True`` ImageNet weights are not fetchable offline): loading a state
+dict that leaves every ``feature.*`` tensor untouched (e.g. through the callers' key filter,
+``test_kitti.py:57-61``, with a checkpoint of another layout) warns that the backbone stays
+random.
 
 Split of the forward:
 
@@ -20,6 +25,7 @@ from __future__ import annotations
 import collections
 import math
 import os
+import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -27,13 +33,11 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import check, lib
-from .backbone import StubFeature
+from .backbone import Feature
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
-from .engine import Ctx, GWC_STEM_ENABLED, gwc_stem_supported, require_device, run_gwc_stem
+from .engine import Ctx, GWC_STEM_ENABLED, gwc_stem_supported, param_token, require_device, run_gwc_stem
 
-__all__ = ["ESMStereo", "FeatUp", "HotPath"]
-
-Feature = StubFeature  # placeholder backbone with the reference interface (see backbone.py)
+__all__ = ["ESMStereo", "ESMStereo_trt", "FeatUp", "HotPath"]
 
 
 class FeatUp(nn.Module):
@@ -152,6 +156,11 @@ class HotPath:
             dst.copy_(src)
 
     def close(self) -> None:
+        # the plan's buffers came from torch's caching allocator on the stream current at build
+        # time, but replays may run on other streams (launch(stream)): drain the device before
+        # the memory can be handed out again
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         self.ctx.close()
 
 
@@ -159,7 +168,9 @@ class ESMStereo(nn.Module):
     """ESMStereo stereo network with the HIP hot path (reference models/ESMStereo.py:511-745)."""
 
     def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
-                 backbone: str = "efficientnet_b2", cv_scale: int = 4) -> None:
+                 backbone: str = "efficientnet_b2", cv_scale: int = 4, *, feature_cls=None) -> None:
+        """Reference positional signature (ESMStereo.py:512).  ``feature_cls`` (keyword only)
+        replaces the backbone class; the golden-vector tests pass ``backbone.StubFeature``."""
         super().__init__()
         self.maxdisp = maxdisp
         self.vol_size = cv_scale
@@ -168,7 +179,7 @@ class ESMStereo(nn.Module):
         self.backbone = backbone
         if cv_scale not in _STEMS:
             raise ValueError("Choose the cost volume resolution: 4, 8, 16")
-        self.feature = Feature(self.backbone)
+        self.feature = (feature_cls or Feature)(self.backbone)
         if cv_scale in (4, 8):
             self.feature_up = FeatUp(self.feature.chans, cv_scale)
         for name, cin, c in _STEMS[cv_scale]:
@@ -211,9 +222,26 @@ class ESMStereo(nn.Module):
         self.invalidate_plans()
         return super()._apply(fn, *args, **kwargs)
 
-    def _load_from_state_dict(self, *args, **kwargs):
+    def _hot_param_token(self) -> tuple:
+        """Identity (storage, in-place version) of every hot-path tensor: a weight edited in place
+        (``param.copy_``, BN statistics updated elsewhere) changes it, so the plan cache never
+        replays stale packed weights."""
+        mods = [m for name in ("group_stem", "corr_stem", "agg", "aggregation_out", "upsample_module")
+                if getattr(self, name, None) is not None for m in getattr(self, name).modules()]
+        return param_token(*mods)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self.invalidate_plans()
-        return super()._load_from_state_dict(*args, **kwargs)
+        feat = {k: v for k, v in self.feature.state_dict().items() if k.endswith("weight")}
+        got = {k: state_dict.get(prefix + "feature." + k) for k in feat}
+        others = [k for k in state_dict if k.startswith(prefix) and not k.startswith(prefix + "feature.")]
+        untouched = all(v is None or (v.shape == feat[k].shape and torch.equal(v.to(feat[k].device), feat[k]))
+                        for k, v in got.items())
+        if feat and others and untouched:
+            warnings.warn("ESMStereo.load_state_dict: no feature.* (backbone) weight changed; the backbone keeps "
+                          "its random initialisation (checkpoint of another backbone layout?)", RuntimeWarning,
+                          stacklevel=3)
+        return super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     # ------------------------------------------------------------------ forward pieces
     def prefix(self, left: torch.Tensor, right: torch.Tensor):
@@ -286,7 +314,7 @@ class ESMStereo(nn.Module):
         for t in [ml, mr, *up] + ([att] if att is not None else []):
             require_device(t, "hot-path input")
         key = (tuple(ml.shape), None if att is None else tuple(att.shape), tuple(tuple(u.shape) for u in up),
-               bool(train_status), ml.device)
+               bool(train_status), ml.device, self._hot_param_token())
         hp = self._plans.get(key)
         if hp is None:
             hp = HotPath(self, int(ml.shape[0]), int(ml.shape[2]), int(ml.shape[3]),
@@ -310,3 +338,14 @@ class ESMStereo(nn.Module):
         with torch.no_grad():
             ml, mr, att, up = self.prefix(left, right)
             return self.hot_path(ml, mr, att, up, train_status)
+
+
+class ESMStereo_trt(ESMStereo):
+    """The export / deployment signature (reference ``models/ESMStereo_trt.py:511-737``, exported by
+    ``onnx_transformed.py:48-51`` with inputs ``left``, ``right`` and output ``disp``): the same
+    module tree and state dict as :class:`ESMStereo`, and ``forward(left, right) -> disp [B, H, W]``,
+    the eval output of ``ESMStereo.forward`` (``ESMStereo_trt.py:638,735``), over the same compiled
+    HIP plan."""
+
+    def forward(self, left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
+        return super().forward(left, right, False)[0]

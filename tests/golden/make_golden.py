@@ -2,7 +2,8 @@
 
 Run in the build container only (it imports the reference from /root/reference):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py               # fixture-size vectors (rewrites the manifest)
+    python tests/golden/make_golden.py --fullsize    # + full-size summaries (BASELINE KITTI size)
 
 What it does (SURVEY.md §8(c) recipe):
 * imports ``models/submodule.py``, ``models/shufflemixer.py`` and ``models/ESMStereo.py``
@@ -151,8 +152,64 @@ def hot_path(sm, model, ml, mr, att, up):
     return inter
 
 
+# Full-size configurations pinned to the reference itself: the hot path of
+# ESMStereo.forward (:700-745) on seeded feature inputs (tests/helpers.py fullsize_inputs) at the
+# BASELINE KITTI size.  Summaries only (the volumes are 3-184 MB): cost sum / L2 / 64 sampled
+# voxels, per-pixel top-3 of the aggregated cost (the regression_topk flip analysis), init_pred
+# in full, disp_0 sum / L2 and every 4th row and column.
+FULL_CASES = [
+    # (tag, variant, cv, B, H, W, maxdisp, weight seed, input seed)
+    ("S_gwc_K", "S", "gwc", 1, 384, 1248, 192, 11, 101),
+    ("L_gwc_K", "L", "gwc", 1, 384, 1248, 192, 15, 102),
+    ("L_nc_K", "L", "nc", 1, 384, 1248, 192, 16, 103),
+]
+
+
+def make_fullsize(sm, es):
+    from helpers import digest, fullsize_inputs
+
+    man = {}
+    for tag, var, cv, B, H, W, maxdisp, wseed, iseed in FULL_CASES:
+        backbone, cv_scale = VARIANTS[var]
+        model = es.ESMStereo(maxdisp, cv == "gwc", cv == "nc", backbone, cv_scale).eval()
+        spec = module_spec(model)
+        model.load_state_dict(seeded_state(spec, wseed))
+        ml, mr, att, up = fullsize_inputs(cv_scale, B, H, W, maxdisp, iseed, att=cv_scale == 16)
+        T = lambda a: None if a is None else torch.from_numpy(a)  # noqa: E731
+        with torch.no_grad():
+            inter = hot_path(sm, model, T(ml), T(mr), T(att), [T(u) for u in up])
+        cost = inter["cost"][:, 0]  # [B, D, h, w]
+        flat = cost.reshape(-1)
+        rng = np.random.default_rng(iseed + 1000)
+        idx = np.sort(rng.choice(flat.numel(), 64, replace=False)).astype(np.int64)
+        sv, si = torch.sort(cost.double(), dim=1, descending=True, stable=True)
+        d0 = inter["disp_0"]
+        arrays = dict(
+            cost_sum=np.float64(cost.double().sum()), cost_l2=np.float64(cost.double().norm()),
+            cost_absmax=np.float64(cost.abs().max()), cost_idx=idx, cost_val=flat[idx].numpy(),
+            top3_idx=si[:, :3].numpy().astype(np.int16), top3_val=sv[:, :3].numpy(),
+            init_pred=inter["init_pred"].numpy(),
+            disp0_sum=np.float64(d0.double().sum()), disp0_l2=np.float64(d0.double().norm()),
+            disp0_sub=d0[:, ::4, ::4].numpy())
+        np.savez_compressed(os.path.join(HERE, f"full_{tag}.npz"), **arrays)
+        man[f"full_{tag}.npz"] = dict(variant=var, cv=cv, backbone=backbone, cv_scale=cv_scale, B=B, H=H, W=W,
+                                      maxdisp=maxdisp, weight_seed=wseed, input_seed=iseed,
+                                      spec=f"spec_{var}_{cv}.json", input_sha256=digest(ml, mr, att, *up),
+                                      disp0_shape=list(d0.shape))
+        print(tag, {k: getattr(v, "shape", ()) for k, v in arrays.items()})
+    return man
+
+
 def main():
     torch.set_num_threads(8)
+    if "--fullsize" in sys.argv:  # add the full-size fixtures to an existing manifest
+        sm, es = load_reference()
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        manifest.update(make_fullsize(sm, es))
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1)
+        return
     sm, es = load_reference()
     manifest = {}
     for (var, cv, B, H, W, maxdisp, seed) in CASES:

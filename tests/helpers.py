@@ -147,3 +147,54 @@ def feature_pair(B: int, C: int, h: int, w: int, seed: int, D: int) -> Tuple[tor
         right[:, :, y, :] = full[:, :, y, D - d: D - d + w]
     right += 0.1 * rng.standard_normal(right.shape).astype(np.float32)
     return torch.from_numpy(left), torch.from_numpy(right)
+
+
+# ----------------------------------------------------------------------------- full-size fixtures
+# Hot-path inputs at a BASELINE configuration, generated from a seed with numpy only (PCG64
+# normals, then fixed-order float64 additions), so the GPU box regenerates them bit for bit (each
+# fixture stores the SHA-256 of the bytes it was made from).  SURVEY.md §8(d) input: a smooth
+# texture for the matching features with the right view shifted by a planar disparity field, so
+# the cost volume is peaked; the upsampler features are smooth random maps.
+
+# (channels, stride) of the upsampler feature inputs per cv_scale (models/ESMStereo.py:722,726,733)
+UP_LAYOUT = {4: [(96, 8), (48, 4), (32, 2)], 8: [(240, 16), (96, 8), (24, 4), (32, 2)],
+             16: [(32, 8), (32, 16), (24, 4), (24, 2)]}
+
+
+def smooth_field(rng: np.random.Generator, shape: Sequence[int], k: int = 2) -> np.ndarray:
+    """Normals box-blurred over the last two axes ((2k+1)^2 window), unit-ish scale, float32."""
+    *lead, h, w = shape
+    a = rng.standard_normal(tuple(lead) + (h + 2 * k, w + 2 * k))
+    acc = np.zeros(tuple(lead) + (h + 2 * k, w), dtype=np.float64)
+    for i in range(2 * k + 1):
+        acc += a[..., i:i + w]
+    out = np.zeros(tuple(lead) + (h, w), dtype=np.float64)
+    for i in range(2 * k + 1):
+        out += acc[..., i:i + h, :]
+    return (out / (2 * k + 1)).astype(np.float32)
+
+
+def fullsize_inputs(cv_scale: int, B: int, H: int, W: int, maxdisp: int, seed: int, att: bool):
+    """(match_left, match_right, att or None, [upsampler features]) as float32 numpy arrays."""
+    rng = np.random.default_rng(seed)
+    h, w = H // cv_scale, W // cv_scale
+    D = maxdisp // cv_scale
+    tex = smooth_field(rng, (B, 64, h, w + D))
+    ml = np.ascontiguousarray(tex[..., D:])
+    mr = np.empty_like(ml)
+    for y in range(h):  # right[x] = left texture at x - d(y), d planar in y within [0.1, 0.8] D
+        d = int((0.1 + 0.7 * y / max(1, h - 1)) * D)
+        mr[:, :, y, :] = tex[:, :, y, D - d: D - d + w]
+    mr += (0.05 * rng.standard_normal(mr.shape)).astype(np.float32)
+    a = (0.5 + rng.random((B, 32, h, w))).astype(np.float32) if att else None
+    up = [smooth_field(rng, (B, c, H // s, W // s), 1) for c, s in UP_LAYOUT[cv_scale]]
+    return ml, mr, a, up
+
+
+def digest(*arrays) -> str:
+    import hashlib
+    hs = hashlib.sha256()
+    for x in arrays:
+        if x is not None:
+            hs.update(np.ascontiguousarray(x).tobytes())
+    return hs.hexdigest()

@@ -20,6 +20,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
 import esmstereo_amd as E  # noqa: E402
+from esmstereo_amd.backbone import StubFeature  # noqa: E402
 from helpers import load_spec, seeded_state  # noqa: E402
 from oracle import esm_oracle as O  # noqa: E402
 
@@ -42,7 +43,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda")
     bb, cvs = VARIANTS[args.variant]
-    model = E.ESMStereo(args.maxdisp, args.cv == "gwc", args.cv == "nc", bb, cvs)
+    model = E.ESMStereo(args.maxdisp, args.cv == "gwc", args.cv == "nc", bb, cvs, feature_cls=StubFeature)
     sd = seeded_state(load_spec(f"spec_{args.variant}_{args.cv}.json"), args.seed)
     model.load_state_dict(sd)
     model.eval().to(dev)

@@ -15,6 +15,7 @@ from helpers import GOLDEN_DIR, load_spec, module_spec
 
 import esmstereo_amd
 from esmstereo_amd import _lib
+from esmstereo_amd.backbone import StubFeature
 from esmstereo_amd.engine import pack_conv, pack_weight
 
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "esmstereo_amd.h")
@@ -123,7 +124,8 @@ def test_state_dict_matches_reference(var, cv):
     with open(os.path.join(GOLDEN_DIR, "manifest.json")) as f:
         man = json.load(f)
     m = man[f"hot_{var}_{cv}.npz"]
-    model = esmstereo_amd.ESMStereo(m["maxdisp"], cv == "gwc", cv == "nc", m["backbone"], m["cv_scale"])
+    model = esmstereo_amd.ESMStereo(m["maxdisp"], cv == "gwc", cv == "nc", m["backbone"], m["cv_scale"],
+                                    feature_cls=StubFeature)
     assert module_spec(model) == [tuple(e) for e in load_spec(m["spec"])]
 
 
@@ -144,3 +146,16 @@ def test_training_mode_is_refused():
 
 def test_models_registry():
     assert esmstereo_amd.__models__["ESMStereo"] is esmstereo_amd.ESMStereo
+    assert esmstereo_amd.__models__["ESMStereo_trt"] is esmstereo_amd.ESMStereo_trt
+
+
+def test_trt_signature_and_state_dict():
+    """ESMStereo_trt (models/ESMStereo_trt.py:511-737): reference ctor, same state dict as ESMStereo,
+    forward(left, right) without train_status (onnx_transformed.py:48-51 calls it with two inputs)."""
+    import inspect
+    a = esmstereo_amd.ESMStereo(192, True, False, "efficientnet_b2", 4)
+    b = esmstereo_amd.__models__["ESMStereo_trt"](192, True, False, "efficientnet_b2", 4)
+    assert [(k, v.shape) for k, v in a.state_dict().items()] == [(k, v.shape) for k, v in b.state_dict().items()]
+    assert list(inspect.signature(b.forward).parameters) == ["left", "right"]
+    with pytest.raises(RuntimeError, match="ROCm"):
+        b.eval()(torch.randn(1, 3, 64, 128), torch.randn(1, 3, 64, 128))

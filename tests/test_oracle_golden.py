@@ -59,3 +59,23 @@ def test_expected_raises_recorded():
     assert r["S_oddD"].startswith("RuntimeError")
     assert r["L_oddD"].startswith("RuntimeError")
     assert r["S_hw_not_32"].startswith("RuntimeError")
+
+
+FULL = sorted(k for k in MANIFEST if k.startswith("full_"))
+
+
+@pytest.mark.parametrize("name", FULL)
+def test_oracle_fullsize_vs_reference(name):
+    """The oracle at BASELINE KITTI size (S-K gwc, L-K gwc, L-K nc) against the reference's own
+    summaries of the same seeded inputs (tests/golden/make_golden.py --fullsize): cost samples / sum
+    / L2 <= 1e-5 relative; disparities EPE <= 1e-3 (L: flip-masked, tests/parity.py)."""
+    from parity import check_fullsize, fullsize_case
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    m, g, (ml, mr, att, up) = fullsize_case(name)
+    sd = seeded_state(load_spec(m["spec"]), m["weight_seed"])
+    with torch.no_grad():
+        out = O.hot_path(sd, m["cv_scale"], m["maxdisp"], m["cv"] == "gwc", _t(ml), _t(mr),
+                         None if att is None else _t(att), [_t(u) for u in up])
+    rep = check_fullsize(name, m, g, out["cost"][:, 0], out["init_pred"], out["disp_0"])
+    print(name, rep)
