@@ -22,7 +22,8 @@ Printed (rank 0, one JSON line): the contract fields, plus
                 (the north_star headline: HBM fraction of the volume kernel);
   cpu_baseline  the CPU oracle (oracle/esm_oracle.py, PyTorch fp32 on the host cores) timed
                 on a bounded sample of the same workload, rank 0 at N = 1 only;
-  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input;
+  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input (and relative to
+                mean |disparity_oracle|: random-init weights give disparities of thousands of px);
   concurrent    (N = 1) serving-style side measurement: --streams independent hot-path instances
                 (own buffers and graphs, same batch per instance) replayed concurrently on as many
                 HIP streams.  `value` stays the single-stream rate.
@@ -513,6 +514,9 @@ def main() -> None:
             line["cpu_baseline"] = cb
             got = hp.outputs[0][:1].detach().cpu()  # the oracle ran the batch's first pair
             line["epe_vs_oracle"] = float((got - ref).abs().mean())
+            # the random-init weights give unnormalised disparity_regression outputs (the reference sums
+            # cost * d without a softmax, submodule.py:211-216): thousands of px, so also relative
+            line["epe_vs_oracle_rel"] = float((got - ref).abs().mean() / ref.abs().mean().clamp_min(1e-12))
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -13,12 +13,19 @@ int launch_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 int launch_gwc_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 bool c1in_ok(const esm_conv_desc& a);                    // conv_stem.hip
 int launch_c1in(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
+bool small_ok(const esm_conv_desc& a);                   // conv_small.hip
+bool small_auto(const esm_conv_desc& a);                 // conv_small.hip
+int launch_small(const esm_conv_desc& a, hipStream_t s);  // conv_small.hip
+bool wide_ok(const esm_conv_desc& a);                    // conv_wide.hip
+int launch_wide(const esm_conv_desc& a, hipStream_t s);  // conv_wide.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
 constexpr int kHintNoStem = 1 << 18;  // automatic choice among the other forms
 constexpr int kHintGwcStem = 1 << 19;  // input = the virtual gwc volume of src[0..2] (conv_stem.hip)
 constexpr int kHintC1in = 1 << 20;     // force the VALU single-input-channel form (conv_stem.hip)
+constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound layers (conv_small.hip)
+constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -51,6 +58,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
             return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
         if (a.Ho != 2 * a.Hi || a.Wo != 2 * a.Wi || (d3 && a.Do != 2 * a.Di))
             return arg_error("conv: transposed output extent must be 2x the input");
+        if ((a.hint & kHintSmall) || (a.hint == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
     }
     const int S = a.stride;
@@ -59,6 +67,8 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         (d3 && a.Do != (a.Di + 2 * a.pd - a.kd) / S + 1))
         return arg_error("conv: output extent inconsistent with kernel/stride/padding");
     if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
+    if (a.hint & kHintSmall) return conv::launch_small(a, s);
+    if (a.hint & kHintWide) return conv::launch_wide(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).
@@ -73,6 +83,8 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     }
     // 8 / 12 / 24 output channels, 3x3(x3) stride 1: the 16-block MFMA form wastes no tile rows
     if (a.hint == 0 && conv::stem_auto(a)) return conv::launch_stem(a, s);
+    // latency-bound layers (most of the hot path): the lean K-split form (conv_small.hip)
+    if (a.hint == 0 && conv::small_auto(a)) return conv::launch_small(a, s);
     return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
 }
 

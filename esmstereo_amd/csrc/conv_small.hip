@@ -1,0 +1,248 @@
+// Lean K-split convolution for the latency-bound layers of the hot path: the low-resolution
+// levels of the 3-D aggregation hourglass (models/ESMStereo.py:129-182, 1/32-1/64 of the input at
+// S-K: 2x3x10 .. 6x12x39 voxels) and the small 2-D maps of the ESM upsampler's first stage and its
+// refinement hourglass (:185-239, 242-509: 12x39 .. 48x156), i.e. BasicConv (models/submodule.py:
+// 12-38) where the whole layer is a few dozen output tiles.
+//
+// Why a third form: at these sizes one wave's lifetime is the kernel's duration, and in the general
+// forms it is dominated by instruction issue, not by memory or the matrix pipe: per-op PMC of the S-K
+// step (profiles/r02_pmc_sq_ops_SK.txt) shows ~700 VALU + ~700 SALU instructions per wave (runtime
+// tap decomposition, grid-index divisions, SGPR spills to VGPR lanes) around 9-54 MFMAs, 15k cycles
+// per wave, 43 % of them issuing.  Here everything a wave does is fixed at compile time except the
+// channel-group loop:
+//   * grid = (16-pixel column segment, sub-grid row, plane x batch x parity class x cout tile); the
+//     z split uses host-computed reciprocals (two s_mul_hi), no division sequence;
+//   * the K reduction is split over the 4 waves by 4-channel GROUP (wave w takes groups w, w+4, ..),
+//     so every wave walks the same compile-time tap list; a group's B operand is one buffer_load per
+//     tap: per-lane voffset = channel + column part (kOOB-marked outside, conv_direct.h), wave-uniform
+//     soffset = the tap's (plane, row) part (kOOB for a padding row), so borders cost no branches;
+//   * A (weights [cls][tap][cin_pad][cout_pad]): per-lane voffset fixed for the whole kernel, the
+//     tap / group part in soffset;
+//   * the 4 waves' partial tiles meet in LDS and are added in a fixed order (w0 + w1 + w2 + w3:
+//     deterministic); then every thread finishes one (cout, pixel) element: BN scale/shift,
+//     activation, optional residual, * post_scale (+ the second copy), one coalesced store.
+// Plain epilogues only (no `* mul`, bilinear add or PixelShuffle): the launcher falls back otherwise.
+#include "conv_direct.h"
+
+namespace esm {
+namespace conv {
+namespace {
+
+constexpr int kSmallThreads = 256;
+
+// floor(n / d) for n * d < 2^32 from the host-computed m = ceil(2^32 / d) (m = 0 encodes d = 1)
+__device__ __forceinline__ int fast_div(int n, unsigned m) {
+    return m ? static_cast<int>(__umulhi(static_cast<unsigned>(n), m)) : n;
+}
+
+inline unsigned magic_for(int d) {
+    return d <= 1 ? 0u : static_cast<unsigned>(((1ull << 32) + static_cast<unsigned long long>(d) - 1) / d);
+}
+
+template <bool D3, int K, int S, bool TR, int MT>
+__global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
+    constexpr int KT = TR ? 2 : K;  // taps per dim (per parity class when transposed)
+    constexpr int KDT = D3 ? KT : 1;
+    constexpr int TAPS = KDT * KT * KT;
+    constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
+    __shared__ __attribute__((aligned(16))) float red[4 * MT * 4 * 64];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n16 = lane & 15, kq = lane >> 4;
+
+    const int Ws = TR ? a.Wi : a.Wo;
+    const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
+    const int x0 = blockIdx.x * 16;
+    const int ys = blockIdx.y;
+    const int zz = blockIdx.z;
+    const int r1 = fast_div(zz, m_ds);
+    const int zs = zz - r1 * Ds;
+    const int r2 = fast_div(r1, m_b);
+    const int b = r1 - r2 * a.B;
+    const int cls = TR ? (r2 & (NCLS - 1)) : 0;
+    const int cob = (TR ? r2 / NCLS : r2) * 16 * MT;
+    const int qd = (TR && D3) ? (cls >> 2) & 1 : 0;
+    const int qh = TR ? (cls >> 1) & 1 : 0;
+    const int qw = TR ? cls & 1 : 0;
+
+    // epilogue constants of the (cout, pixel) elements this thread finishes, loaded up front
+    const int ej = tid >> 6;  // accumulator register j of the element
+    const int ecol = lane & 15;
+    float scl[MT], shf[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int co = min(cob + 16 * mt + 4 * kq + ej, a.Cout - 1);
+        scl[mt] = a.scale ? a.scale[co] : 1.f;
+        shf[mt] = a.shift ? a.shift[co] : 0.f;
+    }
+
+    // per-lane column byte offsets per horizontal tap (kOOB: outside the input or past the map)
+    const int xs = x0 + n16;
+    unsigned xoff[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        const int xi = TR ? xs + qw - t : xs * S - a.pw + t;
+        xoff[t] = (xs < Ws && xi >= 0 && xi < a.Wi) ? 4u * xi : kOOB;
+    }
+    // input plane / row of each vertical tap (wave-uniform)
+    int zin[KDT], yin[KT];
+    bool zok[KDT], yok[KT];
+#pragma unroll
+    for (int t = 0; t < KDT; ++t) {
+        zin[t] = D3 ? (TR ? zs + qd - t : zs * S - a.pd + t) : 0;
+        zok[t] = !D3 || (zin[t] >= 0 && zin[t] < a.Di);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        yin[t] = TR ? ys + qh - t : ys * S - a.ph + t;
+        yok[t] = yin[t] >= 0 && yin[t] < a.Hi;
+    }
+
+    const int wtap = a.cin_pad * a.cout_pad;  // elements per tap in the packed weights
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w + static_cast<long long>(cls) * TAPS * wtap), static_cast<short>(0), 4 * TAPS * wtap,
+        0x00020000);
+    const unsigned wl = 4u * (kq * a.cout_pad + cob + n16);
+
+    floatx4 acc[2][MT];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[c][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int G = (a.Cin + 3) >> 2;
+    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
+    for (int g = wave; g < G; g += 4) {
+        const int c0 = 4 * g;
+        // the group's source (4-channel aligned splits): named-field selects, no runtime index
+        const int s = c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2);
+        const int lo = s == 0 ? 0 : (s == 1 ? lo1 : lo2);
+        const float* sp = s == 0 ? a.src[0].ptr : (s == 1 ? a.src[1].ptr : a.src[2].ptr);
+        const int sC = s == 0 ? a.src[0].C : (s == 1 ? a.src[1].C : a.src[2].C);
+        const long long sb = s == 0 ? a.src[0].sb : (s == 1 ? a.src[1].sb : a.src[2].sb);
+        const int sc = static_cast<int>(s == 0 ? a.src[0].sc : (s == 1 ? a.src[1].sc : a.src[2].sc));
+        const int sd = static_cast<int>(s == 0 ? a.src[0].sd : (s == 1 ? a.src[1].sd : a.src[2].sd));
+        const int sh = static_cast<int>(s == 0 ? a.src[0].sh : (s == 1 ? a.src[1].sh : a.src[2].sh));
+        const int span = 4 * ((sC - 1) * sc + (D3 ? (a.Di - 1) * sd : 0) + (a.Hi - 1) * sh + a.Wi);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sp + b * sb), static_cast<short>(0), span, 0x00020000);
+        const int cl = c0 - lo + kq;
+        const unsigned chv = (c0 + kq < a.Cin && cl < sC) ? 4u * cl * sc : kOOB;
+
+        float bv[TAPS], av[TAPS][MT];
+#pragma unroll
+        for (int dz = 0; dz < KDT; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < KT; ++dy) {
+                const int roff = (zok[dz] && yok[dy]) ? 4 * ((D3 ? zin[dz] * sd : 0) + yin[dy] * sh)
+                                                      : static_cast<int>(kOOB);
+#pragma unroll
+                for (int dx = 0; dx < KT; ++dx) {
+                    const int tap = (dz * KT + dy) * KT + dx;
+                    bv[tap] = buf_load_s(rs, chv + xoff[dx], roff);
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        av[tap][mt] = buf_load_s(wrs, wl, 4 * (tap * wtap + c0 * a.cout_pad + 16 * mt));
+                }
+            }
+        __builtin_amdgcn_sched_barrier(0);  // every load of the group in flight before the first MFMA
+#pragma unroll
+        for (int tap = 0; tap < TAPS; ++tap)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                acc[tap & 1][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tap][mt], bv[tap], acc[tap & 1][mt], 0, 0, 0);
+    }
+
+    // the 4 waves' partial tiles -> LDS [wave][mt][j][lane]; fixed-order sum per element
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[((wave * MT + mt) * 4 + j) * 64 + lane] = acc[0][mt][j] + acc[1][mt][j];
+    __syncthreads();
+
+    const int xsub = x0 + ecol;
+    if (xsub >= Ws) return;
+    const int oz = TR ? 2 * zs + qd : zs;
+    const int oy = TR ? 2 * ys + qh : ys;
+    const int ox = TR ? 2 * xsub + qw : xsub;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int co = cob + 16 * mt + 4 * kq + ej;
+        if (co >= a.Cout) continue;
+        const int e = (mt * 4 + ej) * 64 + lane;
+        float v = ((red[e] + red[MT * 256 + e]) + red[2 * MT * 256 + e]) + red[3 * MT * 256 + e];
+        v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
+        v = apply_act(v, a.act);
+        if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(oz) * a.rd + static_cast<long long>(oy) * a.rh + ox];
+        const long long o = b * a.ob + co * a.oc + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox;
+        a.out[o] = v * a.post_scale;
+        if (a.out2) a.out2[o] = v * a.post_scale2;
+    }
+}
+
+template <bool D3, int K, int S, bool TR>
+int launch_small_m(const esm_conv_desc& a, hipStream_t s) {
+    constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
+    const int Hs = TR ? a.Hi : a.Ho, Ws = TR ? a.Wi : a.Wo;
+    const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
+    const int MT = a.Cout > 16 ? 2 : 1;
+    const long long z = static_cast<long long>(Ds) * a.B * NCLS * ceil_div(a.Cout, 16 * MT);
+    if (Hs > 65535 || z > 65535) return arg_error("conv(small): grid too large");
+    const dim3 grid(ceil_div(Ws, 16), static_cast<unsigned>(Hs), static_cast<unsigned>(z));
+    const unsigned mds = magic_for(Ds), mb = magic_for(a.B);
+    if (MT == 1)
+        hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+    else
+        hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+    return check_launch("conv(small)");
+}
+
+}  // namespace
+
+// Whether the lean form can run this layer: plain epilogue, 4-channel aligned source splits, spans
+// addressable by 32-bit buffer offsets (conv_direct.h direct_ok), a kernel shape it instantiates.
+bool small_ok(const esm_conv_desc& a) {
+    if (a.mul || a.up || a.shuffle > 1 || !direct_ok(a)) return false;
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    if (a.transposed) return a.kh == 4 && a.stride == 2;
+    if (a.stride != 1 && a.stride != 2) return false;
+    if (a.kh == 5) return !d3 && a.stride == 1;
+    return a.kh == 1 || a.kh == 3;
+}
+
+// Automatic choice (no hint): the small form for every layer it can run whose output is at most
+// 2^17 (pixel x 16-cout tile) units.  Fitted to scripts/autotune.py on MI355X (profiles/
+// r02_autotune_*.log): it won on every layer of the S / M / L hot paths up to the 96x312 maps and tied
+// at 192x624; the wide 3-D stems keep the 16-block form (checked first), single-output-channel
+// transposed layers keep their VALU form.
+bool small_auto(const esm_conv_desc& a) {
+    if (!small_ok(a)) return false;
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    if (a.transposed && a.Cout == 1) return false;
+    const long long px = static_cast<long long>(a.B) * (d3 ? a.Do : 1) * a.Ho * a.Wo;
+    const long long units = px * ceil_div(a.Cout, a.Cout > 16 ? 32 : 16);
+    return units <= (1LL << 17);
+}
+
+int launch_small(const esm_conv_desc& a, hipStream_t s) {
+    if (!small_ok(a)) return arg_error("conv: small-form hint not applicable");
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    if (a.transposed) return d3 ? launch_small_m<true, 4, 2, true>(a, s) : launch_small_m<false, 4, 2, true>(a, s);
+    const int k = a.kh, S = a.stride;
+    if (d3) {
+        if (k == 1 && S == 1) return launch_small_m<true, 1, 1, false>(a, s);
+        if (k == 3 && S == 1) return launch_small_m<true, 3, 1, false>(a, s);
+        if (k == 3 && S == 2) return launch_small_m<true, 3, 2, false>(a, s);
+    } else {
+        if (k == 1 && S == 1) return launch_small_m<false, 1, 1, false>(a, s);
+        if (k == 3 && S == 1) return launch_small_m<false, 3, 1, false>(a, s);
+        if (k == 3 && S == 2) return launch_small_m<false, 3, 2, false>(a, s);
+        if (k == 5 && S == 1) return launch_small_m<false, 5, 1, false>(a, s);
+    }
+    return arg_error("conv(small): unsupported kernel/stride");
+}
+
+}  // namespace conv
+}  // namespace esm

@@ -1,0 +1,192 @@
+// Register-resident-weight row-streaming convolution for the full-resolution 2-D layers of the ESM
+// upsampler (models/ESMStereo.py:242-509: dmNx, spx_Nx, the refinement hourglass' conv1.1 / agg
+// layers at 96x312 .. 192x624 for ESMStereo-S at KITTI): BasicConv (models/submodule.py:12-38),
+// stride 1, k1 / k3, one input source, Cout <= 32.
+//
+// A wave owns one 16-pixel column strip and R consecutive output rows (compile time), all couts of
+// its tile and the full K.  Everything but the strip / row origin is fixed at compile time:
+//   * the layer's weights live in VGPRs for the whole wave (A operands of v_mfma_f32_16x16x4_f32,
+//     K*K*NG*MT registers: 36 for 16 -> 16 k3), loaded once: no LDS, no per-MFMA operand read;
+//   * per input row and 4-channel group the K horizontally shifted B operands are K buffer_loads
+//     (per-lane voffset = channel + shifted column, kOOB-marked outside; the row in soffset, kOOB
+//     for a padding row), issued one row ahead of their MFMAs;
+//   * input row r feeds output rows r - dy (dy < K): the row loop is unrolled over the R + K - 1 input
+//     rows and only the (input, output) row pairs inside the wave's block are multiplied, so the
+//     MFMA count is exactly R * K*K * NG * MT; consecutive MFMAs go to different output rows'
+//     accumulators (no dependent-issue stall);
+//   * an output row is finished as soon as its last input row is in: BN scale/shift, activation,
+//     optional residual, * post_scale (+ second copy), 16 consecutive pixels per store.
+// The 4 waves of a workgroup take 4 adjacent strips of the same rows (their halo columns are each
+// other's interior: L1 / L2 hits).
+#include "conv_direct.h"
+
+namespace esm {
+namespace conv {
+namespace {
+
+constexpr int kWideThreads = 256;
+
+template <int K, int NG, int MT, int R>
+__global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a) {
+    constexpr int NR = R + K - 1;  // input rows a wave reads
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int n16 = lane & 15, kq = lane >> 4;
+    const int x0 = (blockIdx.x * 4 + wave) * 16;
+    const int y0 = blockIdx.y * R;
+    const int b = blockIdx.z;
+    const int cob = 0;  // Cout <= 16 * MT: one cout tile
+
+    // ---- weights -> VGPRs: w[tap][cin_pad][cout_pad], lane (kq, n16) = k row 4g + kq, cout n16
+    float wv[K * K][NG][MT];
+    {
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.w), static_cast<short>(0), 4 * K * K * a.cin_pad * a.cout_pad, 0x00020000);
+        const unsigned wl = 4u * (kq * a.cout_pad + cob + n16);
+#pragma unroll
+        for (int t = 0; t < K * K; ++t)
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    wv[t][g][mt] = buf_load_s(wrs, wl, 4 * ((t * a.cin_pad + 4 * g) * a.cout_pad + 16 * mt));
+    }
+    // BN / bias constants of the lane's couts
+    float scl[MT][4], shf[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = min(cob + 16 * mt + 4 * kq + j, a.Cout - 1);
+            scl[mt][j] = a.scale ? a.scale[co] : 1.f;
+            shf[mt][j] = a.shift ? a.shift[co] : 0.f;
+        }
+
+    // ---- input addressing
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0), 4 * ((s0.C - 1) * sc + (a.Hi - 1) * sh + a.Wi),
+        0x00020000);
+    const int xo = x0 + n16;
+    unsigned vo[NG][K];  // per-lane byte offset of group g's channel at column shift dx
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int c = 4 * g + kq;
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx) {
+            const int xi = xo - a.pw + dx;
+            vo[g][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
+        }
+    }
+    auto load_row = [&](float (&dst)[NG][K], int r) {  // input row y0 - ph + r
+        const int yi = y0 - a.ph + r;
+        const int roff = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int dx = 0; dx < K; ++dx) dst[g][dx] = buf_load_s(rs, vo[g][dx], roff);
+    };
+
+    floatx4 acc[R][MT];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[r][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const long long obase = b * a.ob;
+    auto finish = [&](int r) {  // output row y0 + r is complete
+        const int yo = y0 + r;
+        if (yo >= a.Ho || xo >= a.Wo) return;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = cob + 16 * mt + 4 * kq + j;
+                if (co >= a.Cout) continue;
+                float v = acc[r][mt][j];
+                v = a.scale ? v * scl[mt][j] + shf[mt][j] : v + shf[mt][j];
+                v = apply_act(v, a.act);
+                if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(yo) * a.rh + xo];
+                const long long o = obase + co * a.oc + static_cast<long long>(yo) * a.oh + xo;
+                a.out[o] = v * a.post_scale;
+                if (a.out2) a.out2[o] = v * a.post_scale2;
+            }
+    };
+
+    float bin[2][NG][K];
+    load_row(bin[0], 0);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {  // input row r feeds output rows r - dy, dy = K-1 .. 0
+        if (r + 1 < NR) load_row(bin[(r + 1) & 1], r + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+                for (int dy = 0; dy < K; ++dy) {
+                    const int ro = r - dy;  // output row (block-relative) this tap row feeds
+                    if (ro < 0 || ro >= R) continue;
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[ro][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[dy * K + dx][g][mt], bin[r & 1][g][dx],
+                                                                           acc[ro][mt], 0, 0, 0);
+                }
+        if (r - (K - 1) >= 0) finish(r - (K - 1));
+    }
+}
+
+template <int K, int NG, int MT>
+int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
+    const long long units = static_cast<long long>(a.B) * a.Ho * ceil_div(a.Wo, 16);
+    // rows per wave: enough waves for ~4 per SIMD (1024 SIMDs), else fewer halo rows per output row
+    const int R = units >= 4LL * 4096 ? 4 : 2;
+    const dim3 grid(ceil_div(a.Wo, 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide): grid too large");
+    if (R == 4)
+        hipLaunchKernelGGL((wconv_kernel<K, NG, MT, 4>), grid, dim3(kWideThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((wconv_kernel<K, NG, MT, 2>), grid, dim3(kWideThreads), 0, s, a);
+    return check_launch("conv(wide)");
+}
+
+}  // namespace
+
+// Whether the wide form can run this layer (and its weights fit the register budget).
+bool wide_ok(const esm_conv_desc& a) {
+    if (a.transposed || a.stride != 1 || a.nsrc != 1 || a.kd != 1 || a.Di != 1 || a.Do != 1) return false;
+    if (a.mul || a.up || a.shuffle > 1 || a.Cout > 32 || !direct_ok(a)) return false;
+    if (a.kh != a.kw || (a.kh != 1 && a.kh != 3)) return false;
+    const int ng = (a.Cin + 3) / 4, mt = a.Cout > 16 ? 2 : 1;
+    return a.kh == 3 ? (ng * mt <= 10 && (mt == 1 || ng <= 4)) : ng * mt <= 32;
+}
+
+int launch_wide(const esm_conv_desc& a, hipStream_t s) {
+    if (!wide_ok(a)) return arg_error("conv: wide-form hint not applicable");
+    const int ng = (a.Cin + 3) / 4;
+    const bool m2 = a.Cout > 16;
+    if (a.kh == 3) {
+        if (!m2) {
+            if (ng <= 2) return launch_wide_r<3, 2, 1>(a, s);
+            if (ng <= 4) return launch_wide_r<3, 4, 1>(a, s);
+            if (ng <= 6) return launch_wide_r<3, 6, 1>(a, s);
+            if (ng <= 8) return launch_wide_r<3, 8, 1>(a, s);
+            return launch_wide_r<3, 10, 1>(a, s);
+        }
+        if (ng <= 2) return launch_wide_r<3, 2, 2>(a, s);
+        return launch_wide_r<3, 4, 2>(a, s);
+    }
+    if (!m2) {
+        if (ng <= 4) return launch_wide_r<1, 4, 1>(a, s);
+        if (ng <= 8) return launch_wide_r<1, 8, 1>(a, s);
+        if (ng <= 16) return launch_wide_r<1, 16, 1>(a, s);
+        return launch_wide_r<1, 32, 1>(a, s);
+    }
+    if (ng <= 4) return launch_wide_r<1, 4, 2>(a, s);
+    if (ng <= 8) return launch_wide_r<1, 8, 2>(a, s);
+    return launch_wide_r<1, 16, 2>(a, s);
+}
+
+}  // namespace conv
+}  // namespace esm

@@ -115,7 +115,11 @@ typedef struct {
                      D/h/w; a 3x3x3 s1 p1 stem with 8 couts; bitwise equal to esm_gwc_volume_f32 followed
                      by esm_conv_f32 on the volume, without storing the volume |
                      C1IN << 20: force the VALU form for 2-D convs with one input channel
-                     (tuning sweeps / tests; see conv_impl.h launch_geom) */
+                     (tuning sweeps / tests; see conv_impl.h launch_geom) |
+                     SMALL << 21: the lean K-split form for latency-bound layers (conv_small.hip;
+                     plain epilogues: no mul / up / shuffle) |
+                     WIDE << 22: register-resident-weight row-streaming form (conv_wide.hip; 2-D, stride 1,
+                     k1 / k3, one source, Cout <= 32, plain epilogues) */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;
