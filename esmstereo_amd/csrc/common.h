@@ -30,9 +30,34 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned>((a + b - 1) / b); }
 
+// erf(x) with the two minimax polynomials of the device library's erff (|x| < 1: odd polynomial
+// in x^2; |x| >= 1: 1 - exp(-p(|x|))), both evaluated and selected instead of branched on.  The
+// library form branches per value under an exec mask, so the four values a lane finishes in an
+// MFMA epilogue run one after the other as serial dependency chains; branch-free, they interleave
+// (profiles/r02_pmc_*: ~2600 VALU per wave and 43 % issue stalls in the pair kernel were mostly erf).
+__device__ __forceinline__ float erf_bf(float x) {
+    const float ax = fabsf(x);
+    const float x2 = x * x;
+    float s = fmaf(x2, __int_as_float(0xba1345e1), __int_as_float(0x3ba10414));
+    s = fmaf(x2, s, __int_as_float(0xbcdac9b8));
+    s = fmaf(x2, s, __int_as_float(0x3de703be));
+    s = fmaf(x2, s, __int_as_float(0xbec09330));
+    s = fmaf(x2, s, __int_as_float(0x3e0375d0));
+    const float rs = fmaf(ax, s, ax);
+    float l = fmaf(ax, __int_as_float(0x378e98ab), __int_as_float(0xb9c68948));
+    l = fmaf(ax, l, __int_as_float(0x3b7cd369));
+    l = fmaf(ax, l, __int_as_float(0xbcc618b2));
+    l = fmaf(ax, l, __int_as_float(0x3dda74e4));
+    l = fmaf(ax, l, __int_as_float(0x3f228afd));
+    l = fmaf(ax, l, __int_as_float(0x3e03c728));
+    l = fmaf(ax, l, ax);
+    const float rl = 1.0f - expf(-l);
+    return copysignf(ax < 1.0f ? rs : rl, x);
+}
+
 // exact-erf GELU as nn.GELU() (models/submodule.py:37): x * 0.5 * (1 + erf(x / sqrt 2))
 __device__ __forceinline__ float gelu_erf(float x) {
-    return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+    return x * 0.5f * (1.0f + erf_bf(x * 0.70710678118654752440f));
 }
 
 // SiLU as nn.SiLU: x / (1 + exp(-x))
@@ -44,6 +69,17 @@ __device__ __forceinline__ float apply_act(float v, int act) {
         case ESM_ACT_SILU: return silu(v);
         case ESM_ACT_RELU: return v > 0.f ? v : 0.f;
         default: return v;
+    }
+}
+
+// Activation fixed at compile time (ACT >= 0: one folded case, no per-value switch in an
+// epilogue) or chosen at run time (ACT < 0).
+template <int ACT>
+__device__ __forceinline__ float act_t(float v, int act) {
+    if constexpr (ACT < 0) {
+        return apply_act(v, act);
+    } else {
+        return apply_act(v, ACT);
     }
 }
 

@@ -68,7 +68,14 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return arg_error("conv: output extent inconsistent with kernel/stride/padding");
     if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
     if (a.hint & kHintSmall) return conv::launch_small(a, s);
-    if (a.hint & kHintWide) return conv::launch_wide(a, s);
+    if (a.hint & kHintWide) {
+        // a tuned choice for a concat whose sources lie outside one buffer window (eager use, outside
+        // a launch list's arena): the automatic rules instead
+        if (conv::wide_ok(a)) return conv::launch_wide(a, s);
+        esm_conv_desc d = a;
+        d.hint = 0;
+        return launch_conv(&d, s);
+    }
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

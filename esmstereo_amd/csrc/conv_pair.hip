@@ -277,6 +277,223 @@ __global__ void __launch_bounds__(kPairThreads) pair_kernel(const esm_conv_desc 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lean 1x1 -> 3x3 pair (the full-resolution agg_1 of up_refinement, models/ESMStereo.py:228-235:
+// conv1x1 over the [u2, c1, left_f2x] concat -> BN -> GELU -> conv3x3 -> BN -> GELU).  The same
+// algorithm as pair_kernel above, with the instruction overhead that bound it (profiles/
+// r02_pmc_sq_ops_SK.txt: ~2600 VALU + ~1800 SALU per wave, SGPR spills, one LDS weight read per
+// MFMA) removed:
+//   * both layers' weights live in VGPRs for the whole wave (NKA*MA + 9*4*MA*MB registers);
+//   * the concat sources are addressed through ONE buffer descriptor based at the lowest source
+//     (the launcher checks that every source's whole batch span lies in a window addressable with
+//     the kOOB marking): a k-step's source is folded into its per-lane voffset once, so a row's
+//     loads share one descriptor and one soffset (no per-k-step source selection);
+//   * the R output rows of a wave are compile-time: the row loop is unrolled, only the R + 2 A rows
+//     the block needs are computed, and each A row is DPP-shifted once into the three horizontal
+//     taps' operands, reused by the three B rows it feeds;
+//   * the next A row's loads are in flight during the current row's MFMAs (loading all R + 2 rows up
+//     front measured slower: 38 vs 29 us at 192x624, the registers halve the waves per SIMD).
+template <int NKA, int MA, int MB, int R, int ACT>
+__global__ void __launch_bounds__(kPairThreads) lpair_kernel(const esm_conv_desc a, const esm_conv_desc bd,
+                                                             const float* wbase, int wspan, int d0, int d1, int d2) {
+    constexpr int HALO = 1, VALID = 14, NRA = R + 2;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int n16 = lane & 15, kq = lane >> 4;
+    const int H = bd.Ho, W = bd.Wo;
+    const int tx = blockIdx.x * 4 + wave;
+    const int y0 = blockIdx.y * R;
+    const int b = blockIdx.z;
+    const int col = tx * VALID - HALO + n16;  // image column of this lane (A and B tiles alike)
+    const bool col_ok = col >= 0 && col < W;
+
+    // ---- weights -> VGPRs.  A: k-step g, lane (kq, n16) = channel 4g + kq, A-cout 16ma + n16.
+    //      B: k-step (ma, j) = A channels 16ma + 4kq + j on lane group kq, B-cout 16mb + n16.
+    float wa[NKA][MA], wb[9][MA][4][MB];
+    {
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.w), static_cast<short>(0), 4 * a.cin_pad * a.cout_pad, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(bd.w), static_cast<short>(0), 4 * 9 * bd.cin_pad * bd.cout_pad, 0x00020000);
+#pragma unroll
+        for (int g = 0; g < NKA; ++g)
+#pragma unroll
+            for (int m = 0; m < MA; ++m)
+                wa[g][m] = buf_load_s(ra, 4u * ((4 * g + kq) * a.cout_pad + 16 * m + n16), 0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int m = 0; m < MA; ++m)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int mb = 0; mb < MB; ++mb)
+                        wb[t][m][j][mb] = buf_load_s(
+                            rb, 4u * ((t * bd.cin_pad + 16 * m + 4 * kq + j) * bd.cout_pad + 16 * mb + n16), 0);
+    }
+    float sA[MA][4], hA[MA][4], sB[MB][4], hB[MB][4];
+#pragma unroll
+    for (int m = 0; m < MA; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ch = min(16 * m + 4 * kq + j, a.Cout - 1);
+            sA[m][j] = a.scale ? a.scale[ch] : 1.f;
+            hA[m][j] = a.shift ? a.shift[ch] : 0.f;
+        }
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = min(16 * m + 4 * kq + j, bd.Cout - 1);
+            sB[m][j] = bd.scale ? bd.scale[co] : 1.f;
+            hB[m][j] = bd.shift ? bd.shift[co] : 0.f;
+        }
+
+    // ---- A's input: per-lane byte offset of k-step g from the window base (kOOB outside)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), static_cast<short>(0), wspan, 0x00020000);
+    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
+    unsigned vk[NKA];
+#pragma unroll
+    for (int g = 0; g < NKA; ++g) {
+        const int c = 4 * g + kq;
+        const int s = c < lo1 ? 0 : (c < lo2 ? 1 : 2);
+        const int cl = c - (s == 0 ? 0 : (s == 1 ? lo1 : lo2));
+        const long long sb = s == 0 ? a.src[0].sb : (s == 1 ? a.src[1].sb : a.src[2].sb);
+        const long long sc = s == 0 ? a.src[0].sc : (s == 1 ? a.src[1].sc : a.src[2].sc);
+        const int dl = s == 0 ? d0 : (s == 1 ? d1 : d2);
+        vk[g] = (c < a.Cin && col_ok) ? static_cast<unsigned>(dl + 4 * (b * sb + cl * sc + col)) : kOOB;
+    }
+    const int sh = static_cast<int>(a.src[0].sh);  // every source: the same row stride (launcher)
+    auto load_a = [&](float (&dst)[NKA], int ya) {
+        const int roff = (ya >= 0 && ya < H) ? 4 * ya * sh : static_cast<int>(kOOB);
+#pragma unroll
+        for (int g = 0; g < NKA; ++g) dst[g] = buf_load_s(rs, vk[g], roff);
+    };
+
+    floatx4 acc[R][MB];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int m = 0; m < MB; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const bool store_lane = n16 >= HALO && n16 < 16 - HALO && col_ok;
+
+    // software pipeline, one A row ahead: iteration ia issues the loads of A row ia + 2 and the MFMAs of
+    // A row ia + 1 before the epilogue (VALU) of A row ia, so the matrix pipe has independent work
+    // while the wave evaluates GELU (the per-wave phases were serial: PMC showed 43-50 % issue stalls)
+    float bin[3][NKA];
+    floatx4 aA[2][2][MA];  // [A row parity][accumulation chain][m]
+    auto a_mfma = [&](int ia) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int m = 0; m < MA; ++m) aA[ia & 1][c][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < NKA; ++g)
+#pragma unroll
+            for (int m = 0; m < MA; ++m)
+                aA[ia & 1][g & 1][m] =
+                    __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][m], bin[ia % 3][g], aA[ia & 1][g & 1][m], 0, 0, 0);
+    };
+    load_a(bin[0], y0 - 1);
+    load_a(bin[1], y0);
+    a_mfma(0);
+#pragma unroll
+    for (int ia = 0; ia < NRA; ++ia) {  // A row y0 - 1 + ia feeds B rows ia - dy (dy = 0..2)
+        if (ia + 2 < NRA) load_a(bin[(ia + 2) % 3], y0 + ia + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ia + 1 < NRA) a_mfma(ia + 1);
+        // A's epilogue; zero outside the image (B's zero padding) and past A's couts
+        const int ya = y0 - 1 + ia;
+        const bool row_ok = ya >= 0 && ya < H;
+        float v3[3][MA][4];  // the three horizontal taps' B operands (columns n - 1, n, n + 1)
+#pragma unroll
+        for (int m = 0; m < MA; ++m)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = 16 * m + 4 * kq + j;
+                const float sum = aA[ia & 1][0][m][j] + aA[ia & 1][1][m][j];
+                const float v = act_t<ACT>(a.scale ? sum * sA[m][j] + hA[m][j] : sum + hA[m][j], a.act);
+                const float z = (row_ok && col_ok && ch < a.Cout) ? v : 0.f;
+                v3[0][m][j] = row_shift<-1>(z);
+                v3[1][m][j] = z;
+                v3[2][m][j] = row_shift<1>(z);
+            }
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+            const int ro = ia - dy;  // B row (block-relative) fed by this A row through tap row dy
+            if (ro < 0 || ro >= R) continue;
+#pragma unroll
+            for (int m = 0; m < MA; ++m)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                        for (int mb = 0; mb < MB; ++mb)
+                            acc[ro][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[dy * 3 + dx][m][j][mb], v3[dx][m][j],
+                                                                               acc[ro][mb], 0, 0, 0);
+        }
+        const int rf = ia - 2;  // B row complete after its last A row
+        if (rf < 0) continue;
+        const int yb = y0 + rf;
+        if (yb >= H || !store_lane) continue;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 16 * mb + 4 * kq + j;
+                if (co >= bd.Cout) continue;
+                const float s = acc[rf][mb][j];
+                float v = act_t<ACT>(bd.scale ? s * sB[mb][j] + hB[mb][j] : s + hB[mb][j], bd.act);
+                if (bd.res) v = v + bd.res[b * bd.rb + co * bd.rc + static_cast<long long>(yb) * bd.rh + col];
+                bd.out[b * bd.ob + co * bd.oc + static_cast<long long>(yb) * bd.oh + col] = v * bd.post_scale;
+            }
+    }
+}
+
+// Lean 1x1 -> 3x3 form, when its preconditions hold: returns ESM_ERR_UNSUPPORTED (no launch) otherwise.
+template <int MA, int MB>
+int launch_lpair_m(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s, const float* base, int span,
+                   const int (&dl)[3], int nk, int R) {
+    const int H = b.Ho, W = b.Wo;
+    const dim3 grid(ceil_div(ceil_div(W, 14), 4), ceil_div(H, R), static_cast<unsigned>(a.B));
+    if (grid.y > 65535u || grid.z > 65535u) return ESM_ERR_UNSUPPORTED;
+    // both BasicConvs of the hot path end in GELU: that case compiled with the activation folded in
+    const bool gg = a.act == ESM_ACT_GELU && b.act == ESM_ACT_GELU;
+#define ESM_LPAIR(NK, RR)                                                                                          \
+    do {                                                                                                          \
+        if (gg)                                                                                                   \
+            hipLaunchKernelGGL((lpair_kernel<NK, MA, MB, RR, ESM_ACT_GELU>), grid, dim3(kPairThreads), 0, s, a, b, \
+                               base, span, dl[0], dl[1], dl[2]);                                                  \
+        else                                                                                                      \
+            hipLaunchKernelGGL((lpair_kernel<NK, MA, MB, RR, -1>), grid, dim3(kPairThreads), 0, s, a, b, base,     \
+                               span, dl[0], dl[1], dl[2]);                                                        \
+    } while (0)
+    if (nk <= 4) { if (R == 4) ESM_LPAIR(4, 4); else ESM_LPAIR(4, 2); }
+    else if (nk <= 8) { if (R == 4) ESM_LPAIR(8, 4); else ESM_LPAIR(8, 2); }
+    else if (nk <= 16) { if (R == 4) ESM_LPAIR(16, 4); else ESM_LPAIR(16, 2); }
+    else if (nk <= 24 && MA == 1) ESM_LPAIR(24, 2);  // 4 rows: 264 registers, one wave per SIMD
+    else return ESM_ERR_UNSUPPORTED;
+#undef ESM_LPAIR
+    return check_launch("conv pair (lean)");
+}
+
+int launch_lpair(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
+    if (a.kh != 1 || b.kh != 3 || b.res || b.out2) return ESM_ERR_UNSUPPORTED;
+    // one descriptor over every source's whole batch span (conv_direct.h source_window)
+    const float* base = nullptr;
+    int span = 0, dl[ESM_MAX_SRC];
+    if (!source_window(a, &base, &span, dl)) return ESM_ERR_UNSUPPORTED;
+    const int nk = (a.Cin + 3) / 4;
+    const long long units = static_cast<long long>(a.B) * b.Ho * ceil_div(b.Wo, 14);
+    const int R = units >= 4LL * 2048 ? 4 : 2;  // rows per wave: ~2+ waves per SIMD either way
+    const int ma = a.Cout > 16 ? 2 : 1, mb = b.Cout > 16 ? 2 : 1;
+    if (ma == 1 && mb == 1) return launch_lpair_m<1, 1>(a, b, s, base, span, dl, nk, R);
+    if (ma == 1 && mb == 2) return launch_lpair_m<1, 2>(a, b, s, base, span, dl, nk, R);
+    return ESM_ERR_UNSUPPORTED;
+}
+
 template <int KA, int KB, int MA, int MB, int NKA>
 int launch_pair_t(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     using G = PGeo<KA, KB, MA, MB, NKA>;
@@ -348,6 +565,9 @@ int launch_conv_pair(const esm_conv_desc* pa, const esm_conv_desc* pb, hipStream
         a.Cin > 96)
         return arg_error("conv pair: inconsistent shapes");
     int rc = ESM_ERR_UNSUPPORTED;
+    // the lean 1x1 -> 3x3 form unless a.hint asks for the LDS-weight kernel (bit 23: A/B, tests)
+    if (a.kh == 1 && b.kh == 3 && !(a.hint & (1 << 23))) rc = launch_lpair(a, b, s);
+    if (rc != ESM_ERR_UNSUPPORTED) return rc;
     if (a.kh == 1 && b.kh == 3) rc = launch_pair_m<1, 3>(a, b, s);
     else if (a.kh == 3 && b.kh == 3) rc = launch_pair_m<3, 3>(a, b, s);
     else if (a.kh == 3 && b.kh == 1) rc = launch_pair_m<3, 1>(a, b, s);

@@ -39,7 +39,7 @@ inline unsigned magic_for(int d) {
     return d <= 1 ? 0u : static_cast<unsigned>(((1ull << 32) + static_cast<unsigned long long>(d) - 1) / d);
 }
 
-template <bool D3, int K, int S, bool TR, int MT>
+template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN>
 __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
     constexpr int KT = TR ? 2 : K;  // taps per dim (per parity class when transposed)
     constexpr int KDT = D3 ? KT : 1;
@@ -163,10 +163,31 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
     __syncthreads();
 
     const int xsub = x0 + ecol;
-    if (xsub >= Ws) return;
     const int oz = TR ? 2 * zs + qd : zs;
     const int oy = TR ? 2 * ys + qh : ys;
     const int ox = TR ? 2 * xsub + qw : xsub;
+    if constexpr (PLAIN) {
+        // buffer store over this batch item: (cout, column) in voffset, (plane, row) in soffset; a cout
+        // past Cout or a column past the map carries kOOB and the hardware drops the store
+        const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+            a.out + b * a.ob, static_cast<short>(0),
+            4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (D3 ? (a.Do - 1) * static_cast<int>(a.od) : 0) +
+                 (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+            0x00020000);
+        const int orow = 4 * ((D3 ? oz * static_cast<int>(a.od) : 0) + oy * static_cast<int>(a.oh));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int co = cob + 16 * mt + 4 * kq + ej;
+            const int e = (mt * 4 + ej) * 64 + lane;
+            float v = ((red[e] + red[MT * 256 + e]) + red[2 * MT * 256 + e]) + red[3 * MT * 256 + e];
+            v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
+            v = act_t<ACT>(v, a.act);
+            const unsigned vo = (co < a.Cout && xsub < Ws) ? 4u * (co * static_cast<int>(a.oc) + ox) : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(vo), orow, 0);
+        }
+        return;
+    }
+    if (xsub >= Ws) return;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const int co = cob + 16 * mt + 4 * kq + ej;
@@ -174,7 +195,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
         const int e = (mt * 4 + ej) * 64 + lane;
         float v = ((red[e] + red[MT * 256 + e]) + red[2 * MT * 256 + e]) + red[3 * MT * 256 + e];
         v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
-        v = apply_act(v, a.act);
+        v = act_t<ACT>(v, a.act);
         if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(oz) * a.rd + static_cast<long long>(oy) * a.rh + ox];
         const long long o = b * a.ob + co * a.oc + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox;
         a.out[o] = v * a.post_scale;
@@ -192,10 +213,17 @@ int launch_small_m(const esm_conv_desc& a, hipStream_t s) {
     if (Hs > 65535 || z > 65535) return arg_error("conv(small): grid too large");
     const dim3 grid(ceil_div(Ws, 16), static_cast<unsigned>(Hs), static_cast<unsigned>(z));
     const unsigned mds = magic_for(Ds), mb = magic_for(a.B);
-    if (MT == 1)
-        hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
-    else
-        hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+    // BasicConv (BN + GELU, nothing else) with the activation folded in and the buffer-store epilogue
+    const bool gelu = a.act == ESM_ACT_GELU && !a.res && !a.out2 && a.post_scale == 1.f &&
+                      static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(D3 ? a.Do : 1) * a.od +
+                              static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (MT == 1) {
+        if (gelu) hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1, ESM_ACT_GELU, true>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+        else hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1, -1, false>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+    } else {
+        if (gelu) hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2, ESM_ACT_GELU, true>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+        else hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2, -1, false>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+    }
     return check_launch("conv(small)");
 }
 

@@ -1,7 +1,7 @@
 // Register-resident-weight row-streaming convolution for the full-resolution 2-D layers of the ESM
 // upsampler (models/ESMStereo.py:242-509: dmNx, spx_Nx, the refinement hourglass' conv1.1 / agg
 // layers at 96x312 .. 192x624 for ESMStereo-S at KITTI): BasicConv (models/submodule.py:12-38),
-// stride 1, k1 / k3, one input source, Cout <= 32.
+// stride 1, k1 / k3, Cout <= 32, one input or a channel concat of up to 3 (spx_Nx.0, agg_N.0).
 //
 // A wave owns one 16-pixel column strip and R consecutive output rows (compile time), all couts of
 // its tile and the full K.  Everything but the strip / row origin is fixed at compile time:
@@ -9,7 +9,7 @@
 //     K*K*NG*MT registers: 36 for 16 -> 16 k3), loaded once: no LDS, no per-MFMA operand read;
 //   * per input row and 4-channel group the K horizontally shifted B operands are K buffer_loads
 //     (per-lane voffset = channel + shifted column, kOOB-marked outside; the row in soffset, kOOB
-//     for a padding row), issued one row ahead of their MFMAs;
+//     for a padding row), issued one (R = 2) or two (R >= 4) rows ahead of their MFMAs;
 //   * input row r feeds output rows r - dy (dy < K): the row loop is unrolled over the R + K - 1 input
 //     rows and only the (input, output) row pairs inside the wave's block are multiplied, so the
 //     MFMA count is exactly R * K*K * NG * MT; consecutive MFMAs go to different output rows'
@@ -26,8 +26,9 @@ namespace {
 
 constexpr int kWideThreads = 256;
 
-template <int K, int NG, int MT, int R>
-__global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a) {
+template <int K, int NG, int MT, int R, int ACT, bool PLAIN>
+__global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a, const float* wbase, int wspan,
+                                                             int d0, int d1, int d2) {
     constexpr int NR = R + K - 1;  // input rows a wave reads
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -62,21 +63,28 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
             shf[mt][j] = a.shift ? a.shift[co] : 0.f;
         }
 
-    // ---- input addressing
-    const esm_src& s0 = a.src[0];
-    const int sc = static_cast<int>(s0.sc), sh = static_cast<int>(s0.sh);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0), 4 * ((s0.C - 1) * sc + (a.Hi - 1) * sh + a.Wi),
-        0x00020000);
+    // ---- input addressing: one descriptor over the sources' window (conv_direct.h source_window);
+    //      a group's source, batch item and channel are folded into its per-lane voffsets once
+    const int sh = static_cast<int>(a.src[0].sh);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), static_cast<short>(0), wspan, 0x00020000);
+    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
     const int xo = x0 + n16;
     unsigned vo[NG][K];  // per-lane byte offset of group g's channel at column shift dx
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
         const int c = 4 * g + kq;
+        const int s = c < lo1 ? 0 : (c < lo2 ? 1 : 2);
+        const int cl = c - (s == 0 ? 0 : (s == 1 ? lo1 : lo2));
+        const long long sb = s == 0 ? a.src[0].sb : (s == 1 ? a.src[1].sb : a.src[2].sb);
+        const long long sc = s == 0 ? a.src[0].sc : (s == 1 ? a.src[1].sc : a.src[2].sc);
+        const int dl = s == 0 ? d0 : (s == 1 ? d1 : d2);
 #pragma unroll
         for (int dx = 0; dx < K; ++dx) {
             const int xi = xo - a.pw + dx;
-            vo[g][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
+            vo[g][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi)
+                            ? static_cast<unsigned>(dl + 4 * (b * sb + cl * sc + xi))
+                            : kOOB;
         }
     }
     auto load_row = [&](float (&dst)[NG][K], int r) {  // input row y0 - ph + r
@@ -94,31 +102,52 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[r][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    const long long obase = b * a.ob;
+    // output through a buffer descriptor over this batch item: per-lane voffset (cout, column) fixed
+    // for the whole wave, the row in soffset; a cout past Cout / column past Wo / row past Ho carries
+    // kOOB, so the hardware drops the store (no branches, no 64-bit address arithmetic per store)
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0), 4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+    unsigned ovo[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = cob + 16 * mt + 4 * kq + j;
+            ovo[mt][j] = (co < a.Cout && xo < a.Wo) ? 4u * (co * static_cast<int>(a.oc) + xo) : kOOB;
+        }
     auto finish = [&](int r) {  // output row y0 + r is complete
         const int yo = y0 + r;
-        if (yo >= a.Ho || xo >= a.Wo) return;
+        const int orow = yo < a.Ho ? 4 * yo * static_cast<int>(a.oh) : static_cast<int>(kOOB);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int co = cob + 16 * mt + 4 * kq + j;
-                if (co >= a.Cout) continue;
                 float v = acc[r][mt][j];
                 v = a.scale ? v * scl[mt][j] + shf[mt][j] : v + shf[mt][j];
-                v = apply_act(v, a.act);
-                if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(yo) * a.rh + xo];
-                const long long o = obase + co * a.oc + static_cast<long long>(yo) * a.oh + xo;
-                a.out[o] = v * a.post_scale;
-                if (a.out2) a.out2[o] = v * a.post_scale2;
+                v = act_t<ACT>(v, a.act);
+                if constexpr (!PLAIN) {
+                    const int co = cob + 16 * mt + 4 * kq + j;
+                    if (yo >= a.Ho || xo >= a.Wo || co >= a.Cout) continue;
+                    if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(yo) * a.rh + xo];
+                    const long long o = b * a.ob + co * a.oc + static_cast<long long>(yo) * a.oh + xo;
+                    a.out[o] = v * a.post_scale;
+                    if (a.out2) a.out2[o] = v * a.post_scale2;
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(ovo[mt][j]), orow, 0);
+                }
             }
     };
 
-    float bin[2][NG][K];
-    load_row(bin[0], 0);
+    // input rows in flight: PF ahead of the row being multiplied (ring of PF + 1 row buffers)
+    constexpr int PF = R >= 4 ? 2 : 1;
+    constexpr int NB = PF + 1;
+    float bin[NB][NG][K];
+#pragma unroll
+    for (int r = 0; r < PF; ++r) load_row(bin[r], r);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {  // input row r feeds output rows r - dy, dy = K-1 .. 0
-        if (r + 1 < NR) load_row(bin[(r + 1) & 1], r + 1);
+        if (r + PF < NR) load_row(bin[(r + PF) % NB], r + PF);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < NG; ++g)
@@ -130,7 +159,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
                     if (ro < 0 || ro >= R) continue;
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt)
-                        acc[ro][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[dy * K + dx][g][mt], bin[r & 1][g][dx],
+                        acc[ro][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[dy * K + dx][g][mt], bin[r % NB][g][dx],
                                                                            acc[ro][mt], 0, 0, 0);
                 }
         if (r - (K - 1) >= 0) finish(r - (K - 1));
@@ -140,14 +169,33 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
 template <int K, int NG, int MT>
 int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
     const long long units = static_cast<long long>(a.B) * a.Ho * ceil_div(a.Wo, 16);
-    // rows per wave: enough waves for ~4 per SIMD (1024 SIMDs), else fewer halo rows per output row
-    const int R = units >= 4LL * 4096 ? 4 : 2;
+    // rows per wave, from a sweep of the 3x3 16 -> 16 layer at 192x624 (scripts/probes/k3_micro.hip):
+    // 8 rows (2 rows of loads in flight) 10.3 us, 4 rows 11.7, 2 rows 14.1 -- fewer halo rows and
+    // longer MFMA runs beat more waves per SIMD; small maps keep at least ~1 wave per SIMD
+    const int R = units >= 6144 ? 8 : (units >= 3072 ? 4 : 2);
     const dim3 grid(ceil_div(a.Wo, 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide): grid too large");
-    if (R == 4)
-        hipLaunchKernelGGL((wconv_kernel<K, NG, MT, 4>), grid, dim3(kWideThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL((wconv_kernel<K, NG, MT, 2>), grid, dim3(kWideThreads), 0, s, a);
+    const float* base = nullptr;
+    int span = 0, dl[ESM_MAX_SRC];
+    if (!source_window(a, &base, &span, dl)) return arg_error("conv(wide): sources outside one buffer window");
+    // BasicConv (BN + GELU, nothing else: the hot path's common case) compiled with the activation
+    // folded in and the branch-free buffer-store epilogue; anything else takes the general epilogue
+    const bool gelu = a.act == ESM_ACT_GELU && !a.res && !a.out2 && a.post_scale == 1.f &&
+                      static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+#define ESM_WIDE(RR, AC)                                                                                         \
+    hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU)>), grid, dim3(kWideThreads), 0, s, a, base, \
+                       span, dl[0], dl[1], dl[2])
+    if (R == 8) {
+        if (gelu) ESM_WIDE(8, ESM_ACT_GELU);
+        else ESM_WIDE(8, -1);
+    } else if (R == 4) {
+        if (gelu) ESM_WIDE(4, ESM_ACT_GELU);
+        else ESM_WIDE(4, -1);
+    } else {
+        if (gelu) ESM_WIDE(2, ESM_ACT_GELU);
+        else ESM_WIDE(2, -1);
+    }
+#undef ESM_WIDE
     return check_launch("conv(wide)");
 }
 
@@ -155,8 +203,11 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
 
 // Whether the wide form can run this layer (and its weights fit the register budget).
 bool wide_ok(const esm_conv_desc& a) {
-    if (a.transposed || a.stride != 1 || a.nsrc != 1 || a.kd != 1 || a.Di != 1 || a.Do != 1) return false;
+    if (a.transposed || a.stride != 1 || a.kd != 1 || a.Di != 1 || a.Do != 1) return false;
     if (a.mul || a.up || a.shuffle > 1 || a.Cout > 32 || !direct_ok(a)) return false;
+    const float* base;
+    int span, dl[ESM_MAX_SRC];
+    if (!source_window(a, &base, &span, dl)) return false;
     if (a.kh != a.kw || (a.kh != 1 && a.kh != 3)) return false;
     const int ng = (a.Cin + 3) / 4, mt = a.Cout > 16 ? 2 : 1;
     return a.kh == 3 ? (ng * mt <= 10 && (mt == 1 || ng <= 4)) : ng * mt <= 32;
@@ -180,7 +231,10 @@ int launch_wide(const esm_conv_desc& a, hipStream_t s) {
     if (!m2) {
         if (ng <= 4) return launch_wide_r<1, 4, 1>(a, s);
         if (ng <= 8) return launch_wide_r<1, 8, 1>(a, s);
+        if (ng <= 12) return launch_wide_r<1, 12, 1>(a, s);
+        if (ng <= 14) return launch_wide_r<1, 14, 1>(a, s);
         if (ng <= 16) return launch_wide_r<1, 16, 1>(a, s);
+        if (ng <= 24) return launch_wide_r<1, 24, 1>(a, s);
         return launch_wide_r<1, 32, 1>(a, s);
     }
     if (ng <= 4) return launch_wide_r<1, 4, 2>(a, s);

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import math
 import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -177,6 +178,8 @@ class Ctx:
         # one entry per launch-list op: name, kernel family, algorithmic flops / HBM bytes
         self.meta: List[dict] = []
         self.stream = None if plan else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self._arena: Optional[torch.Tensor] = None
+        self._arena_off = 0
 
     def launch(self, graph: bool = True, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Run a plan context's launch list (as a hipGraph by default) on the current stream."""
@@ -203,10 +206,22 @@ class Ctx:
         except Exception:
             pass
 
+    ARENA_CHUNK = 256 << 20  # bytes: one chunk holds every buffer of an S / M plan at KITTI size
+
     def empty(self, *shape: int) -> torch.Tensor:
-        t = torch.empty(shape, device=self.device, dtype=torch.float32)
-        if self.plan:
-            self.keep.append(t)
+        """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of large arena chunks, so
+        the buffers of one launch list sit close together: kernels that address several sources through
+        one buffer descriptor (the lean conv pair) need them inside one window."""
+        if not self.plan:
+            return torch.empty(shape, device=self.device, dtype=torch.float32)
+        n = math.prod(shape)
+        nb = (4 * n + 255) // 256 * 256
+        if self._arena is None or self._arena_off + nb > self._arena.numel():
+            self._arena = torch.empty(max(self.ARENA_CHUNK, nb), device=self.device, dtype=torch.uint8)
+            self._arena_off = 0
+            self.keep.append(self._arena)
+        t = self._arena[self._arena_off:self._arena_off + 4 * n].view(torch.float32).view(shape)
+        self._arena_off += nb
         return t
 
     def hold(self, *objs) -> None:
@@ -515,6 +530,8 @@ def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, att
 
 # Fused pairs (esm_conv_pair_f32) are used unless ESM_NO_PAIR is set (A/B measurements).
 PAIRS_ENABLED = not os.environ.get("ESM_NO_PAIR")
+PAIR_LEGACY = bool(os.environ.get("ESM_PAIR_LEGACY"))
+PAIR_K1 = bool(os.environ.get("ESM_PAIR_K1"))  # fuse 1x1 -> 3x3 pairs again (A/B runs)
 
 
 def pair_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
@@ -528,9 +545,13 @@ def pair_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor])
     # (cheap first conv) and 3x3 -> 1x1 (no row halo) win
     if pa.k == 3 and pb.k == 3:
         return False
-    # 1x1 -> 3x3 wins only on the full-resolution map (ref4x.agg_1, 192x624: -3 us); on the smaller
-    # ones the pair's shorter row runs leave too few waves and it loses 1.6-2.3 us to two launches
+    # 1x1 -> 3x3: two launches of the register-weight row-streaming form (conv_wide.hip) beat every
+    # fused pair measured (scripts/probes/conv_bench.cpp at ref4x.agg_1, 192x624: lean pair 29.2 us,
+    # LDS-weight pair 30.5, wide 1x1 11.7 + wide 3x3 14.9 before the 8-row waves); the pair recomputes
+    # the 1x1 rows under each wave's halo
     B, _, H, W = (int(v) for v in srcs[0].shape)
+    if pa.k == 1 and not PAIR_K1:
+        return False
     if pa.k == 1 and B * H * W < 65536:
         return False
     cins = [int(t.shape[1]) for t in srcs]
@@ -559,6 +580,8 @@ def run_conv_pair(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: Pa
         mid = run_conv(ctx, pa, srcs, tag=tags[0] or tag + ".a")
         return run_conv(ctx, pb, [mid], out, res=res, tag=tags[1] or tag + ".b")
     da, _, ma = _conv_desc(ctx, pa, srcs, alloc_out=False, tag=tag)
+    if PAIR_LEGACY:
+        da.hint |= 1 << 23  # the LDS-weight pair kernel instead of the lean 1x1 -> 3x3 form (A/B runs)
     B, _, H, W = (int(v) for v in srcs[0].shape)
     db, out, mb = _conv_desc(ctx, pb, [], out, res=res, tag=tag, virtual_in=(B, pa.cout, H, W))
     ctx.meta.append(dict(name=tag, kind="conv_pair", flops=ma["flops"] + mb["flops"],

@@ -259,7 +259,7 @@ def test_conv_small_form(nd, cins, cout, k, s, tr, shape):
 HINT_WIDE = 1 << 22
 WIDE_CASES = [(16, 16, 3, 1, (192, 624)), (16, 16, 3, 1, (94, 310)), (40, 16, 3, 1, (96, 312)),
               (16, 8, 3, 1, (96, 312)), (16, 16, 1, 1, (94, 310)), (56, 16, 1, 0, (96, 312)),
-              (32, 32, 3, 1, (47, 83)), (6, 24, 3, 1, (33, 50)), (128, 16, 1, 0, (9, 70)), (16, 16, 3, 1, (5, 17))]
+              (16, 32, 3, 1, (47, 83)), (6, 24, 3, 1, (33, 50)), (128, 16, 1, 0, (9, 70)), (16, 16, 3, 1, (5, 17))]
 
 
 @pytest.mark.parametrize("cin,cout,k,p,shape", WIDE_CASES)
@@ -278,6 +278,23 @@ def test_conv_wide_form(cin, cout, k, p, shape):
                  post_scale2=2.0, hint=HINT_WIDE)
     ref2 = _ref_conv([x], conv, bn, ACT_GELU, res=res)
     assert rel(y, ref2 * 4) < 1e-5 and rel(out2, ref2 * 2) < 1e-5
+
+
+@pytest.mark.parametrize("cins,cout,k,p,shape", [((16, 24), 16, 3, 1, (96, 312)), ((16, 16, 24), 16, 1, 0, (96, 312)),
+                                                  ((16, 16, 32), 16, 1, 0, (47, 157)), ((8, 8), 24, 3, 1, (19, 40))])
+def test_conv_wide_form_multisource(cins, cout, k, p, shape):
+    """Wide form over a channel concat (spx_Nx.0, agg_N.0): the sources carved out of one allocation, as a
+    launch list's arena carves them, so one buffer window covers them; vs fp64 torch (1e-5 relative)."""
+    conv, bn = _mk(2, sum(cins), cout, k, 1, p, seed=10)
+    n = [2 * c * shape[0] * shape[1] for c in cins]
+    pool = torch.randn(sum(n) + 1000, device=DEV)
+    xs, off = [], 500
+    for c, m in zip(cins, n):
+        xs.append(pool[off:off + m].view(2, c, *shape))
+        off += m
+    ref = _ref_conv([x.cpu() for x in xs], conv, bn, ACT_GELU)
+    y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), xs, hint=HINT_WIDE)
+    assert rel(y, ref) < 1e-5
 
 
 def test_conv_small_form_epilogues():
@@ -435,7 +452,7 @@ def test_shuffle_tail(nf, r, H, W):
 def test_conv_pair(ka, kb, cins, cm, cout, act_a, act_b, res, H, W):
     """Fused pair (esm_conv_pair_f32) vs fp64 torch of the two layers; rel <= 1e-5.  Ragged
     extents (tiles of 12-14 valid columns, rows not a multiple of the wave's run)."""
-    from esmstereo_amd.engine import run_conv_pair, pair_supported
+    from esmstereo_amd.engine import PAIR_K1, run_conv_pair, pair_supported
     bias_a = act_a == ACT_SILU
     ca, ba = _mk(2, sum(cins), cm, ka, 1, ka // 2, bias=bias_a, bn=not bias_a, seed=21)
     cb, bb = _mk(2, cm, cout, kb, 1, kb // 2, bias=res, bn=not res, seed=22)
@@ -445,7 +462,8 @@ def test_conv_pair(ka, kb, cins, cm, cout, act_a, act_b, res, H, W):
     ref = _ref_conv([mid], cb, bb, act_b, res=resid)
     pa, pb = pk(ca, ba, act_a), pk(cb, bb, act_b)
     big = 2 * H * W >= 65536
-    assert pair_supported(pa, pb, [x.to(DEV) for x in xs]) == ((cm <= 16 or cout <= 16) and ((ka == 1 and big) or kb == 1))
+    assert pair_supported(pa, pb, [x.to(DEV) for x in xs]) == ((cm <= 16 or cout <= 16) and
+                                                               ((ka == 1 and big and PAIR_K1) or kb == 1))
     y = run_conv_pair(Ctx(DEV), pa, [x.to(DEV) for x in xs], pb, res=resid.to(DEV) if res else None)
     assert rel(y, ref) < 1e-5
     if not pair_supported(pa, pb, [x.to(DEV) for x in xs]) and (cm <= 16 or cout <= 16):
@@ -457,6 +475,29 @@ def test_conv_pair(ka, kb, cins, cm, cout, act_a, act_b, res, H, W):
         db, out, _ = _conv_desc(ctx, pb, [], virtual_in=(2, cm, H, W))
         ctx.pair(da, db)
         assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("cins,cout,H,W", [((16, 16, 24), 16, 130, 270), ((16, 16, 24), 16, 192, 624),
+                                           ((56,), 16, 37, 61), ((16, 32), 32, 23, 80), ((6,), 16, 5, 9),
+                                           ((16, 16, 32), 16, 48, 156)])
+def test_conv_pair_lean_vs_lds(cins, cout, H, W):
+    """The lean 1x1 -> 3x3 pair (register weights, one descriptor over the concat sources, compile-time
+    rows) and the LDS-weight pair kernel (forced by hint bit 23) vs fp64 torch (1e-5 relative), batch 2,
+    ragged extents, one and two B cout tiles."""
+    from esmstereo_amd.engine import _conv_desc
+    ca, ba = _mk(2, sum(cins), 16, 1, 1, 0, seed=31)
+    cb, bb = _mk(2, 16, cout, 3, 1, 1, seed=32)
+    xs = [torch.randn(2, c, H, W) for c in cins]
+    ref = _ref_conv([_ref_conv(xs, ca, ba, ACT_GELU)], cb, bb, ACT_GELU)
+    pa, pb = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
+    xd = [x.to(DEV) for x in xs]
+    for hint in (0, 1 << 23):
+        ctx = Ctx(DEV)
+        da, _, _ = _conv_desc(ctx, pa, xd, alloc_out=False)
+        da.hint = hint
+        db, out, _ = _conv_desc(ctx, pb, [], virtual_in=(2, 16, H, W))
+        ctx.pair(da, db)
+        assert rel(out, ref) < 1e-5, hex(hint)
 
 
 def test_conv_multisource_crop_and_epilogues():
@@ -818,3 +859,23 @@ def test_conv_c1in_form(cout, k, s, p, H, W):
     pc = pk(conv, bn, ACT_GELU)
     for h in (1 << 20, 0):
         assert rel(run_conv(Ctx(DEV), pc, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
+
+
+def test_gelu_epilogue_branch_free_erf():
+    """The conv epilogue's GELU (common.h erf_bf: the device library's erff polynomials, evaluated
+    branch-free) through a 1x1 identity conv over [-12, 12], densest around the |x / sqrt 2| = 1 switch,
+    vs fp64 torch GELU: |error| <= 2.5e-7 |x| (2 fp32 ulps of the input's scale: 1 + erf cancels for
+    negative x, in every fp32 evaluation of the formula, torch's own included)."""
+    x = torch.cat([torch.linspace(-12, 12, 200001), torch.linspace(1.40, 1.43, 20001),
+                   torch.linspace(-1.43, -1.40, 20001), torch.tensor([0.0, -0.0, 1e-30, -1e-30])])
+    n = x.numel()
+    conv = torch.nn.Conv2d(1, 1, 1, bias=False)
+    with torch.no_grad():
+        conv.weight.fill_(1.0)
+    p = pk(conv, None, ACT_GELU)
+    for hint in (0, HINT_SMALL, HINT_WIDE):
+        y = run_conv(Ctx(DEV), p, [x.view(1, 1, 1, n).to(DEV)], hint=hint).view(-1).double().cpu()
+        ref = F.gelu(x.double())
+        assert bool(((y - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all()), hex(hint)
+        yt = F.gelu(x.to(DEV)).double().cpu()  # torch's own fp32 GELU meets the same bound
+        assert bool(((yt - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all())
