@@ -18,6 +18,8 @@ bool small_auto(const esm_conv_desc& a);                 // conv_small.hip
 int launch_small(const esm_conv_desc& a, hipStream_t s);  // conv_small.hip
 bool wide_ok(const esm_conv_desc& a);                    // conv_wide.hip
 int launch_wide(const esm_conv_desc& a, hipStream_t s);  // conv_wide.hip
+bool wide3_ok(const esm_conv_desc& a);                    // conv_wide3.hip
+int launch_wide3(const esm_conv_desc& a, hipStream_t s);  // conv_wide3.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
@@ -26,6 +28,7 @@ constexpr int kHintGwcStem = 1 << 19;  // input = the virtual gwc volume of src[
 constexpr int kHintC1in = 1 << 20;     // force the VALU single-input-channel form (conv_stem.hip)
 constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound layers (conv_small.hip)
 constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
+constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -76,6 +79,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         d.hint = 0;
         return launch_conv(&d, s);
     }
+    if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

@@ -1,0 +1,193 @@
+// Register-resident-weight plane-streaming 3-D convolution (3x3x3, stride 1, padding 1, Cout <= 16):
+// the 3-D stems of the hot path, group_stem (32 -> 8), corr_stem (1 -> 8) and agg (8 -> 8)
+// (models/ESMStereo.py:610,620,622, used at :703-715; BasicConv, models/submodule.py:12-38), which at
+// ESMStereo-L KITTI are a fifth of the whole step.
+//
+// The 3-D analogue of conv_wide.hip.  A workgroup owns one 16-pixel column strip of one output row y
+// and a block of Z output planes; its 4 waves split the work KSW ways over 4-channel groups (wave
+// w takes groups w % KSW, w % KSW + KSW, ...) and 4 / KSW ways over sub-blocks of the planes.  A wave
+// keeps its groups' 27-tap weights in VGPRs and streams input planes: plane zi's 9 in-plane taps are
+// 9 buffer_loads per group (3 rows x 3 column shifts, kOOB-marked borders), and each feeds the MFMAs
+// of the three output planes zi + 1, zi, zi - 1 (tap plane dz = 0, 1, 2), so a loaded operand is
+// used three times and consecutive MFMAs go to different planes' accumulators.  The loop over input
+// planes is unrolled (compile-time Z) and only (input, output) plane pairs inside the block are
+// multiplied.  The waves' partial tiles meet in LDS at the end and are added in a fixed order
+// (deterministic); every thread then finishes its (plane, cout, pixel) elements.
+#include "conv_direct.h"
+
+namespace esm {
+namespace conv {
+namespace {
+
+constexpr int kW3Threads = 256;
+
+template <int KSW, int NGW, int ZW, int ACT, bool PLAIN>
+__global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc a) {
+    constexpr int ZS = 4 / KSW;        // plane sub-blocks per workgroup
+    constexpr int NZ = ZW + 2;         // input planes a wave streams
+    constexpr int ZB = ZW * ZS;        // output planes per workgroup
+    __shared__ __attribute__((aligned(16))) float red[4][ZW][4][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int n16 = lane & 15, kq = lane >> 4;
+    const int kpart = wave % KSW, zpart = wave / KSW;
+    const int x0 = blockIdx.x * 16;
+    const int y = blockIdx.y;
+    const int nzb = (a.Do + ZB - 1) / ZB;
+    const int b = blockIdx.z / nzb;
+    const int z0 = (blockIdx.z - b * nzb) * ZB + zpart * ZW;  // this wave's first output plane
+
+    // ---- weights of the wave's groups -> VGPRs: w[tap][cin_pad][cout_pad], tap = (dz*3 + dy)*3 + dx
+    float wv[NGW][27];
+    {
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
+        const unsigned wl = 4u * (kq * a.cout_pad + n16);
+#pragma unroll
+        for (int i = 0; i < NGW; ++i) {
+            const int g = kpart + i * KSW;
+#pragma unroll
+            for (int t = 0; t < 27; ++t)
+                wv[i][t] = buf_load_s(wrs, wl, 4 * ((t * a.cin_pad + 4 * g) * a.cout_pad));  // past cin_pad: OOB -> 0
+        }
+    }
+    // ---- input addressing (one source)
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
+        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const int xo = x0 + n16;
+    unsigned vo[NGW][3];  // group i's channel at column shift dx
+#pragma unroll
+    for (int i = 0; i < NGW; ++i) {
+        const int c = 4 * (kpart + i * KSW) + kq;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            const int xi = xo - 1 + dx;
+            vo[i][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
+        }
+    }
+    int roff[3];  // rows y - 1 .. y + 1 (kOOB outside)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+        const int yi = y - 1 + dy;
+        roff[dy] = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
+    }
+    auto load_plane = [&](float (&d)[NGW][9], int zi) {
+        const int poff = (zi >= 0 && zi < a.Di) ? 4 * zi * sd : static_cast<int>(kOOB);
+#pragma unroll
+        for (int i = 0; i < NGW; ++i)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) d[i][dy * 3 + dx] = buf_load_s(rs, vo[i][dx], poff + roff[dy]);
+    };
+
+    floatx4 acc[ZW];
+#pragma unroll
+    for (int z = 0; z < ZW; ++z) acc[z] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float bin[2][NGW][9];
+    load_plane(bin[0], z0 - 1);
+#pragma unroll
+    for (int p = 0; p < NZ; ++p) {  // input plane z0 - 1 + p feeds output planes p - dz (dz = 0..2)
+        if (p + 1 < NZ) load_plane(bin[(p + 1) & 1], z0 + p);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NGW; ++i)
+#pragma unroll
+            for (int t9 = 0; t9 < 9; ++t9)
+#pragma unroll
+                for (int dz = 0; dz < 3; ++dz) {
+                    const int zo = p - dz;
+                    if (zo < 0 || zo >= ZW) continue;
+                    acc[zo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i][dz * 9 + t9], bin[p & 1][i][t9], acc[zo], 0, 0, 0);
+                }
+    }
+
+    // ---- K-split partial sums: LDS [wave][plane][j][lane], fixed-order sum over the KSW parts
+#pragma unroll
+    for (int z = 0; z < ZW; ++z)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[wave][z][j][lane] = acc[z][j];
+    __syncthreads();
+    // thread t finishes element (plane sub-block zp, plane z, j, lane) for every (z, j) with
+    // (zp * ZW + z) * 4 + j == t >> 6 (mod 4 * ZB / 4 ... ) -- ZB * 4 * 64 elements over 256 threads
+    constexpr int NE = ZB * 4 * 64 / kW3Threads;  // elements per thread
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0),
+        4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int idx = e * kW3Threads + static_cast<int>(threadIdx.x);  // over (zp, z, j, lane)
+        const int l = idx & 63, j = (idx >> 6) & 3, zz = idx >> 8;       // zz = zp * ZW + z
+        const int zp = zz / ZW, z = zz - zp * ZW;
+        float v = red[zp * KSW][z][j][l];
+#pragma unroll
+        for (int k = 1; k < KSW; ++k) v += red[zp * KSW + k][z][j][l];
+        const int co = 4 * (l >> 4) + j, px = x0 + (l & 15);
+        const int zo = (blockIdx.z - b * nzb) * ZB + zz;
+        const float sc_ = a.scale ? a.scale[min(co, a.Cout - 1)] : 1.f;
+        const float sh_ = a.shift ? a.shift[min(co, a.Cout - 1)] : 0.f;
+        v = a.scale ? v * sc_ + sh_ : v + sh_;
+        v = act_t<ACT>(v, a.act);
+        if constexpr (PLAIN) {
+            const unsigned o = (co < a.Cout && px < a.Wo && zo < a.Do)
+                                   ? 4u * (co * static_cast<int>(a.oc) + zo * static_cast<int>(a.od) + y * static_cast<int>(a.oh) + px)
+                                   : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0, 0);
+        } else {
+            if (co >= a.Cout || px >= a.Wo || zo >= a.Do) continue;
+            if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + static_cast<long long>(y) * a.mh + px];
+            if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(zo) * a.rd + static_cast<long long>(y) * a.rh + px];
+            const long long o = b * a.ob + co * a.oc + static_cast<long long>(zo) * a.od + static_cast<long long>(y) * a.oh + px;
+            a.out[o] = v * a.post_scale;
+            if (a.out2) a.out2[o] = v * a.post_scale2;
+        }
+    }
+}
+
+template <int KSW, int NGW, int ZW>
+int launch_w3(const esm_conv_desc& a, hipStream_t s) {
+    constexpr int ZB = ZW * (4 / KSW);
+    const long long z = static_cast<long long>(a.B) * ((a.Do + ZB - 1) / ZB);
+    if (a.Ho > 65535 || z > 65535) return arg_error("conv(wide3): grid too large");
+    const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(a.Ho), static_cast<unsigned>(z));
+    const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
+                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
+                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (plain)
+        hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true>), grid, dim3(kW3Threads), 0, s, a);
+    else
+        hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false>), grid, dim3(kW3Threads), 0, s, a);
+    return check_launch("conv(wide3)");
+}
+
+}  // namespace
+
+// 3x3x3 stride-1 padding-1 3-D convs with <= 16 couts over one source (plain or `* mul` / residual
+// epilogues), input channels up to 32.
+bool wide3_ok(const esm_conv_desc& a) {
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    if (!d3 || a.transposed || a.stride != 1 || a.kd != 3 || a.kh != 3 || a.kw != 3) return false;
+    if (a.pd != 1 || a.ph != 1 || a.pw != 1 || a.nsrc != 1 || a.Cout > 16 || a.Cin > 32 || a.up || a.shuffle > 1)
+        return false;
+    return direct_ok(a);
+}
+
+int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
+    if (!wide3_ok(a)) return arg_error("conv: wide3-form hint not applicable");
+    const int ng = (a.Cin + 3) / 4;
+    // plane blocks: 4 planes per wave where the grid stays wide, else 2
+    const long long rows = static_cast<long long>(a.B) * a.Ho * ceil_div(a.Wo, 16);
+    if (ng > 4) {  // 5..8 groups: 4 waves split K, 2 groups each
+        return rows * a.Do >= 4LL * 16384 ? launch_w3<4, 2, 4>(a, s) : launch_w3<4, 2, 2>(a, s);
+    }
+    if (ng > 2) return launch_w3<4, 1, 2>(a, s);  // 3..4 groups: one each
+    if (ng == 2) return rows * a.Do >= 4LL * 16384 ? launch_w3<2, 1, 4>(a, s) : launch_w3<2, 1, 2>(a, s);
+    return rows * a.Do >= 4LL * 16384 ? launch_w3<1, 1, 4>(a, s) : launch_w3<1, 1, 2>(a, s);
+}
+
+}  // namespace conv
+}  // namespace esm

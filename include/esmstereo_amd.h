@@ -119,7 +119,11 @@ typedef struct {
                      SMALL << 21: the lean K-split form for latency-bound layers (conv_small.hip;
                      plain epilogues: no mul / up / shuffle) |
                      WIDE << 22: register-resident-weight row-streaming form (conv_wide.hip; 2-D, stride 1,
-                     k1 / k3, one source, Cout <= 32, plain epilogues) */
+                     k1 / k3, one source, Cout <= 32, plain epilogues) |
+                     WIDE3 << 24: register-weight plane-streaming form for 3x3x3 s1 p1 3-D convs with <= 16 couts
+                     and <= 32 input channels (conv_wide3.hip; plain, `* mul` and residual epilogues).
+                     Bit 23 is read from a PAIR's first descriptor: the LDS-weight pair kernel instead of the lean
+                     1x1 -> 3x3 form (A/B measurements) */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;

@@ -26,5 +26,10 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpur
     python3 scripts/gwc_ring.py > gpurun_out/pmc_gwc_f.log 2>&1 || stop pmc_fetch $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/pmc_gwc_w" -o w -- \
     python3 scripts/gwc_ring.py > gpurun_out/pmc_gwc_w.log 2>&1 || stop pmc_write $?
-tail -1 gpurun_out/pmc_gwc_f.log
+# gwc_ring.py: L-K ring (3 fill + 24 timed launches), then configs[2] (2 fill + 8 timed), then concat
+python3 scripts/pmc_kernel_avg.py gpurun_out/pmc_gwc_f gpurun_out/pmc_gwc_w gwc_kernel "gwc ring B1 96x312 D48" \
+    gwc_volume 199360512 gpurun_out/pmc_traffic_gwc.json 3 24
+python3 scripts/pmc_kernel_avg.py gpurun_out/pmc_gwc_f gpurun_out/pmc_gwc_w gwc_kernel "gwc ring B8 136x240 D48" \
+    gwc_volume 1738014720 gpurun_out/pmc_traffic_gwc.json 29 8
+rm -rf gpurun_out/pmc_gwc_f gpurun_out/pmc_gwc_w
 exit 0

@@ -24,7 +24,7 @@ __device__ __forceinline__ float row_shift(float v) {
 }
 
 // PF: input rows loaded ahead (1 = next row only; NR = all rows up front); DPP: 1 load + 2 row shifts
-template <int R, int PF, bool GELU, bool DPP>
+template <int R, int PF, bool GELU, bool DPP, int PIPE = 0>
 __global__ void __launch_bounds__(256) k3(const float* x, const float* w, float* out) {
     constexpr int NR = R + 2;
     constexpr int VALID = DPP ? 14 : 16;
@@ -84,15 +84,38 @@ __global__ void __launch_bounds__(256) k3(const float* x, const float* w, float*
                     acc[ro] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[dy * 3 + dx][g], bv, acc[ro], 0, 0, 0);
                 }
             }
-        const int rf = r - 2;
-        if (rf < 0) continue;
-        const int yo = y0 + rf;
-        if (yo >= H || xo >= W || xo < 0 || (DPP && (n16 == 0 || n16 == 15))) continue;
+        // PIPE: the epilogue of the row completed one iteration earlier runs here, after this row's
+        // MFMAs were issued (same basic block: the scheduler may fill the MFMA gaps with it)
+        const int rf = PIPE ? r - 3 : r - 2;
+        if (rf >= 0) {
+            const int yo = y0 + rf;
+            if (!(yo >= H || xo >= W || xo < 0 || (DPP && (n16 == 0 || n16 == 15)))) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float v = acc[rf][j] * 1.01f + 0.01f;
-            if constexpr (GELU) v = esm::gelu_erf(v);
-            out[(4 * kq + j) * H * W + yo * W + xo] = v;
+                for (int j = 0; j < 4; ++j) {
+                    float v = acc[rf][j] * 1.01f + 0.01f;
+                    if constexpr (GELU) v = esm::gelu_erf(v);
+                    out[(4 * kq + j) * H * W + yo * W + xo] = v;
+                }
+            }
+        }
+        if constexpr (PIPE == 2) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+            }
+        }
+    }
+    if constexpr (PIPE != 0) {
+        const int rf = NR - 3;
+        const int yo = y0 + rf;
+        if (!(yo >= H || xo >= W || xo < 0)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v = acc[rf][j] * 1.01f + 0.01f;
+                if constexpr (GELU) v = esm::gelu_erf(v);
+                out[(4 * kq + j) * H * W + yo * W + xo] = v;
+            }
         }
     }
 }
@@ -129,8 +152,12 @@ int main() {
                hipLaunchKernelGGL((k3<R, PF, G, D>), dim3((W + 4 * valid - 1) / (4 * valid), (H + R - 1) / R), \
                                   dim3(256), 0, 0, x, w, o);                                                  \
            }))
-    RUN(2, 1, true, false); RUN(2, 1, false, false); RUN(2, 4, true, false); RUN(4, 1, true, false);
-    RUN(4, 6, true, false); RUN(4, 2, true, false); RUN(8, 2, true, false); RUN(1, 3, true, false);
-    RUN(2, 1, true, true); RUN(4, 1, true, true); RUN(4, 6, true, true); RUN(8, 3, true, true); RUN(4, 6, false, true);
+    RUN(2, 1, true, false); RUN(4, 2, true, false); RUN(8, 2, true, false); RUN(8, 2, false, false);
+#define RUNP(R, PF, P)                                                                                        \
+    printf("R %d prefetch %d pipe %d: %7.2f us\n", R, PF, P, timeit([&] {                                     \
+               hipLaunchKernelGGL((k3<R, PF, true, false, P>), dim3((W + 63) / 64, (H + R - 1) / R), dim3(256), 0, \
+                                  0, x, w, o);                                                                \
+           }))
+    RUNP(2, 1, 1); RUNP(4, 2, 1); RUNP(8, 2, 1); RUNP(2, 1, 2); RUNP(4, 2, 2); RUNP(8, 2, 2); RUNP(16, 2, 1); RUNP(16, 2, 2);
     return 0;
 }

@@ -297,6 +297,28 @@ def test_conv_wide_form_multisource(cins, cout, k, p, shape):
     assert rel(y, ref) < 1e-5
 
 
+HINT_WIDE3 = 1 << 24
+
+
+@pytest.mark.parametrize("cin,cout,shape,B", [(32, 8, (12, 24, 78), 1), (8, 8, (12, 24, 78), 1), (1, 8, (12, 24, 78), 2),
+                                              (32, 8, (7, 9, 37), 2), (16, 16, (5, 6, 20), 1), (24, 12, (3, 5, 17), 1),
+                                              (12, 12, (6, 12, 39), 1), (32, 8, (48, 20, 50), 1)])
+def test_conv_wide3_form(cin, cout, shape, B):
+    """3x3x3 plane-streaming form (conv_wide3.hip, hint 1 << 24) vs fp64 torch (1e-5 relative): every K split
+    (1, 2, 4 waves over the channel groups), plane blocks not dividing D, ragged widths, batch 2; plus the
+    `* att` (corr_stem of ESMStereo-S nc) and residual epilogues."""
+    conv, bn = _mk(3, cin, cout, 3, 1, 1, seed=11)
+    x = torch.randn(B, cin, *shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_WIDE3)
+    assert rel(y, ref) < 1e-5
+    att = torch.rand(B, cout, shape[1], shape[2]) + 0.5
+    res = torch.randn_like(ref)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], mul=att.to(DEV), res=res.to(DEV), hint=HINT_WIDE3)
+    assert rel(y, _ref_conv([x], conv, bn, ACT_GELU, mul=att, res=res)) < 1e-5
+
+
 def test_conv_small_form_epilogues():
     """Residual, post_scale and the second scaled copy in the small form; `* mul` / bilinear add /
     PixelShuffle are refused (the launcher falls back to the general forms for them)."""
