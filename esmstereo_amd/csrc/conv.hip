@@ -20,6 +20,8 @@ bool wide_ok(const esm_conv_desc& a);                    // conv_wide.hip
 int launch_wide(const esm_conv_desc& a, hipStream_t s);  // conv_wide.hip
 bool wide3_ok(const esm_conv_desc& a);                    // conv_wide3.hip
 int launch_wide3(const esm_conv_desc& a, hipStream_t s);  // conv_wide3.hip
+bool widet_ok(const esm_conv_desc& a);                    // conv_widet.hip
+int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
@@ -29,6 +31,7 @@ constexpr int kHintC1in = 1 << 20;     // force the VALU single-input-channel fo
 constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound layers (conv_small.hip)
 constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
 constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
+constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 form, all 4 classes per wave (conv_widet.hip)
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -61,6 +64,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
             return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
         if (a.Ho != 2 * a.Hi || a.Wo != 2 * a.Wi || (d3 && a.Do != 2 * a.Di))
             return arg_error("conv: transposed output extent must be 2x the input");
+        if (a.hint & kHintWideT) return conv::launch_widet(a, s);
         if ((a.hint & kHintSmall) || (a.hint == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
     }

@@ -11,7 +11,8 @@
 // of the three output planes zi + 1, zi, zi - 1 (tap plane dz = 0, 1, 2), so a loaded operand is
 // used three times and consecutive MFMAs go to different planes' accumulators.  The loop over input
 // planes is unrolled (compile-time Z) and only (input, output) plane pairs inside the block are
-// multiplied.  The waves' partial tiles meet in LDS at the end and are added in a fixed order
+// multiplied.  With <= 8 couts the 16 MFMA rows carry two output planes (a plane pair), so no row
+// is padding.  The waves' partial tiles meet in LDS at the end and are added in a fixed order
 // (deterministic); every thread then finishes its (plane, cout, pixel) elements.
 #include "conv_direct.h"
 
@@ -21,12 +22,17 @@ namespace {
 
 constexpr int kW3Threads = 256;
 
-template <int KSW, int NGW, int ZW, int ACT, bool PLAIN>
+template <int KSW, int NGW, int ZW, int ACT, bool PLAIN, bool PZ>
 __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc a) {
     constexpr int ZS = 4 / KSW;        // plane sub-blocks per workgroup
     constexpr int NZ = ZW + 2;         // input planes a wave streams
     constexpr int ZB = ZW * ZS;        // output planes per workgroup
-    __shared__ __attribute__((aligned(16))) float red[4][ZW][4][64];
+    // PZ (<= 8 couts): the 16 MFMA rows hold 8 couts x 2 output planes (a plane pair 2q, 2q + 1), so
+    // no row is padding.  Input plane z0 - 1 + p reaches pair q through relative plane r = p - 2q in
+    // 0..3: rows 0-7 use tap plane dz = r (if <= 2), rows 8-15 dz = r - 1 (if >= 0); 4 weight sets
+    constexpr int NA = PZ ? ZW / 2 : ZW;  // accumulators (pairs or planes)
+    static_assert(!PZ || ZW % 2 == 0, "plane pairs need an even plane block");
+    __shared__ __attribute__((aligned(16))) float red[4][NA][4][64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
@@ -38,17 +44,25 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
     const int z0 = (blockIdx.z - b * nzb) * ZB + zpart * ZW;  // this wave's first output plane
 
     // ---- weights of the wave's groups -> VGPRs: w[tap][cin_pad][cout_pad], tap = (dz*3 + dy)*3 + dx
-    float wv[NGW][27];
+    constexpr int NWS = PZ ? 4 : 3;  // weight sets: tap planes dz (or the pair-relative planes r)
+    float wv[NGW][NWS][9];
     {
         const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
-        const unsigned wl = 4u * (kq * a.cout_pad + n16);
+        const unsigned wl = 4u * (kq * a.cout_pad + (PZ ? (n16 & 7) : n16));
 #pragma unroll
         for (int i = 0; i < NGW; ++i) {
             const int g = kpart + i * KSW;
 #pragma unroll
-            for (int t = 0; t < 27; ++t)
-                wv[i][t] = buf_load_s(wrs, wl, 4 * ((t * a.cin_pad + 4 * g) * a.cout_pad));  // past cin_pad: OOB -> 0
+            for (int r = 0; r < NWS; ++r)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    int dz = r;
+                    if constexpr (PZ) dz = n16 < 8 ? r : r - 1;  // per-lane: rows 8-15 lag one plane
+                    const bool ok = dz >= 0 && dz <= 2;
+                    const float v = buf_load_s(wrs, ok ? wl : kOOB, 4 * (((ok ? dz : 0) * 9 + t) * a.cin_pad + 4 * g) * a.cout_pad);
+                    wv[i][r][t] = v;  // past cin_pad or an invalid plane: out of range -> 0
+                }
         }
     }
     // ---- input addressing (one source)
@@ -84,13 +98,13 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
                 for (int dx = 0; dx < 3; ++dx) d[i][dy * 3 + dx] = buf_load_s(rs, vo[i][dx], poff + roff[dy]);
     };
 
-    floatx4 acc[ZW];
+    floatx4 acc[NA];
 #pragma unroll
-    for (int z = 0; z < ZW; ++z) acc[z] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < NA; ++z) acc[z] = floatx4{0.f, 0.f, 0.f, 0.f};
     float bin[2][NGW][9];
     load_plane(bin[0], z0 - 1);
 #pragma unroll
-    for (int p = 0; p < NZ; ++p) {  // input plane z0 - 1 + p feeds output planes p - dz (dz = 0..2)
+    for (int p = 0; p < NZ; ++p) {  // input plane z0 - 1 + p
         if (p + 1 < NZ) load_plane(bin[(p + 1) & 1], z0 + p);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -98,36 +112,45 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
 #pragma unroll
             for (int t9 = 0; t9 < 9; ++t9)
 #pragma unroll
-                for (int dz = 0; dz < 3; ++dz) {
-                    const int zo = p - dz;
-                    if (zo < 0 || zo >= ZW) continue;
-                    acc[zo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i][dz * 9 + t9], bin[p & 1][i][t9], acc[zo], 0, 0, 0);
+                for (int k = 0; k < (PZ ? 2 : 3); ++k) {
+                    if constexpr (PZ) {  // pairs q with r = p - 2q in 0..3
+                        const int q = p / 2 - k;
+                        const int r = p - 2 * q;
+                        if (q < 0 || q >= NA || r > 3) continue;
+                        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i][r][t9], bin[p & 1][i][t9], acc[q], 0, 0, 0);
+                    } else {  // output planes p - dz
+                        const int zo = p - k;
+                        if (zo < 0 || zo >= ZW) continue;
+                        acc[zo] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i][k][t9], bin[p & 1][i][t9], acc[zo], 0, 0, 0);
+                    }
                 }
     }
 
-    // ---- K-split partial sums: LDS [wave][plane][j][lane], fixed-order sum over the KSW parts
+    // ---- K-split partial sums: LDS [wave][acc][j][lane], fixed-order sum over the KSW parts
 #pragma unroll
-    for (int z = 0; z < ZW; ++z)
+    for (int z = 0; z < NA; ++z)
 #pragma unroll
         for (int j = 0; j < 4; ++j) red[wave][z][j][lane] = acc[z][j];
     __syncthreads();
-    // thread t finishes element (plane sub-block zp, plane z, j, lane) for every (z, j) with
-    // (zp * ZW + z) * 4 + j == t >> 6 (mod 4 * ZB / 4 ... ) -- ZB * 4 * 64 elements over 256 threads
-    constexpr int NE = ZB * 4 * 64 / kW3Threads;  // elements per thread
+    // elements (plane sub-block zp, accumulator z, j, lane) over the 256 threads, lane fastest
+    constexpr int NE = ZS * NA * 4 * 64 / kW3Threads;  // elements per thread
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
         4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
         0x00020000);
+    const int zbase = (blockIdx.z - b * nzb) * ZB;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         const int idx = e * kW3Threads + static_cast<int>(threadIdx.x);  // over (zp, z, j, lane)
-        const int l = idx & 63, j = (idx >> 6) & 3, zz = idx >> 8;       // zz = zp * ZW + z
-        const int zp = zz / ZW, z = zz - zp * ZW;
+        const int l = idx & 63, j = (idx >> 6) & 3, zz = idx >> 8;       // zz = zp * NA + z (= e)
+        const int zp = zz / NA, z = zz - zp * NA;
         float v = red[zp * KSW][z][j][l];
 #pragma unroll
         for (int k = 1; k < KSW; ++k) v += red[zp * KSW + k][z][j][l];
-        const int co = 4 * (l >> 4) + j, px = x0 + (l & 15);
-        const int zo = (blockIdx.z - b * nzb) * ZB + zz;
+        const int row = 4 * (l >> 4) + j;                      // MFMA row of the element
+        const int co = PZ ? (row & 7) : row;
+        const int zo = zbase + zp * ZW + (PZ ? 2 * z + (row >> 3) : z);
+        const int px = x0 + (l & 15);
         const float sc_ = a.scale ? a.scale[min(co, a.Cout - 1)] : 1.f;
         const float sh_ = a.shift ? a.shift[min(co, a.Cout - 1)] : 0.f;
         v = a.scale ? v * sc_ + sh_ : v + sh_;
@@ -157,10 +180,17 @@ int launch_w3(const esm_conv_desc& a, hipStream_t s) {
     const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
-    if (plain)
-        hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true>), grid, dim3(kW3Threads), 0, s, a);
-    else
-        hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false>), grid, dim3(kW3Threads), 0, s, a);
+    if (a.Cout <= 8) {  // plane pairs: no padding MFMA rows
+        if (plain)
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, true>), grid, dim3(kW3Threads), 0, s, a);
+        else
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, true>), grid, dim3(kW3Threads), 0, s, a);
+    } else {
+        if (plain)
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, false>), grid, dim3(kW3Threads), 0, s, a);
+        else
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, false>), grid, dim3(kW3Threads), 0, s, a);
+    }
     return check_launch("conv(wide3)");
 }
 
@@ -181,8 +211,10 @@ int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
     const int ng = (a.Cin + 3) / 4;
     // plane blocks: 4 planes per wave where the grid stays wide, else 2
     const long long rows = static_cast<long long>(a.B) * a.Ho * ceil_div(a.Wo, 16);
-    if (ng > 4) {  // 5..8 groups: 4 waves split K, 2 groups each
-        return rows * a.Do >= 4LL * 16384 ? launch_w3<4, 2, 4>(a, s) : launch_w3<4, 2, 2>(a, s);
+    const long long vox = rows * a.Do;
+    if (ng > 4) {  // 5..8 groups: 4 waves split K, 2 groups each; more planes per wave on big volumes
+        if (vox >= 16LL * 65536) return launch_w3<4, 2, 8>(a, s);
+        return vox >= 4LL * 16384 ? launch_w3<4, 2, 4>(a, s) : launch_w3<4, 2, 2>(a, s);
     }
     if (ng > 2) return launch_w3<4, 1, 2>(a, s);  // 3..4 groups: one each
     if (ng == 2) return rows * a.Do >= 4LL * 16384 ? launch_w3<2, 1, 4>(a, s) : launch_w3<2, 1, 2>(a, s);

@@ -319,6 +319,27 @@ def test_conv_wide3_form(cin, cout, shape, B):
     assert rel(y, _ref_conv([x], conv, bn, ACT_GELU, mul=att, res=res)) < 1e-5
 
 
+HINT_WIDET = 1 << 25
+
+
+@pytest.mark.parametrize("cin,cout,shape,B", [(16, 16, (96, 312), 1), (16, 16, (12, 39), 2), (16, 16, (48, 156), 1),
+                                              (8, 16, (23, 45), 2), (4, 24, (17, 70), 1), (16, 1, (19, 33), 1)])
+def test_conv_widet_form(cin, cout, shape, B):
+    """ConvTranspose2d k4 s2 p1 in the all-classes-per-wave form (conv_widet.hip, hint 1 << 25) vs fp64 torch
+    (1e-5 relative): ragged strips and rows, two cout tiles, batch 2, the 1-cout refinement head with the residual
+    epilogue path."""
+    conv, bn = _mk(2, cin, cout, 4, 2, 1, transposed=True, seed=12, bn=cout > 1)
+    act = ACT_GELU if cout > 1 else ACT_NONE
+    x = torch.randn(B, cin, *shape)
+    ref = _ref_conv([x], conv, bn, act)
+    p = pk(conv, bn, act)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_WIDET)
+    assert rel(y, ref) < 1e-5
+    res = torch.randn_like(ref)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), post_scale=4.0, hint=HINT_WIDET)
+    assert rel(y, _ref_conv([x], conv, bn, act, res=res, post=4.0)) < 1e-5
+
+
 def test_conv_small_form_epilogues():
     """Residual, post_scale and the second scaled copy in the small form; `* mul` / bilinear add /
     PixelShuffle are refused (the launcher falls back to the general forms for them)."""
