@@ -102,6 +102,7 @@ SIGNATURES = {
     "esm_plan_num_ops": (c_int, [c_void_p]),
     "esm_plan_op_kind": (c_int, [c_void_p, c_int]),
     "esm_plan_set_conv_hint": (c_int, [c_void_p, c_int, c_int]),
+    "esm_plan_set_repeat": (c_int, [c_void_p, c_int, c_int]),
     "esm_plan_run": (c_int, [c_void_p, c_void_p]),
     "esm_plan_run_op": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "esm_plan_graph_build": (c_int, [c_void_p, c_void_p]),

@@ -60,8 +60,22 @@ __device__ __forceinline__ float gelu_erf(float x) {
     return x * 0.5f * (1.0f + erf_bf(x * 0.70710678118654752440f));
 }
 
+// f(integral_constant<int, I>) for I = B .. E-1, unrolled at compile time (ring-buffer indices
+// inside runtime loops over ring periods)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // SiLU as nn.SiLU: x / (1 + exp(-x))
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+
+// SiLU with the hardware exp2 / reciprocal (a few ulp): per-pixel chains where the libm forms'
+// division and exp sequences dominate the instruction count (smix, shuffle_tail)
+__device__ __forceinline__ float silu_fast(float x) { return __fdividef(x, 1.0f + __expf(-x)); }
 
 __device__ __forceinline__ float apply_act(float v, int act) {
     switch (act) {

@@ -61,6 +61,7 @@ struct Op {
     esm_shuffle_tail_desc st{};
     VolArgs vol{};
     RegArgs reg{};
+    int repeat = 1;  // launches per replay (esm_plan_set_repeat: 0 drops the op, 2 doubles it)
 };
 
 int run_op(const Op& op, hipStream_t s) {
@@ -167,8 +168,10 @@ struct esm_plan {
                     return ESM_ERR_RUNTIME;
                 }
             }
-            const int rc = run_op(ops[i], s);
-            if (rc != ESM_OK) return rc;
+            for (int r = 0; r < ops[i].repeat; ++r) {
+                const int rc = run_op(ops[i], s);
+                if (rc != ESM_OK) return rc;
+            }
             if (i == probe_index && slot >= 0) {
                 const hipError_t e = hipEventRecordWithFlags(ev1[slot], s, flags);
                 if (e != hipSuccess) {
@@ -306,6 +309,17 @@ int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint) {
     return prev;
 }
 
+int esm_plan_set_repeat(esm_plan* plan, int index, int repeat) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (index < 0 || index >= static_cast<int>(plan->ops.size())) return esm::arg_error("plan: op index out of range");
+    if (repeat < 0 || repeat > 8) return esm::arg_error("plan: repeat must be 0..8");
+    if (repeat == 0 && index == plan->probe_index) return esm::arg_error("plan: cannot drop the probed op");
+    plan->clear_graph();
+    const int prev = plan->ops[index].repeat;
+    plan->ops[index].repeat = repeat;
+    return prev;
+}
+
 int esm_plan_run(esm_plan* plan, void* stream) {
     if (!plan) return esm::arg_error("plan: null");
     return plan->launch_all(esm::as_stream(stream), next_slot(plan));
@@ -341,7 +355,7 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
     int rc = ESM_OK;
     for (int i = 0; i < static_cast<int>(plan->ops.size()) && rc == ESM_OK; ++i) {
         if (i == plan->probe_index) before = capture_frontier(plan->cap_stream);
-        rc = run_op(plan->ops[i], plan->cap_stream);
+        for (int r = 0; r < plan->ops[i].repeat && rc == ESM_OK; ++r) rc = run_op(plan->ops[i], plan->cap_stream);
         if (i == plan->probe_index) after = capture_frontier(plan->cap_stream);
     }
     hipGraph_t g = nullptr;

@@ -18,9 +18,6 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// SiLU with the hardware exp2 / reciprocal (a few ulp; the unfused epilogue uses the libm forms)
-__device__ __forceinline__ float silu_fast(float x) { return __fdividef(x, 1.0f + __expf(-x)); }
-
 template <int NF, int R, int TH, int kTW>
 struct StGeo {
     static constexpr int LRH = TH / R + 2;  // low-res rows under tile + halo

@@ -42,17 +42,19 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict
         var += dv * dv;
     }
     var = var / static_cast<float>(C);
-    const float den = sqrtf(var + 1e-5f);
+    // (t - mu) / sqrt(var + eps) as a multiply by the hardware reciprocal square root (1 ulp): the C
+    // IEEE divisions of the libm form were most of the per-pixel chain (profiles/r02_pmc_sq_ops_SK.txt)
+    const float inv = __builtin_amdgcn_rsqf(var + 1e-5f);
     float n[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) / den * w[Lyt::LN + c];
+    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) * inv * w[Lyt::LN + c];
     float h[C];
 #pragma unroll
     for (int j = 0; j < C; ++j) {
         float s = w[Lyt::F0B + j];
 #pragma unroll
         for (int i = 0; i < H2; ++i) s += w[Lyt::F0W + j * H2 + i] * n[i];
-        h[j] = silu(s);
+        h[j] = silu_fast(s);
     }
     float cat[C];
 #pragma unroll

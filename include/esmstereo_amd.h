@@ -254,6 +254,10 @@ int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */
 int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint);
+/* Diagnostics: launch op `index` `repeat` times per replay (0..8; 0 drops it, so the step time
+ * minus the dropped step time is the op's marginal cost in the chain, gaps included).  Returns the
+ * previous count; drops a built graph.  Results of a plan with a dropped op are not meaningful. */
+int esm_plan_set_repeat(esm_plan* plan, int index, int repeat);
 int esm_plan_run(esm_plan* plan, void* stream);
 /* Launch op `index` alone, `reps` times back to back on `stream` (timing one kernel of the
  * path with a single hipEvent pair around the batch; the op's buffers are the plan's own). */
