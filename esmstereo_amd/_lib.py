@@ -18,7 +18,8 @@ HEADER_PATH = os.path.join(ROOT, "include", "esmstereo_amd.h")
 MAX_SRC = 3
 SMIX_MAX_STAGES = 2
 
-ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU = 0, 1, 2, 3
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3, 4
+CONF_COST_FEATURES, CONF_ATTEND, CONF_ENLARGE, CONF_COMBINE, CONF_SIGMOID = 1, 2, 3, 4, 5
 
 
 class EsmSrc(Structure):
@@ -71,6 +72,11 @@ class EsmShuffleTailDesc(Structure):
                 ("reserved", c_int32)]
 
 
+class EsmConfDesc(Structure):
+    _fields_ = [("op", c_int32), ("B", c_int32), ("C", c_int32), ("D", c_int32), ("H", c_int32), ("W", c_int32),
+                ("x", c_void_p * 4), ("out", c_void_p)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/esmstereo_amd.h
 SIGNATURES = {
     "esm_last_error": (ctypes.c_char_p, []),
@@ -85,6 +91,7 @@ SIGNATURES = {
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
     "esm_fmnet_f32": (c_int, [POINTER(EsmFmnetDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
+    "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
     "esm_conv_pair_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
@@ -99,6 +106,7 @@ SIGNATURES = {
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_regression": (c_int, [c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 4),
+    "esm_plan_add_conf": (c_int, [c_void_p, POINTER(EsmConfDesc)]),
     "esm_plan_num_ops": (c_int, [c_void_p]),
     "esm_plan_op_kind": (c_int, [c_void_p, c_int]),
     "esm_plan_set_conv_hint": (c_int, [c_void_p, c_int, c_int]),
@@ -126,7 +134,8 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc, EsmShuffleTailDesc, EsmFmnetDesc)):
+    for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc, EsmShuffleTailDesc, EsmFmnetDesc,
+                                    EsmConfDesc)):
         if lib.esm_struct_size(which) != ctypes.sizeof(st):
             raise ImportError(f"esmstereo_amd: ABI mismatch for {st.__name__}: "
                               f"C {lib.esm_struct_size(which)} vs ctypes {ctypes.sizeof(st)}")

@@ -17,6 +17,7 @@ int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
 int launch_fmnet(const esm_fmnet_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
+int launch_conf(const esm_conf_desc*, hipStream_t);
 namespace conv {
 int launch_conv_pair(const esm_conv_desc*, const esm_conv_desc*, hipStream_t);
 }
@@ -34,7 +35,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8, kFmnet = 9 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8, kFmnet = 9, kConf = 10 };
 
 struct VolArgs {
     const float* L;
@@ -61,6 +62,7 @@ struct Op {
     esm_shuffle_tail_desc st{};
     VolArgs vol{};
     RegArgs reg{};
+    esm_conf_desc cf{};
     int repeat = 1;  // launches per replay (esm_plan_set_repeat: 0 drops the op, 2 doubles it)
 };
 
@@ -71,6 +73,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kFmnet: return esm::launch_fmnet(&op.fm, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
         case kConvPair: return esm::conv::launch_conv_pair(&op.conv, &op.conv2, s);
+        case kConf: return esm::launch_conf(&op.cf, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
                                    op.vol.D, op.vol.G, s);
@@ -198,6 +201,7 @@ int esm_struct_size(int which) {
         case 3: return static_cast<int>(sizeof(esm_smix_desc));
         case 4: return static_cast<int>(sizeof(esm_shuffle_tail_desc));
         case 5: return static_cast<int>(sizeof(esm_fmnet_desc));
+        case 6: return static_cast<int>(sizeof(esm_conf_desc));
         default: return -1;
     }
 }
@@ -281,6 +285,14 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
     Op op;
     op.kind = kRegression;
     op.reg = RegArgs{kind, cost, out, B, D, H, W};
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc) {
+    if (!desc) return esm::arg_error("plan: null conf descriptor");
+    Op op;
+    op.kind = kConf;
+    op.cf = *desc;
     return add_op(plan, std::move(op));
 }
 

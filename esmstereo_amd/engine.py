@@ -22,9 +22,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, ACT_SILU, EsmConvDesc, EsmShuffleTailDesc, EsmSmixDesc, check, lib
+from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleTailDesc,
+                   EsmSmixDesc, check, lib)
 
-__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "run_conv_pair", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU"]
+__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "run_conv_pair", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU",
+           "ACT_SIGMOID"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -291,6 +293,25 @@ class Ctx:
         else:
             check(lib.esm_normcorr_volume_f32(L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C, H, W, D,
                                               self.stream), "normcorr")
+
+    def conf(self, op: int, xs: Sequence[Optional[torch.Tensor]], out: torch.Tensor, B: int, C: int, D: int, H: int,
+             W: int, name: str = "conf") -> None:
+        """One per-pixel stage of the confidence head (esm_conf_f32; contiguous NCHW operands)."""
+        for t in list(xs) + [out]:
+            if t is not None and not t.is_contiguous():
+                raise ValueError(f"{name}: confidence-head operands must be contiguous")
+        d = EsmConfDesc()
+        d.op, d.B, d.C, d.D, d.H, d.W = op, B, C, D, H, W
+        for i, t in enumerate(xs):
+            d.x[i] = t.data_ptr() if t is not None else None
+        d.out = out.data_ptr()
+        nbytes = 4 * (sum(t.numel() for t in xs if t is not None) + out.numel())
+        self.meta.append(dict(name=name, kind="conf", flops=0, bytes=nbytes, reads=_spans(*xs), writes=_spans(out)))
+        if self.plan:
+            self.hold(*xs, out)
+            check(lib.esm_plan_add_conf(self.plan, ctypes.byref(d)), name)
+        else:
+            check(lib.esm_conf_f32(ctypes.byref(d), self.stream), name)
 
     def regression(self, kind, cost, out, B, D, H, W, samples=None) -> None:
         self.meta.append(dict(name="regression_topk2" if kind else "disparity_regression", kind="regression",

@@ -37,7 +37,7 @@ from .backbone import Feature
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
 from .engine import Ctx, GWC_STEM_ENABLED, gwc_stem_supported, param_token, require_device, run_gwc_stem
 
-__all__ = ["ESMStereo", "ESMStereo_trt", "FeatUp", "HotPath"]
+__all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath"]
 
 
 class FeatUp(nn.Module):
@@ -246,6 +246,9 @@ class ESMStereo(nn.Module):
     # ------------------------------------------------------------------ forward pieces
     def prefix(self, left: torch.Tensor, right: torch.Tensor):
         """Backbone side, reference lines 640-697 -> (match_left, match_right, att, upsampler feats)."""
+        return self._prefix(left, right)[:4]
+
+    def _prefix(self, left: torch.Tensor, right: torch.Tensor):
         vs = self.vol_size
         fl = self.feature(left)
         fr = self.feature(right)
@@ -266,7 +269,7 @@ class ESMStereo(nn.Module):
             up = [fl[2], fl[1], fl[0], sx]
         else:
             up = [fl[2], self.conv_f2(fl[3]), fl[1], self.conv_f0(fl[0])]
-        return ml, mr, att, up
+        return ml, mr, att, up, fl
 
     def _emit_hot(self, ctx: Ctx, ml: torch.Tensor, mr: torch.Tensor, att: Optional[torch.Tensor],
                   up: Sequence[torch.Tensor], train_status: bool) -> List[torch.Tensor]:
@@ -302,11 +305,19 @@ class ESMStereo(nn.Module):
         ctx.regression(1 if vs == 4 else 0, cost.view(B, D, h, w), init, B, D, h, w)
         outs = self.upsample_module.emit(ctx, up, init, final_scale=4.0,
                                          scaled_copies=4.0 if train_status else None)
+        extra = self._emit_extra(ctx, cost.view(B, D, h, w), init, ml, up)
+        if extra:
+            return [outs[0].view(B, outs[0].shape[-2], outs[0].shape[-1])] + extra
         if train_status:
             finals, copies = outs
             return [finals[0].view(B, finals[0].shape[-2], finals[0].shape[-1])] + \
                    [c.view(B, c.shape[-2], c.shape[-1]) for c in copies]
         return [outs[0].view(B, outs[0].shape[-2], outs[0].shape[-1])]
+
+    def _emit_extra(self, ctx: Ctx, cost: torch.Tensor, init: torch.Tensor, ml: torch.Tensor,
+                    up: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+        """Heads that read the hot path's intermediates (ESMStereo_confidence); none here."""
+        return []
 
     def hot_path(self, ml: torch.Tensor, mr: torch.Tensor, att: Optional[torch.Tensor], up: Sequence[torch.Tensor],
                  train_status: bool = False) -> List[torch.Tensor]:
@@ -349,3 +360,53 @@ class ESMStereo_trt(ESMStereo):
 
     def forward(self, left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
         return super().forward(left, right, False)[0]
+
+
+class ESMStereo_confidence(ESMStereo):
+    """ESMStereo with the LAFNet confidence head (reference ``models/ESMStereo_confidence.py:746-974``).
+
+    Same constructor as the reference (``device`` is accepted; tensors follow the module), the
+    :class:`ESMStereo` module tree plus ``confidence_net = LAFNet_ESM(16)`` for ``cv_scale=16`` (the
+    only scale the reference builds it for, ``:915-916``), and ``forward(left, right) -> (disp * 4,
+    confidence)`` (``:974``).  The head is emitted into the same compiled plan as the hot path: it
+    reads the aggregated cost, ``init_pred`` and ``match_left`` in place (``:972``)."""
+
+    def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
+                 backbone: str = "efficientnet_b2", cv_scale: int = 4, device=None, *, feature_cls=None) -> None:
+        super().__init__(maxdisp, gwc, norm_correlation, backbone, cv_scale, feature_cls=feature_cls)
+        self.device = device
+        if cv_scale == 16:
+            from .confidence import LAFNet_ESM
+            self.confidence_net = LAFNet_ESM(16)
+            for name, mod in self.confidence_net.named_modules():
+                object.__setattr__(mod, "_esm_name", "confidence_net" + ("." + name if name else ""))
+
+    def _hot_param_token(self) -> tuple:
+        tok = super()._hot_param_token()
+        net = getattr(self, "confidence_net", None)
+        return tok + (param_token(*net.modules()) if net is not None else ())
+
+    def prefix(self, left: torch.Tensor, right: torch.Tensor):
+        """As :meth:`ESMStereo.prefix`, with features_left[3] appended to the upsampler features
+        (the confidence head's ``left_f1x``, ``:972``)."""
+        ml, mr, att, up, fl = self._prefix(left, right)
+        if self.vol_size == 16:
+            up = list(up) + [fl[3]]
+        return ml, mr, att, up
+
+    def _emit_extra(self, ctx: Ctx, cost: torch.Tensor, init: torch.Tensor, ml: torch.Tensor,
+                    up: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+        net = getattr(self, "confidence_net", None)
+        if net is None:
+            return []
+        B = int(cost.shape[0])
+        # confidence_net(cost.squeeze(1), init_pred, match_left, features_left[3], features_left[1]) (:972)
+        conf = net.emit(ctx, cost, init, ml, up[4], up[2])
+        return [conf.view(B, conf.shape[-2], conf.shape[-1])]
+
+    def forward(self, left: torch.Tensor, right: torch.Tensor):  # type: ignore[override]
+        if self.vol_size != 16:
+            # the reference returns conf_out, which only the cv_scale=16 branch assigns (:966-974)
+            raise UnboundLocalError("local variable 'conf_out' referenced before assignment")
+        outs = super().forward(left, right, False)
+        return outs[0], outs[1]

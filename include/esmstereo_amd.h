@@ -31,6 +31,10 @@
  *                             agg_0 / agg_1 of up_refinement (models/ESMStereo.py:214-218,228-235),
  *                             spx_* (:256-259,283-286 and twins), dmNx.1 -> dmNx.2 (:250-253),
  *                             FMBlock.conv (models/shufflemixer.py:124-131)
+ *   esm_conf_f32              the per-pixel stages of the confidence head LAFNet_ESM /
+ *                             conf_upsample (models/ESMStereo_confidence.py:511-744) between its
+ *                             convs (which run through esm_conv_f32): cost features, attention,
+ *                             the scale-driven 3x grid_sample, the softmax-weighted x4 upsample
  *   esm_plan_*                the orchestration of models/ESMStereo.py:700-745 as a native
  *                             launch list, optionally replayed as one hipGraph
  *   esm_preprocess_u8         the input side: pad to /32 + ToTensor +
@@ -58,6 +62,7 @@ extern "C" {
 #define ESM_ACT_GELU 1 /* exact erf GELU, nn.GELU() */
 #define ESM_ACT_SILU 2
 #define ESM_ACT_RELU 3
+#define ESM_ACT_SIGMOID 4 /* 1 / (1 + exp(-x)), torch.sigmoid */
 
 #define ESM_MAX_SRC 3
 
@@ -194,7 +199,8 @@ typedef struct {
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc; -1 for an unknown id. */
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc;
+ * -1 for an unknown id. */
 int esm_struct_size(int which);
 
 int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* V, int B, int C, int H, int W,
@@ -220,6 +226,31 @@ int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
  * out2.  Returns ESM_ERR_UNSUPPORTED (no launch) for a pair without a fused form: run the two convs
  * with esm_conv_f32 instead. */
 int esm_conv_pair_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
+
+/* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
+ *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D <= 64) -> out [B,7,H,W]: the 7 largest of
+ *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
+ *   ESM_CONF_ATTEND         x[0..2] = cost_x, disp_x, imag_x [B,C,H,W], x[3] = logits [B,3,H,W] ->
+ *                           out [B,3C,H,W] = cat(x_k * softmax_k(logits)) (:679-689)
+ *   ESM_CONF_ENLARGE        x[0] = feat [B,C,H,W], x[1] = scale [B,1,H,W] -> out [B,9C,H,W]: the 3x
+ *                           enlarged grid_sample(feat, grid(scale), bilinear, align_corners, zeros) of
+ *                           :691-714, stored space-to-depth (channel c*9 + 3i + j = sample (3y+i, 3x+j)),
+ *                           so embed_conv2 (k3 s3) runs as a 1x1 conv over 9C channels
+ *   ESM_CONF_COMBINE        x[0] = logits [B,9,4H,4W], x[1] = init [B,1,H,W] -> out [B,1,4H,4W] =
+ *                           sum_k softmax_k(logits) * unfold3x3(init)[k] at (Y/4, X/4) (:538-543)
+ *   ESM_CONF_SIGMOID        x[0] [B*C*H*W] -> out, torch.sigmoid (:744) */
+#define ESM_CONF_COST_FEATURES 1
+#define ESM_CONF_ATTEND 2
+#define ESM_CONF_ENLARGE 3
+#define ESM_CONF_COMBINE 4
+#define ESM_CONF_SIGMOID 5
+typedef struct {
+    int32_t op;
+    int32_t B, C, D, H, W;
+    const float* x[4];
+    float* out;
+} esm_conf_desc;
+int esm_conf_f32(const esm_conf_desc* desc, void* stream);
 
 /* img: [B, H, W, 3] uint8 RGB (PIL order); out: [B, 3, Hp, Wp] fp32.  The image lands at rows
  * [top, top+H), columns [left, left+W); pad_normalized = 1 fills the rest with normalised zeros
@@ -247,9 +278,10 @@ int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float*
                           int H, int W, int D);
 /* kind 0 = disparity_regression, 1 = regression_topk k=2 */
 int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
+int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet */
+ * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet, 10 = conf */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */
