@@ -138,15 +138,15 @@ def test_conf_upsample_stage_golden(name):
 
 def test_confidence_model_forward():
     m = MANIFEST["hot_S_gwc.npz"]
-    model = E.ESMStereo_confidence(m["maxdisp"], True, False, m["backbone"], m["cv_scale"], feature_cls=StubFeature)
+    maxdisp = 192  # topk(7) over D = maxdisp / 16 needs D >= 7 (the fixture's maxdisp 64 gives D = 4)
+    model = E.ESMStereo_confidence(maxdisp, True, False, m["backbone"], m["cv_scale"], feature_cls=StubFeature)
     spec = load_spec(m["spec"])
     sd = seeded_state(spec, m["seed"])
     conf_sd = seeded_state(load_spec("spec_conf.json"), 77)
     sd.update({"confidence_net." + k: v for k, v in conf_sd.items()})
     model.load_state_dict(sd)
     model = model.eval().to(DEV)
-    g = load_golden("hot_S_gwc.npz")
-    left, right = cu(g["left"]), cu(g["right"])
+    left, right = (t.to(DEV) for t in stereo_pair(1, 128, 320, 5, max_shift=40))
     with torch.no_grad():
         disp, conf = model(left, right)
         ml, mr, att, up = model.prefix(left, right)
@@ -158,12 +158,21 @@ def test_confidence_model_forward():
     cpu = lambda t: t.detach().float().cpu()  # noqa: E731
     sd_cpu = {k: v.float() for k, v in sd.items() if v.is_floating_point()}
     with torch.no_grad():
-        inter = O.hot_path(sd_cpu, 16, m["maxdisp"], True, cpu(ml), cpu(mr), cpu(att), [cpu(u) for u in up[:4]])
+        inter = O.hot_path(sd_cpu, 16, maxdisp, True, cpu(ml), cpu(mr), cpu(att), [cpu(u) for u in up[:4]])
         ref = CO.lafnet(sd_cpu, "confidence_net.", inter["cost"].squeeze(1), inter["init_pred"], cpu(ml), cpu(up[4]),
                         cpu(up[2]))
     err = maxabs(conf, ref.squeeze(1))
     print("confidence model: max |conf - oracle|", err)
     assert err < 1e-3
+
+
+def test_confidence_small_maxdisp_raises():
+    """D = maxdisp / 16 < 7: the reference's topk(k=7) raises; so does the head, before any launch."""
+    m = MANIFEST["hot_S_gwc.npz"]
+    model = E.ESMStereo_confidence(64, True, False, m["backbone"], 16, feature_cls=StubFeature).eval().to(DEV)
+    x = torch.zeros(1, 3, 64, 128, device=DEV)
+    with pytest.raises(RuntimeError):
+        model(x, x)
 
 
 def test_confidence_requires_cv16():
