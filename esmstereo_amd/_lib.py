@@ -95,6 +95,7 @@ SIGNATURES = {
     "esm_conv_pair_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
+    "esm_node_filter_u16": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_float, c_void_p]),
     "esm_plan_create": (c_void_p, []),
     "esm_plan_destroy": (None, [c_void_p]),
     "esm_plan_add_conv": (c_int, [c_void_p, POINTER(EsmConvDesc)]),

@@ -16,6 +16,10 @@
 //    (save_disp.py:85): round half to even (rintf), then the low 16 bits of the integer (numpy's
 //    float -> uint16 cast on x86-64 goes through a 32-bit integer; a disparity in [0, 256) -
 //    every KITTI value - is exact either way).
+//  esm_node_filter_u16  the ROS node's post-processing (kitti_publisher_cuda_node.cpp:385-397) on the
+//    device: crop to the image (:385-388), cv::medianBlur 5x5 (BORDER_REPLICATE inside the crop,
+//    :391), valid_mask = (d > 0) & (d < max_disp) with the rest set to 0 (:400-402),
+//    convertTo(CV_16UC1, 256.0) = saturate_cast<ushort>(rint(d * 256)) (:403).
 // One thread per output element, consecutive threads along W (coalesced 4-byte stores); the
 // RGB reads are 3-byte strided and served by L1/L2 (each 64-lane load touches 192 contiguous bytes).
 #include "common.h"
@@ -68,7 +72,59 @@ __global__ void __launch_bounds__(kThreads) disp_u16_kernel(const float* __restr
     out[i] = static_cast<uint16_t>(static_cast<uint32_t>(static_cast<int32_t>(r)));
 }
 
+// median of 25 by a full compare-exchange sort (exact: selection only, no arithmetic)
+__device__ __forceinline__ float median25(float (&v)[25]) {
+#pragma unroll
+    for (int i = 0; i < 25; ++i)
+#pragma unroll
+        for (int j = 0; j < 24 - i; ++j) {
+            const float a = v[j], b = v[j + 1];
+            v[j] = fminf(a, b);
+            v[j + 1] = fmaxf(a, b);
+        }
+    return v[12];
+}
+
+__global__ void __launch_bounds__(kThreads) node_filter_kernel(const float* __restrict__ disp, uint16_t* __restrict__ out,
+                                                               float* __restrict__ filtered, int Hp, int Wp, int top,
+                                                               int left, int h, int w, float max_disp, long long n) {
+    const long long i = static_cast<long long>(blockIdx.x) * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const int x = static_cast<int>(i % w);
+    long long t = i / w;
+    const int y = static_cast<int>(t % h);
+    const long long b = t / h;
+    const float* d = disp + (b * Hp + top) * Wp + left;
+    float v[25];
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy) {
+        const int yy = min(max(y + dy - 2, 0), h - 1);  // BORDER_REPLICATE inside the cropped window
+#pragma unroll
+        for (int dx = 0; dx < 5; ++dx) {
+            const int xx = min(max(x + dx - 2, 0), w - 1);
+            v[dy * 5 + dx] = d[static_cast<long long>(yy) * Wp + xx];
+        }
+    }
+    float m = median25(v);
+    if (!(m > 0.f && m < max_disp)) m = 0.f;  // valid_mask = (d > 0) & (d < max_disp); setTo(0, ~valid)
+    if (filtered) filtered[i] = m;
+    // convertTo(CV_16UC1, 256.0): saturate_cast<ushort>(d * 256) = round half to even, clamp to [0, 65535]
+    const float r = rintf(m * 256.0f);
+    out[i] = static_cast<uint16_t>(fminf(fmaxf(r, 0.f), 65535.f));
+}
+
 }  // namespace
+
+int launch_node_filter(const float* disp, uint16_t* out, float* filtered, int B, int Hp, int Wp, int top, int left,
+                       int h, int w, float max_disp, hipStream_t s) {
+    if (!disp || !out) return arg_error("node_filter: null pointer");
+    if (B <= 0 || Hp <= 0 || Wp <= 0 || h <= 0 || w <= 0) return arg_error("node_filter: non-positive size");
+    if (top < 0 || left < 0 || top + h > Hp || left + w > Wp) return arg_error("node_filter: window outside the map");
+    const long long n = static_cast<long long>(B) * h * w;
+    hipLaunchKernelGGL(node_filter_kernel, dim3(ceil_div(n, kThreads)), dim3(kThreads), 0, s, disp, out, filtered, Hp, Wp,
+                       top, left, h, w, max_disp, n);
+    return check_launch("node_filter");
+}
 
 int launch_preprocess(const uint8_t* img, float* out, int B, int H, int W, int Hp, int Wp, int top, int left,
                       int pad_normalized, hipStream_t s) {
@@ -99,6 +155,11 @@ extern "C" {
 int esm_preprocess_u8(const uint8_t* img, float* out, int B, int H, int W, int Hp, int Wp, int top, int left,
                       int pad_normalized, void* stream) {
     return esm::launch_preprocess(img, out, B, H, W, Hp, Wp, top, left, pad_normalized, esm::as_stream(stream));
+}
+
+int esm_node_filter_u16(const float* disp, uint16_t* out, float* filtered, int B, int Hp, int Wp, int top, int left,
+                        int h, int w, float max_disp, void* stream) {
+    return esm::launch_node_filter(disp, out, filtered, B, Hp, Wp, top, left, h, w, max_disp, esm::as_stream(stream));
 }
 
 int esm_disp_to_u16(const float* disp, uint16_t* out, int B, int Hp, int Wp, int top, int left, int h, int w,

@@ -40,6 +40,8 @@
  *   esm_preprocess_u8         the input side: pad to /32 + ToTensor +
  *                             Normalize of test_kitti.py:93-106 (pad before normalising) or
  *                             datasets/kitti_dataset.py:151-170 (pad after), datasets/data_io.py:7-16
+ *   esm_node_filter_u16       the ROS node's post-processing (kitti_publisher_cuda_node.cpp:385-403):
+ *                             crop, medianBlur 5x5, valid mask, x256 -> uint16
  *   esm_disp_to_u16           the output side: crop of the padded disparity (test_kitti.py:115,
  *                             save_disp.py:81) + np.round(d * 256).astype(np.uint16) (save_disp.py:85)
  */
@@ -260,6 +262,13 @@ int esm_preprocess_u8(const uint8_t* img, float* out, int B, int H, int W, int H
 /* disp: [B, Hp, Wp] fp32; out: [B, h, w] uint16 = round_half_even(disp[b, top+y, left+x] * 256). */
 int esm_disp_to_u16(const float* disp, uint16_t* out, int B, int Hp, int Wp, int top, int left, int h, int w,
                     void* stream);
+
+/* The ROS node's post-processing (kitti_publisher/src/kitti_publisher_cuda_node.cpp:385-403) on the
+ * device: disp [B, Hp, Wp] fp32 -> window (top, left, h, w) -> 5x5 median (cv::medianBlur, replicate
+ * border inside the window) -> 0 outside (0, max_disp) -> out [B, h, w] uint16 =
+ * saturate_cast<ushort>(rint(d * 256)); `filtered` (may be NULL) receives the masked median [B, h, w]. */
+int esm_node_filter_u16(const float* disp, uint16_t* out, float* filtered, int B, int Hp, int Wp, int top, int left,
+                        int h, int w, float max_disp, void* stream);
 
 /* ---- native launch plan (the hot path as one replayable unit) ---- */
 typedef struct esm_plan esm_plan;
