@@ -1,7 +1,8 @@
 // Register-resident-weight row-streaming convolution for the full-resolution 2-D layers of the ESM
 // upsampler (models/ESMStereo.py:242-509: dmNx, spx_Nx, the refinement hourglass' conv1.1 / agg
 // layers at 96x312 .. 192x624 for ESMStereo-S at KITTI): BasicConv (models/submodule.py:12-38),
-// stride 1, k1 / k3, Cout <= 32, one input or a channel concat of up to 3 (spx_Nx.0, agg_N.0).
+// stride 1, k1 / k3 (and the 1 -> 16 5x5 disparity heads dmNx.0), Cout <= 32, one input or a
+// channel concat of up to 3 (spx_Nx.0, agg_N.0).
 //
 // A wave owns one 16-pixel column strip and R consecutive output rows (compile time), all couts of
 // its tile and the full K.  Everything but the strip / row origin is fixed at compile time:
@@ -172,7 +173,9 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
     // rows per wave, from a sweep of the 3x3 16 -> 16 layer at 192x624 (scripts/probes/k3_micro.hip):
     // 8 rows (2 rows of loads in flight) 10.3 us, 4 rows 11.7, 2 rows 14.1 -- fewer halo rows and
     // longer MFMA runs beat more waves per SIMD; small maps keep at least ~1 wave per SIMD
-    const int R = units >= 6144 ? 8 : (units >= 3072 ? 4 : 2);
+    // hint bits 26-27 (tuning, scripts/step_tune.py): 1 / 2 / 3 force R = 2 / 4 / 8
+    const int rsel = (a.hint >> 26) & 3;
+    const int R = rsel ? (1 << rsel) : (units >= 6144 ? 8 : (units >= 3072 ? 4 : 2));
     const dim3 grid(ceil_div(a.Wo, 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide): grid too large");
     const float* base = nullptr;
@@ -208,8 +211,9 @@ bool wide_ok(const esm_conv_desc& a) {
     const float* base;
     int span, dl[ESM_MAX_SRC];
     if (!source_window(a, &base, &span, dl)) return false;
-    if (a.kh != a.kw || (a.kh != 1 && a.kh != 3)) return false;
+    if (a.kh != a.kw || (a.kh != 1 && a.kh != 3 && a.kh != 5)) return false;
     const int ng = (a.Cin + 3) / 4, mt = a.Cout > 16 ? 2 : 1;
+    if (a.kh == 5) return ng <= 2 && mt == 1;  // the 5x5 disparity heads (dmNx.0: 1 -> 16)
     return a.kh == 3 ? (ng * mt <= 10 && (mt == 1 || ng <= 4)) : ng * mt <= 32;
 }
 
@@ -217,6 +221,7 @@ int launch_wide(const esm_conv_desc& a, hipStream_t s) {
     if (!wide_ok(a)) return arg_error("conv: wide-form hint not applicable");
     const int ng = (a.Cin + 3) / 4;
     const bool m2 = a.Cout > 16;
+    if (a.kh == 5) return ng <= 1 ? launch_wide_r<5, 1, 1>(a, s) : launch_wide_r<5, 2, 1>(a, s);
     if (a.kh == 3) {
         if (!m2) {
             if (ng <= 2) return launch_wide_r<3, 2, 1>(a, s);

@@ -176,7 +176,9 @@ __global__ void __launch_bounds__(kWtThreads) wtconv_kernel(const esm_conv_desc 
 template <int NG, int MT>
 int launch_widet_g(const esm_conv_desc& a, hipStream_t s) {
     const long long units = static_cast<long long>(a.B) * a.Hi * ceil_div(a.Wi, 16);
-    const int R = units >= 8192 ? 2 : 1;  // sub-grid rows per wave: keep ~2 waves per SIMD
+    // sub-grid rows per wave: keep ~2 waves per SIMD; hint bits 26-27 = 1 / 2 force R = 1 / 2 (tuning)
+    const int rsel = (a.hint >> 26) & 3;
+    const int R = rsel == 1 ? 1 : (rsel == 2 ? 2 : (units >= 8192 ? 2 : 1));
     const dim3 grid(ceil_div(a.Wi, 64), ceil_div(a.Hi, R), static_cast<unsigned>(a.B));
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide-T): grid too large");
     const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && a.post_scale == 1.f &&

@@ -126,11 +126,13 @@ typedef struct {
                      SMALL << 21: the lean K-split form for latency-bound layers (conv_small.hip;
                      plain epilogues: no mul / up / shuffle) |
                      WIDE << 22: register-resident-weight row-streaming form (conv_wide.hip; 2-D, stride 1,
-                     k1 / k3, one source, Cout <= 32, plain epilogues) |
+                     k1 / k3 / k5, one source window, Cout <= 32) |
                      WIDE3 << 24: register-weight plane-streaming form for 3x3x3 s1 p1 3-D convs with <= 16 couts
                      and <= 32 input channels (conv_wide3.hip; plain, `* mul` and residual epilogues) |
                      WIDET << 25: register-weight ConvTranspose2d k4 s2 form computing all 4 parity classes per
                      wave (conv_widet.hip; one source, 16 * channel groups * cout tiles <= 64).
+                     Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
+                     sub-grid rows); 0 = the automatic choice.
                      Bit 23 is read from a PAIR's first descriptor: the LDS-weight pair kernel instead of the lean
                      1x1 -> 3x3 form (A/B measurements) */
     int64_t ub, uh;

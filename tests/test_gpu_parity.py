@@ -259,7 +259,8 @@ def test_conv_small_form(nd, cins, cout, k, s, tr, shape):
 HINT_WIDE = 1 << 22
 WIDE_CASES = [(16, 16, 3, 1, (192, 624)), (16, 16, 3, 1, (94, 310)), (40, 16, 3, 1, (96, 312)),
               (16, 8, 3, 1, (96, 312)), (16, 16, 1, 1, (94, 310)), (56, 16, 1, 0, (96, 312)),
-              (16, 32, 3, 1, (47, 83)), (6, 24, 3, 1, (33, 50)), (128, 16, 1, 0, (9, 70)), (16, 16, 3, 1, (5, 17))]
+              (16, 32, 3, 1, (47, 83)), (6, 24, 3, 1, (33, 50)), (128, 16, 1, 0, (9, 70)), (16, 16, 3, 1, (5, 17)),
+              (1, 16, 5, 1, (96, 312)), (1, 16, 5, 1, (24, 78)), (6, 16, 5, 1, (13, 40))]
 
 
 @pytest.mark.parametrize("cin,cout,k,p,shape", WIDE_CASES)
@@ -278,6 +279,9 @@ def test_conv_wide_form(cin, cout, k, p, shape):
                  post_scale2=2.0, hint=HINT_WIDE)
     ref2 = _ref_conv([x], conv, bn, ACT_GELU, res=res)
     assert rel(y, ref2 * 4) < 1e-5 and rel(out2, ref2 * 2) < 1e-5
+    for rsel in (1, 2, 3):  # every rows-per-wave block (hint bits 26-27)
+        y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], hint=HINT_WIDE | (rsel << 26))
+        assert rel(y, ref) < 1e-5
 
 
 @pytest.mark.parametrize("cins,cout,k,p,shape", [((16, 24), 16, 3, 1, (96, 312)), ((16, 16, 24), 16, 1, 0, (96, 312)),
@@ -335,6 +339,8 @@ def test_conv_widet_form(cin, cout, shape, B):
     p = pk(conv, bn, act)
     y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_WIDET)
     assert rel(y, ref) < 1e-5
+    for rsel in (1, 2):  # both sub-grid rows-per-wave blocks (hint bits 26-27)
+        assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_WIDET | (rsel << 26)), ref) < 1e-5
     res = torch.randn_like(ref)
     y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), post_scale=4.0, hint=HINT_WIDET)
     assert rel(y, _ref_conv([x], conv, bn, act, res=res, post=4.0)) < 1e-5
