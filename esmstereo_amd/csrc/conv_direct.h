@@ -29,6 +29,17 @@
 namespace esm {
 namespace conv {
 
+// Store cache policy of the buffer-store epilogues: write-through (sc1).  With default-policy
+// stores the output's dirty lines are written back at the kernel boundary, on the critical path of
+// the launch chain (bytes / ~6 TB/s, MI355X_MICROARCH.md price list "boundary"); written through they
+// leave L2 while the kernel runs.  Measured on the S-K step, three rotations on one box (scripts/
+// gpu_ab_multi.sh): 382.1 -> 377.0 us.  A per-store runtime choice (sc1 above a size threshold)
+// measured 388-390 us: the select splits every store into two branches, so the policy is a constant.
+constexpr int kStoreAux = 16;
+__device__ __forceinline__ void store_b32(unsigned v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, vo, so, kStoreAux);
+}
+
 constexpr int kDirectThreads = 256;
 
 #ifdef ESM_CONV_STAMPS

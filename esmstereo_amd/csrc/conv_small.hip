@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
             v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
             v = act_t<ACT>(v, a.act);
             const unsigned vo = (co < a.Cout && xsub < Ws) ? 4u * (co * static_cast<int>(a.oc) + ox) : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(vo), orow, 0);
+            store_b32(__float_as_uint(v), ro_, static_cast<int>(vo), orow);
         }
         return;
     }

@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
                     a.out[o] = v * a.post_scale;
                     if (a.out2) a.out2[o] = v * a.post_scale2;
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(ovo[mt][j]), orow, 0);
+                    store_b32(__float_as_uint(v), ro_, static_cast<int>(ovo[mt][j]), orow);
                 }
             }
     };

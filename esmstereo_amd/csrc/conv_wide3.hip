@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
             const unsigned o = (co < a.Cout && px < a.Wo && zo < a.Do)
                                    ? 4u * (co * static_cast<int>(a.oc) + zo * static_cast<int>(a.od) + y * static_cast<int>(a.oh) + px)
                                    : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0, 0);
+            store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0);
         } else {
             if (co >= a.Cout || px >= a.Wo || zo >= a.Do) continue;
             if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + static_cast<long long>(y) * a.mh + px];

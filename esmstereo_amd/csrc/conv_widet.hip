@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(kWtThreads) wtconv_kernel(const esm_conv_desc 
                         const int orow = oy < a.Ho ? 4 * oy * static_cast<int>(a.oh) : static_cast<int>(kOOB);
                         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                         const u32x2 pk2 = {__float_as_uint(v2[0]), __float_as_uint(v2[1])};
-                        __builtin_amdgcn_raw_buffer_store_b64(pk2, ro_, static_cast<int>(ovo[mt][j]), orow, 0);
+                        __builtin_amdgcn_raw_buffer_store_b64(pk2, ro_, static_cast<int>(ovo[mt][j]), orow, kStoreAux);
                     } else {
                         const int co = 16 * mt + 4 * kq + j;
                         if (co >= a.Cout || xs >= a.Wi || oy >= a.Ho) continue;

@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 cp esmstereo_amd/tuned_hints.json gpurun_out/tuned_hints.json
-timeout -k 10 900 python -u scripts/step_tune.py --mode tune --variants ${VARIANTS:-S} --rounds ${ROUNDS:-3} \
+timeout -k 10 900 python -u scripts/step_tune.py --mode tune --variants ${VARIANTS:-S} --rounds ${ROUNDS:-5} --margin-us ${MARGIN:-0.5} \
     --out gpurun_out/tuned_hints.json --report gpurun_out/step_tune_report.json > gpurun_out/step_tune.log 2>&1 \
     || { tail -30 gpurun_out/step_tune.log; exit 1; }
 grep -v "0.00 us" gpurun_out/step_tune.log | tail -60

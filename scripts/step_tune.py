@@ -105,6 +105,17 @@ def marginal(variant: str, dev, rounds: int) -> dict:
     return {"variant": variant, "step_us": round(step, 1), "ops": rows}
 
 
+def step_only(variant: str, dev, rounds: int) -> dict:
+    hp = build(variant, dev)
+    reps = reps_for(hp)
+    graph_ok(hp)
+    ts = [window(hp, reps) for _ in range(max(rounds, 5) * 4)]
+    hp.close()
+    med = statistics.median(ts)
+    print(f"{variant}: step {med:.2f} us (min {min(ts):.2f}, max {max(ts):.2f}, {len(ts)} windows of {reps})", flush=True)
+    return {"variant": variant, "step_us": round(med, 2), "windows": [round(t, 2) for t in ts]}
+
+
 def tune(variant: str, dev, rounds: int, margin_us: float) -> dict:
     hp = build(variant, dev)
     plan, meta = hp.ctx.plan, hp.ctx.meta
@@ -148,7 +159,7 @@ def tune(variant: str, dev, rounds: int, margin_us: float) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["marginal", "tune"], default="marginal")
+    ap.add_argument("--mode", choices=["marginal", "tune", "step"], default="marginal")
     ap.add_argument("--variants", default="S")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--margin-us", type=float, default=0.3)
@@ -160,6 +171,8 @@ def main():
     variants = args.variants.split(",")
     if args.mode == "marginal":
         reports = [marginal(v, dev, args.rounds) for v in variants]
+    elif args.mode == "step":
+        reports = [step_only(v, dev, args.rounds) for v in variants]
     else:
         reports = [tune(v, dev, args.rounds, args.margin_us) for v in variants]
     os.makedirs(os.path.dirname(args.report), exist_ok=True)
