@@ -189,7 +189,14 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
         if (oy >= HO) continue;
         float* o = a.out + b * a.ob + static_cast<long long>(oy) * a.oh + ox;
         if (ox + 3 < WO && ((reinterpret_cast<uintptr_t>(o)) & 15) == 0) {
-            *reinterpret_cast<conv::floatx4*>(o) = conv::floatx4{acc[0] + tb, acc[1] + tb, acc[2] + tb, acc[3] + tb};
+            // write-through (sc1) 16-B store (conv_direct.h kStoreAux)
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out + b * a.ob, static_cast<short>(0),
+                                                                                0x7fffffff, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(acc[0] + tb), __float_as_uint(acc[1] + tb), __float_as_uint(acc[2] + tb),
+                      __float_as_uint(acc[3] + tb)},
+                rs, static_cast<int>(4 * (static_cast<long long>(oy) * a.oh + ox)), 0, 16);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j)

@@ -105,7 +105,14 @@ __global__ void __launch_bounds__(kThreads) gwc_kernel(const float* __restrict__
         }
         float* dst = vb + static_cast<long long>(dd) * HW;
         if (VEC && pt + kPix <= HW) {
-            *reinterpret_cast<float4*>(dst + pt) = make_float4(o[0], o[1], o[2], o[3]);
+            // write-through (sc1) 16-B stores: no dirty volume lines left for the kernel-boundary
+            // write-back (conv_direct.h kStoreAux; -0.7 us on the S-K step with the two below)
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(vb, static_cast<short>(0), 0x7fffffff,
+                                                                                0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, rv,
+                static_cast<int>(4 * (static_cast<long long>(dd) * HW + pt)), 0, 16);
         } else {
 #pragma unroll
             for (int k = 0; k < kPix; ++k)
