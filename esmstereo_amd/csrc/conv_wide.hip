@@ -27,20 +27,28 @@ namespace {
 
 constexpr int kWideThreads = 256;
 
-template <int K, int NG, int MT, int R, int ACT, bool PLAIN>
+// KS = 2: the K reduction of a strip is split over two waves (channel groups [0, NGW) and [NGW, 2 NGW)),
+// so a 192x624 layer runs ~2 waves per SIMD instead of ~1 (one wave alone leaves the MFMA pipe idle
+// across its dependency and memory stalls); the two partial row blocks meet in
+// LDS once, after the last MFMA, and each wave finishes half of the rows.
+template <int K, int NG, int MT, int R, int ACT, bool PLAIN, int KS = 1>
 __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a, const float* wbase, int wspan,
                                                              int d0, int d1, int d2) {
     constexpr int NR = R + K - 1;  // input rows a wave reads
+    constexpr int NGW = (NG + KS - 1) / KS;  // channel groups per wave
+    static_assert(KS == 1 || (KS == 2 && R % 2 == 0), "K split: two waves, an even row block");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
-    const int x0 = (blockIdx.x * 4 + wave) * 16;
+    const int kh = KS == 2 ? (wave & 1) : 0;  // which half of the channel groups
+    const int gb = kh * NGW;                  // first channel group of this wave
+    const int x0 = (blockIdx.x * (4 / KS) + wave / KS) * 16;
     const int y0 = blockIdx.y * R;
     const int b = blockIdx.z;
     const int cob = 0;  // Cout <= 16 * MT: one cout tile
 
     // ---- weights -> VGPRs: w[tap][cin_pad][cout_pad], lane (kq, n16) = k row 4g + kq, cout n16
-    float wv[K * K][NG][MT];
+    float wv[K * K][NGW][MT];
     {
         const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(a.w), static_cast<short>(0), 4 * K * K * a.cin_pad * a.cout_pad, 0x00020000);
@@ -48,10 +56,10 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
 #pragma unroll
         for (int t = 0; t < K * K; ++t)
 #pragma unroll
-            for (int g = 0; g < NG; ++g)
+            for (int g = 0; g < NGW; ++g)
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    wv[t][g][mt] = buf_load_s(wrs, wl, 4 * ((t * a.cin_pad + 4 * g) * a.cout_pad + 16 * mt));
+                for (int mt = 0; mt < MT; ++mt)  // groups past cin_pad read past the buffer: 0
+                    wv[t][g][mt] = buf_load_s(wrs, wl, 4 * ((t * a.cin_pad + 4 * (gb + g)) * a.cout_pad + 16 * mt));
     }
     // BN / bias constants of the lane's couts
     float scl[MT][4], shf[MT][4];
@@ -71,10 +79,10 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), static_cast<short>(0), wspan, 0x00020000);
     const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
     const int xo = x0 + n16;
-    unsigned vo[NG][K];  // per-lane byte offset of group g's channel at column shift dx
+    unsigned vo[NGW][K];  // per-lane byte offset of group g's channel at column shift dx
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        const int c = 4 * g + kq;
+    for (int g = 0; g < NGW; ++g) {
+        const int c = 4 * (gb + g) + kq;
         const int s = c < lo1 ? 0 : (c < lo2 ? 1 : 2);
         const int cl = c - (s == 0 ? 0 : (s == 1 ? lo1 : lo2));
         const long long sb = s == 0 ? a.src[0].sb : (s == 1 ? a.src[1].sb : a.src[2].sb);
@@ -88,11 +96,11 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
                             : kOOB;
         }
     }
-    auto load_row = [&](float (&dst)[NG][K], int r) {  // input row y0 - ph + r
+    auto load_row = [&](float (&dst)[NGW][K], int r) {  // input row y0 - ph + r
         const int yi = y0 - a.ph + r;
         const int roff = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NGW; ++g)
 #pragma unroll
             for (int dx = 0; dx < K; ++dx) dst[g][dx] = buf_load_s(rs, vo[g][dx], roff);
     };
@@ -143,7 +151,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
     // input rows in flight: PF ahead of the row being multiplied (ring of PF + 1 row buffers)
     constexpr int PF = R >= 4 ? 2 : 1;
     constexpr int NB = PF + 1;
-    float bin[NB][NG][K];
+    float bin[NB][NGW][K];
 #pragma unroll
     for (int r = 0; r < PF; ++r) load_row(bin[r], r);
 #pragma unroll
@@ -151,7 +159,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
         if (r + PF < NR) load_row(bin[(r + PF) % NB], r + PF);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NGW; ++g)
 #pragma unroll
             for (int dx = 0; dx < K; ++dx)
 #pragma unroll
@@ -163,7 +171,38 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
                         acc[ro][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[dy * K + dx][g][mt], bin[r % NB][g][dx],
                                                                            acc[ro][mt], 0, 0, 0);
                 }
-        if (r - (K - 1) >= 0) finish(r - (K - 1));
+        if (KS == 1 && r - (K - 1) >= 0) finish(r - (K - 1));
+    }
+    if constexpr (KS == 2) {
+        // the partner's partial sums of the rows this wave finishes: wave kh finishes rows
+        // [kh R/2, kh R/2 + R/2); it hands the other half over through LDS; sums in the fixed order
+        // (groups [0, NGW)) + (groups [NGW, 2 NGW)) on both sides
+        constexpr int RH = R / 2;
+        __shared__ float xch[4][RH * MT * 4][64];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((r < RH) != (kh == 0)) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) xch[wave][((r % RH) * MT + mt) * 4 + j][lane] = acc[r][mt][j];
+            }
+        }
+        __syncthreads();
+        const int partner = wave ^ 1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((r < RH) == (kh == 0)) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float p = xch[partner][((r % RH) * MT + mt) * 4 + j][lane];
+                        acc[r][mt][j] = kh == 0 ? acc[r][mt][j] + p : p + acc[r][mt][j];
+                    }
+                finish(r);
+            }
+        }
     }
 }
 
@@ -176,7 +215,9 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
     // hint bits 26-27 (tuning, scripts/step_tune.py): 1 / 2 / 3 force R = 2 / 4 / 8
     const int rsel = (a.hint >> 26) & 3;
     const int R = rsel ? (1 << rsel) : (units >= 6144 ? 8 : (units >= 3072 ? 4 : 2));
-    const dim3 grid(ceil_div(a.Wo, 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
+    // hint bit 28: split each strip's K over two waves (the KS = 2 form, 2 strips per workgroup)
+    const bool ks2 = (a.hint & (1 << 28)) && NG >= 2 && R >= 4;
+    const dim3 grid(ceil_div(a.Wo, ks2 ? 32 : 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide): grid too large");
     const float* base = nullptr;
     int span = 0, dl[ESM_MAX_SRC];
@@ -188,6 +229,21 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
 #define ESM_WIDE(RR, AC)                                                                                         \
     hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU)>), grid, dim3(kWideThreads), 0, s, a, base, \
                        span, dl[0], dl[1], dl[2])
+#define ESM_WIDE2(RR, AC)                                                                                        \
+    hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU), 2>), grid, dim3(kWideThreads), 0, s, a, \
+                       base, span, dl[0], dl[1], dl[2])
+    if constexpr (NG >= 2) {
+        if (ks2) {
+            if (R == 8) {
+                if (gelu) ESM_WIDE2(8, ESM_ACT_GELU);
+                else ESM_WIDE2(8, -1);
+            } else {
+                if (gelu) ESM_WIDE2(4, ESM_ACT_GELU);
+                else ESM_WIDE2(4, -1);
+            }
+            return check_launch("conv(wide, K split)");
+        }
+    }
     if (R == 8) {
         if (gelu) ESM_WIDE(8, ESM_ACT_GELU);
         else ESM_WIDE(8, -1);
@@ -199,6 +255,7 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
         else ESM_WIDE(2, -1);
     }
 #undef ESM_WIDE
+#undef ESM_WIDE2
     return check_launch("conv(wide)");
 }
 

@@ -132,7 +132,8 @@ typedef struct {
                      WIDET << 25: register-weight ConvTranspose2d k4 s2 form computing all 4 parity classes per
                      wave (conv_widet.hip; one source, 16 * channel groups * cout tiles <= 64).
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
-                     sub-grid rows); 0 = the automatic choice.
+                     sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
+                     split over two waves (partial rows summed once through LDS; R >= 4).
                      Bit 23 is read from a PAIR's first descriptor: the LDS-weight pair kernel instead of the lean
                      1x1 -> 3x3 form (A/B measurements) */
     int64_t ub, uh;

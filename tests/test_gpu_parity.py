@@ -282,6 +282,12 @@ def test_conv_wide_form(cin, cout, k, p, shape):
     for rsel in (1, 2, 3):  # every rows-per-wave block (hint bits 26-27)
         y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], hint=HINT_WIDE | (rsel << 26))
         assert rel(y, ref) < 1e-5
+    for rsel in (2, 3):  # the K split over two waves (hint bit 28), both epilogues
+        y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], hint=HINT_WIDE | (rsel << 26) | (1 << 28))
+        assert rel(y, ref) < 1e-5
+        y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], res=res.to(DEV), post_scale=4.0, out2=out2,
+                     post_scale2=2.0, hint=HINT_WIDE | (rsel << 26) | (1 << 28))
+        assert rel(y, ref2 * 4) < 1e-5 and rel(out2, ref2 * 2) < 1e-5
 
 
 @pytest.mark.parametrize("cins,cout,k,p,shape", [((16, 24), 16, 3, 1, (96, 312)), ((16, 16, 24), 16, 1, 0, (96, 312)),
