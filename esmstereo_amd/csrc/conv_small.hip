@@ -39,13 +39,15 @@ inline unsigned magic_for(int d) {
     return d <= 1 ? 0u : static_cast<unsigned>(((1ull << 32) + static_cast<unsigned long long>(d) - 1) / d);
 }
 
-template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN>
-__global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
+// NW = 4 or 8 waves splitting the K reduction (8: layers with more than 4 channel groups, so that no
+// wave walks two groups one after the other; the epilogue runs on the first 256 threads)
+template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
     constexpr int KT = TR ? 2 : K;  // taps per dim (per parity class when transposed)
     constexpr int KDT = D3 ? KT : 1;
     constexpr int TAPS = KDT * KT * KT;
     constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
-    __shared__ __attribute__((aligned(16))) float red[4 * MT * 4 * 64];
+    __shared__ __attribute__((aligned(16))) float red[NW * MT * 4 * 64];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -68,7 +70,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
     const int qw = TR ? cls & 1 : 0;
 
     // epilogue constants of the (cout, pixel) elements this thread finishes, loaded up front
-    const int ej = tid >> 6;  // accumulator register j of the element
+    const int ej = (tid >> 6) & 3;  // accumulator register j of the element
     const int ecol = lane & 15;
     float scl[MT], shf[MT];
 #pragma unroll
@@ -114,7 +116,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
 
     const int G = (a.Cin + 3) >> 2;
     const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
-    for (int g = wave; g < G; g += 4) {
+    for (int g = wave; g < G; g += NW) {
         const int c0 = 4 * g;
         // the group's source (4-channel aligned splits): named-field selects, no runtime index
         const int s = c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2);
@@ -161,6 +163,14 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
 #pragma unroll
         for (int j = 0; j < 4; ++j) red[((wave * MT + mt) * 4 + j) * 64 + lane] = acc[0][mt][j] + acc[1][mt][j];
     __syncthreads();
+    if (NW > 4 && tid >= 256) return;
+    // fixed-order sum of the NW partial tiles of element e
+    auto reduced = [&](int e) {
+        float v = red[e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v = v + red[w * MT * 256 + e];
+        return v;
+    };
 
     const int xsub = x0 + ecol;
     const int oz = TR ? 2 * zs + qd : zs;
@@ -179,7 +189,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
         for (int mt = 0; mt < MT; ++mt) {
             const int co = cob + 16 * mt + 4 * kq + ej;
             const int e = (mt * 4 + ej) * 64 + lane;
-            float v = ((red[e] + red[MT * 256 + e]) + red[2 * MT * 256 + e]) + red[3 * MT * 256 + e];
+            float v = reduced(e);
             v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
             v = act_t<ACT>(v, a.act);
             const unsigned vo = (co < a.Cout && xsub < Ws) ? 4u * (co * static_cast<int>(a.oc) + ox) : kOOB;
@@ -193,7 +203,7 @@ __global__ void __launch_bounds__(kSmallThreads) lconv_kernel(const esm_conv_des
         const int co = cob + 16 * mt + 4 * kq + ej;
         if (co >= a.Cout) continue;
         const int e = (mt * 4 + ej) * 64 + lane;
-        float v = ((red[e] + red[MT * 256 + e]) + red[2 * MT * 256 + e]) + red[3 * MT * 256 + e];
+        float v = reduced(e);
         v = a.scale ? v * scl[mt] + shf[mt] : v + shf[mt];
         v = act_t<ACT>(v, a.act);
         if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(oz) * a.rd + static_cast<long long>(oy) * a.rh + ox];
@@ -217,13 +227,23 @@ int launch_small_m(const esm_conv_desc& a, hipStream_t s) {
     const bool gelu = a.act == ESM_ACT_GELU && !a.res && !a.out2 && a.post_scale == 1.f &&
                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(D3 ? a.Do : 1) * a.od +
                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    // hint bit 29: 8 waves per workgroup (K split 8 ways) for layers with more than 4 channel groups
+    const bool w8 = (a.hint & (1 << 29)) && (a.Cin + 3) / 4 > 4;
+#define ESM_SMALL(M, AC, PL)                                                                                   \
+    do {                                                                                                       \
+        if (w8)                                                                                                \
+            hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, M, AC, PL, 8>), grid, dim3(512), 0, s, a, mds, mb); \
+        else                                                                                                   \
+            hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, M, AC, PL>), grid, dim3(kSmallThreads), 0, s, a, mds, mb); \
+    } while (0)
     if (MT == 1) {
-        if (gelu) hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1, ESM_ACT_GELU, true>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
-        else hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 1, -1, false>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+        if (gelu) ESM_SMALL(1, ESM_ACT_GELU, true);
+        else ESM_SMALL(1, -1, false);
     } else {
-        if (gelu) hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2, ESM_ACT_GELU, true>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
-        else hipLaunchKernelGGL((lconv_kernel<D3, K, S, TR, 2, -1, false>), grid, dim3(kSmallThreads), 0, s, a, mds, mb);
+        if (gelu) ESM_SMALL(2, ESM_ACT_GELU, true);
+        else ESM_SMALL(2, -1, false);
     }
+#undef ESM_SMALL
     return check_launch("conv(small)");
 }
 

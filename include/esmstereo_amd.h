@@ -133,7 +133,8 @@ typedef struct {
                      wave (conv_widet.hip; one source, 16 * channel groups * cout tiles <= 64).
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
                      sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
-                     split over two waves (partial rows summed once through LDS; R >= 4).
+                     split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
+                     8 waves per workgroup splitting K (layers with more than 4 channel groups).
                      Bit 23 is read from a PAIR's first descriptor: the LDS-weight pair kernel instead of the lean
                      1x1 -> 3x3 form (A/B measurements) */
     int64_t ub, uh;

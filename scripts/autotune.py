@@ -33,12 +33,12 @@ from esmstereo_amd._lib import check, lib  # noqa: E402
 # narrow-output 16-block form 1 << 17, automatic without it 1 << 18, VALU 1-input-channel form 1 << 20,
 # lean K-split small form 1 << 21, register-weight row-streaming wide form 1 << 22,
 # its 3-D plane-streaming twin 1 << 24, the transposed 2-D twin 1 << 25; bits 26-27 = rows per wave of
-# the two register-weight 2-D forms; bit 28 = the wide form's K split over two waves
+# the two register-weight 2-D forms; bit 28 = the wide form's K split over two waves, bit 29 = the small form on 8 waves
 CANDIDATES = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x211, 0x212, 0x241, 0x242, 0x1211, 0x2211, 0x4211, 0x1212,
               0x2212, 0x400, 0x114, 0x10000, 1 << 17, 1 << 18, 1 << 20, 1 << 21, 1 << 22, 1 << 24, 1 << 25,
               (1 << 22) | (1 << 26), (1 << 22) | (2 << 26), (1 << 22) | (3 << 26), (1 << 25) | (1 << 26),
               (1 << 25) | (2 << 26), (1 << 22) | (1 << 28), (1 << 22) | (2 << 26) | (1 << 28),
-              (1 << 22) | (3 << 26) | (1 << 28)]
+              (1 << 22) | (3 << 26) | (1 << 28), (1 << 21) | (1 << 29)]
 
 
 def op_time(hp, i: int, reps: int) -> float:

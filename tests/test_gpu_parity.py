@@ -254,6 +254,9 @@ def test_conv_small_form(nd, cins, cout, k, s, tr, shape):
     p = pk(conv, bn, act)
     y = run_conv(Ctx(DEV), p, [x.to(DEV) for x in xs], hint=HINT_SMALL)
     assert rel(y, ref) < 1e-5
+    if sum(cins) > 16:  # the 8-wave K split (hint bit 29) where it applies
+        y = run_conv(Ctx(DEV), p, [x.to(DEV) for x in xs], hint=HINT_SMALL | (1 << 29))
+        assert rel(y, ref) < 1e-5
 
 
 HINT_WIDE = 1 << 22
