@@ -220,9 +220,12 @@ int launch_c(const esm_smix_desc& a, hipStream_t s) {
 // smix_kernel (equal to the three-launch chain up to the compiler's FMA contraction choices).
 constexpr int kFTH = 4;
 constexpr int kFTW = 16;
+// 512 threads: the t1 region (4 + 12) x (16 + 12) = 448 pixels and the t2 region (220) are one pass each
+// (with 256 threads the t1 pass ran twice), the depthwise phases take half the iterations
+constexpr int kFThreads = 512;
 
 template <int C, int K>
-__global__ void __launch_bounds__(kThreads) fmnet_kernel(const esm_fmnet_desc a) {
+__global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
     using Lyt = SmixLayout<C>;
     constexpr int R = K / 2;
     constexpr int AH = kFTH + 4 * R, AW = kFTW + 4 * R, AP = AH * AW;  // t1 region
@@ -241,39 +244,55 @@ __global__ void __launch_bounds__(kThreads) fmnet_kernel(const esm_fmnet_desc a)
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
 
-    // weights: stage s (ln | fc0_w | fc0_b | fc2_w | fc2_b) for s = 0..3, then dw0 w, b, dw1 w, b
-    for (int i = tid; i < NW; i += kThreads) {
-        const float* p;
-        int off;
+    // one round trip for everything this workgroup reads from memory: its t1 pixel (AP <= kFThreads:
+    // one per thread) and every weight (stage s = ln | fc0_w | fc0_b | fc2_w | fc2_b for s = 0..3,
+    // then dw0 w, b, dw1 w, b), all loads issued before the first LDS store
+    static_assert(AP <= kFThreads, "one t1 pixel per thread");
+    constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
+    float rw[NWR];
+#pragma unroll
+    for (int k = 0; k < NWR; ++k) {
+        const int i = tid + k * kFThreads;
+        const float* p = nullptr;
+        int off = 0;
         if (i < DW0) {
             const esm_smix_stage& g = a.stage[i / Lyt::STAGE];
             const int j = i % Lyt::STAGE;
             p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
             off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
-        } else {
+        } else if (i < NW) {
             const int l = i < DW1 ? 0 : 1;
             const int j = i - (l ? DW1 : DW0);
             p = j < C * K * K ? a.dw_w[l] : a.dw_b[l];
             off = j < C * K * K ? j : j - C * K * K;
         }
-        wsh[i] = p[off];
+        const float v = (p ? p : a.x)[p ? off : 0];  // unconditional load, then select
+        rw[k] = p ? v : 0.f;
     }
+    const int q = tid;  // this thread's t1 pixel (region A)
+    const int aly = q / AW, alx = q - (q / AW) * AW;
+    const int agy = y0 - 2 * R + aly, agx = x0 - 2 * R + alx;
+    const bool ain = q < AP && agy >= 0 && agy < H && agx >= 0 && agx < W;
+    float t1[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const float v = xb[ain ? c * plane + agy * W + agx : 0];
+        t1[c] = ain ? v : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < NWR; ++k)
+        if (tid + k * kFThreads < NW) wsh[tid + k * kFThreads] = rw[k];
     __syncthreads();
     // t1 = SMLayer0.mlp1 (x) on region A
-    for (int q = tid; q < AP; q += kThreads) {
-        const int ly = q / AW, lx = q - (q / AW) * AW;
-        const int gy = y0 - 2 * R + ly, gx = x0 - 2 * R + lx;
-        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        float t[C];
+    if (q < AP) {
+        if (ain) mix_stage<C>(t1, wsh);
 #pragma unroll
-        for (int c = 0; c < C; ++c) t[c] = in ? xb[c * plane + gy * W + gx] : 0.f;
-        if (in) mix_stage<C>(t, wsh);
-#pragma unroll
-        for (int c = 0; c < C; ++c) s1[(c * AH + ly) * AWP + lx] = in ? t[c] : 0.f;
+        for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
     __syncthreads();
     // dw0 (t1) on region B
-    for (int i = tid; i < C * BP; i += kThreads) {
+    for (int i = tid; i < C * BP; i += kFThreads) {
         const int c = i / BP, p = i - (i / BP) * BP;
         const int py = p / BW, px = p - (p / BW) * BW;
         const float* w = wsh + DW0 + c * K * K;
@@ -286,7 +305,7 @@ __global__ void __launch_bounds__(kThreads) fmnet_kernel(const esm_fmnet_desc a)
     }
     __syncthreads();
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
-    for (int p = tid; p < BP; p += kThreads) {
+    for (int p = tid; p < BP; p += kFThreads) {
         const int py = p / BW, px = p - (p / BW) * BW;
         const int gy = y0 - R + py, gx = x0 - R + px;
         const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
@@ -302,7 +321,7 @@ __global__ void __launch_bounds__(kThreads) fmnet_kernel(const esm_fmnet_desc a)
     }
     __syncthreads();
     // dw1 (t2) on the tile
-    for (int i = tid; i < C * CP; i += kThreads) {
+    for (int i = tid; i < C * CP; i += kFThreads) {
         const int c = i / CP, p = i - (i / CP) * CP;
         const int py = p / kFTW, px = p - (p / kFTW) * kFTW;
         const float* w = wsh + DW1 + c * K * K;
@@ -366,9 +385,9 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
     }
     const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, kFTH), a.B);
     if (a.C == 8)
-        hipLaunchKernelGGL((fmnet_kernel<8, 7>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((fmnet_kernel<8, 7>), grid, dim3(kFThreads), 0, s, a);
     else if (a.C == 16)
-        hipLaunchKernelGGL((fmnet_kernel<16, 7>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((fmnet_kernel<16, 7>), grid, dim3(kFThreads), 0, s, a);
     else {
         set_error("fmnet: C must be 8 or 16");
         return ESM_ERR_UNSUPPORTED;

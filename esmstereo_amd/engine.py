@@ -660,11 +660,11 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
     return out
 
 
-# FMBlock.net as one launch (esm_fmnet_f32): opt-in (ESM_FMNET=1).  Measured on MI355X it saves no
-# time (S-K 1916 vs 1914 pairs/s) and loses at L (397 vs 404): the fused kernel's four
-# barrier-separated phases on a 4x16 tile plus a 6-pixel halo run longer than the launches they
-# replace.
-FMNET_ENABLED = os.environ.get("ESM_FMNET") == "1"
+# FMBlock.net as one launch (esm_fmnet_f32) instead of three smix launches; ESM_FMNET=0 turns it off.
+# Round 1 measured it no faster (its 256-thread workgroups ran the 448-pixel t1 region in two passes
+# and staged weights and pixels in serial round trips); on 512 threads with one staging round trip
+# it takes the S-K step from 369.5 to 362.3 us (three rotations on one box).
+FMNET_ENABLED = os.environ.get("ESM_FMNET", "1") != "0"
 
 
 def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
