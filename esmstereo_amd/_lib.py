@@ -61,7 +61,9 @@ class EsmSmixDesc(Structure):
 class EsmFmnetDesc(Structure):
     _fields_ = [("x", c_void_p), ("out", c_void_p), ("dw_w", c_void_p * 2), ("dw_b", c_void_p * 2),
                 ("dw_k", c_int32), ("reserved", c_int32), ("stage", EsmSmixStage * 4),
-                ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32)]
+                ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32),
+                ("conv0_w", c_void_p), ("conv0_b", c_void_p), ("conv2_w", c_void_p), ("conv2_b", c_void_p),
+                ("hid", c_int32), ("reserved2", c_int32)]
 
 
 class EsmShuffleTailDesc(Structure):

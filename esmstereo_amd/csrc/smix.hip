@@ -218,36 +218,45 @@ int launch_c(const esm_smix_desc& a, hipStream_t s) {
 // halo and t2 on the tile plus an R halo (each zero outside the image: the depthwise convs' zero
 // padding), then the output.  Per pixel and channel the operations and their order are those of
 // smix_kernel (equal to the three-launch chain up to the compiler's FMA contraction choices).
-constexpr int kFTH = 4;
 constexpr int kFTW = 16;
-// 512 threads: the t1 region (4 + 12) x (16 + 12) = 448 pixels and the t2 region (220) are one pass each
-// (with 256 threads the t1 pass ran twice), the depthwise phases take half the iterations
+// 512 threads: the t1 region is one pass (448 / 480 pixels), the t2 region one pass, the depthwise
+// phases half the iterations of a 256-thread workgroup
 constexpr int kFThreads = 512;
 
-template <int C, int K>
+// CONV: FMBlock.conv fused behind net (shufflemixer.py:124-131): out = conv2(silu(conv0(t3) + b0)) + b2
+// + t3, t3 = net(x) + x.  conv0 is 3x3 zero-padded, so t3 is computed on the tile plus a 1-pixel ring
+// (zero outside the image) and kept in LDS; the tile is 2 x 16 so that the t1 region (2 + 2 + 12) x
+// (16 + 2 + 12) = 480 pixels stays one pass.  HID = conv0's output channels (dim + 16).
+template <int C, int K, bool CONV, int HID>
 __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
     using Lyt = SmixLayout<C>;
     constexpr int R = K / 2;
-    constexpr int AH = kFTH + 4 * R, AW = kFTW + 4 * R, AP = AH * AW;  // t1 region
-    constexpr int BH = kFTH + 2 * R, BW = kFTW + 2 * R, BP = BH * BW;  // t2 region
-    constexpr int CP = kFTH * kFTW;                                      // output tile
+    constexpr int TH = CONV ? 2 : 4, TW = kFTW;                        // output tile
+    constexpr int HC = CONV ? 1 : 0;                                    // t3 ring for conv0
+    constexpr int CH = TH + 2 * HC, CW = TW + 2 * HC, CP = CH * CW;    // t3 region
+    constexpr int BH = CH + 2 * R, BW = CW + 2 * R, BP = BH * BW;      // t2 region
+    constexpr int AH = CH + 4 * R, AW = CW + 4 * R, AP = AH * AW;      // t1 region
     constexpr int AWP = AW + 1, BWP = BW + 1;
     constexpr int DW0 = 4 * Lyt::STAGE, DW1 = DW0 + C * K * K + C;
-    constexpr int NW = DW1 + C * K * K + C;
+    constexpr int CV0 = DW1 + C * K * K + C;                            // conv0 w [HID][C][9], b [HID]
+    constexpr int CV2 = CV0 + (CONV ? HID * C * 9 + HID : 0);           // conv2 w [C][HID], b [C]
+    constexpr int NW = CV2 + (CONV ? C * HID + C : 0);
+    static_assert(AP <= kFThreads, "one t1 pixel per thread");
     __shared__ float wsh[NW];
     __shared__ float s1[C * AH * AWP];  // t1 image, then t2 image ([C][BH][BWP])
-    __shared__ float s2[C * BP];        // depthwise results: region B, then the tile
+    __shared__ float s2[C * BP];        // depthwise results: region B, then region C
+    __shared__ float s3[CONV ? C * CP : 1];           // t3 on region C
+    __shared__ float sh[CONV ? HID * TH * TW : 1];    // silu(conv0(t3)) on the tile
     const int tid = threadIdx.x;
     const int H = a.H, W = a.W;
     const int b = blockIdx.z;
-    const int y0 = blockIdx.y * kFTH, x0 = blockIdx.x * kFTW;
+    const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
 
-    // one round trip for everything this workgroup reads from memory: its t1 pixel (AP <= kFThreads:
-    // one per thread) and every weight (stage s = ln | fc0_w | fc0_b | fc2_w | fc2_b for s = 0..3,
-    // then dw0 w, b, dw1 w, b), all loads issued before the first LDS store
-    static_assert(AP <= kFThreads, "one t1 pixel per thread");
+    // one round trip for everything this workgroup reads from memory: its t1 pixel and every weight
+    // (stage s = ln | fc0_w | fc0_b | fc2_w | fc2_b for s = 0..3, dw0 w, b, dw1 w, b[, conv0 w, b, conv2 w, b]),
+    // all loads issued before the first LDS store
     constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
     float rw[NWR];
 #pragma unroll
@@ -260,18 +269,26 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             const int j = i % Lyt::STAGE;
             p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
             off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
-        } else if (i < NW) {
+        } else if (i < CV0) {
             const int l = i < DW1 ? 0 : 1;
             const int j = i - (l ? DW1 : DW0);
             p = j < C * K * K ? a.dw_w[l] : a.dw_b[l];
             off = j < C * K * K ? j : j - C * K * K;
+        } else if (CONV && i < CV2) {
+            const int j = i - CV0;
+            p = j < HID * C * 9 ? a.conv0_w : a.conv0_b;
+            off = j < HID * C * 9 ? j : j - HID * C * 9;
+        } else if (CONV && i < NW) {
+            const int j = i - CV2;
+            p = j < C * HID ? a.conv2_w : a.conv2_b;
+            off = j < C * HID ? j : j - C * HID;
         }
         const float v = (p ? p : a.x)[p ? off : 0];  // unconditional load, then select
         rw[k] = p ? v : 0.f;
     }
     const int q = tid;  // this thread's t1 pixel (region A)
     const int aly = q / AW, alx = q - (q / AW) * AW;
-    const int agy = y0 - 2 * R + aly, agx = x0 - 2 * R + alx;
+    const int agy = y0 - HC - 2 * R + aly, agx = x0 - HC - 2 * R + alx;
     const bool ain = q < AP && agy >= 0 && agy < H && agx >= 0 && agx < W;
     float t1[C];
 #pragma unroll
@@ -307,7 +324,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
     for (int p = tid; p < BP; p += kFThreads) {
         const int py = p / BW, px = p - (p / BW) * BW;
-        const int gy = y0 - R + py, gx = x0 - R + px;
+        const int gy = y0 - HC - R + py, gx = x0 - HC - R + px;
         const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
         float t[C];
 #pragma unroll
@@ -320,10 +337,10 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
     }
     __syncthreads();
-    // dw1 (t2) on the tile
+    // dw1 (t2) on region C
     for (int i = tid; i < C * CP; i += kFThreads) {
         const int c = i / CP, p = i - (i / CP) * CP;
-        const int py = p / kFTW, px = p - (p / kFTW) * kFTW;
+        const int py = p / CW, px = p - (p / CW) * CW;
         const float* w = wsh + DW1 + c * K * K;
         float sacc = 0.f;
 #pragma unroll
@@ -333,20 +350,69 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         s2[c * CP + p] = sacc + wsh[DW1 + C * K * K + c];
     }
     __syncthreads();
-    // out = SMLayer1.mlp2 (dw1) + x on the tile
-    if (tid >= CP) return;
-    const int py = tid / kFTW, px = tid - (tid / kFTW) * kFTW;
-    const int y = y0 + py, x = x0 + px;
-    if (y >= H || x >= W) return;
-    float t[C];
+    // t3 = SMLayer1.mlp2 (dw1) + x on region C
+    if constexpr (!CONV) {
+        if (tid >= CP) return;
+        const int py = tid / CW, px = tid - (tid / CW) * CW;
+        const int y = y0 + py, x = x0 + px;
+        if (y >= H || x >= W) return;
+        float t[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
-    mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
-    const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
+        for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
+        mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
+        const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
 #pragma unroll
-    for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
+        for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
 #pragma unroll
-    for (int c = 0; c < C; ++c) a.out[pix + c * plane] = t[c];
+        for (int c = 0; c < C; ++c) a.out[pix + c * plane] = t[c];
+    } else {
+        if (tid < CP) {
+            const int py = tid / CW, px = tid - (tid / CW) * CW;
+            const int y = y0 - HC + py, x = x0 - HC + px;
+            const bool in = y >= 0 && y < H && x >= 0 && x < W;
+            float t[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
+            if (in) {
+                mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
+                const long long pix = static_cast<long long>(y) * W + x;
+#pragma unroll
+                for (int c = 0; c < C; ++c) t[c] += xb[pix + c * plane];
+            }
+            // conv0 pads t3 with zeros outside the image
+#pragma unroll
+            for (int c = 0; c < C; ++c) s3[c * CP + tid] = in ? t[c] : 0.f;
+        }
+        __syncthreads();
+        // h = silu(conv0(t3) + b0) on the tile: (hidden channel, pixel) items
+        for (int i = tid; i < HID * TH * TW; i += kFThreads) {
+            const int hc = i / (TH * TW), p = i - hc * (TH * TW);
+            const int py = p / TW, px = p - (p / TW) * TW;
+            const float* w = wsh + CV0 + hc * C * 9;
+            float sacc = 0.f;
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) sacc += w[(c * 3 + ky) * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
+            sh[hc * TH * TW + p] = silu(sacc + wsh[CV0 + HID * C * 9 + hc]);
+        }
+        __syncthreads();
+        // out = conv2(h) + b2 + t3 on the tile: (channel, pixel) items
+        for (int i = tid; i < C * TH * TW; i += kFThreads) {
+            const int c = i / (TH * TW), p = i - c * (TH * TW);
+            const int py = p / TW, px = p - (p / TW) * TW;
+            const int y = y0 + py, x = x0 + px;
+            if (y >= H || x >= W) continue;
+            const float* w = wsh + CV2 + c * HID;
+            float sacc = 0.f;
+#pragma unroll
+            for (int hc = 0; hc < HID; ++hc) sacc += w[hc] * sh[hc * TH * TW + p];
+            const float v = sacc + wsh[CV2 + C * HID + c] + s3[(c * CH + py + HC) * CW + px + HC];
+            a.out[static_cast<long long>(b) * C * plane + c * plane + static_cast<long long>(y) * W + x] = v;
+        }
+    }
 }
 
 }  // namespace
@@ -383,12 +449,17 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
         set_error("fmnet: depthwise kernel must be 7 (FMBlock kernel_size)");
         return ESM_ERR_UNSUPPORTED;
     }
-    const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, kFTH), a.B);
-    if (a.C == 8)
-        hipLaunchKernelGGL((fmnet_kernel<8, 7>), grid, dim3(kFThreads), 0, s, a);
-    else if (a.C == 16)
-        hipLaunchKernelGGL((fmnet_kernel<16, 7>), grid, dim3(kFThreads), 0, s, a);
-    else {
+    const bool conv = a.conv0_w != nullptr;
+    if (conv && (!a.conv0_b || !a.conv2_w || !a.conv2_b || a.hid != a.C + 16))
+        return arg_error("fmnet: the fused FMBlock.conv needs conv0/conv2 weights and biases, hid = C + 16");
+    const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, conv ? 2 : 4), a.B);
+    if (a.C == 8) {
+        if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24>), grid, dim3(kFThreads), 0, s, a);
+        else hipLaunchKernelGGL((fmnet_kernel<8, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
+    } else if (a.C == 16) {
+        if (conv) hipLaunchKernelGGL((fmnet_kernel<16, 7, true, 32>), grid, dim3(kFThreads), 0, s, a);
+        else hipLaunchKernelGGL((fmnet_kernel<16, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
+    } else {
         set_error("fmnet: C must be 8 or 16");
         return ESM_ERR_UNSUPPORTED;
     }

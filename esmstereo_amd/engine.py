@@ -665,13 +665,18 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
 # and staged weights and pixels in serial round trips); on 512 threads with one staging round trip
 # it takes the S-K step from 369.5 to 362.3 us (three rotations on one box).
 FMNET_ENABLED = os.environ.get("ESM_FMNET", "1") != "0"
+# ... and FMBlock.conv (3x3 + SiLU, 1x1, + residual) fused behind it: the whole block in one launch
+# (ESM_FMBLOCK=0: net fused, conv as the separate pair launch)
+FMBLOCK_FUSED = os.environ.get("ESM_FMBLOCK", "1") != "0"
 
 
 def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
               dw1: Tuple[torch.Tensor, torch.Tensor], out: Optional[torch.Tensor] = None,
-              tag: str = "fmnet") -> torch.Tensor:
+              tag: str = "fmnet", conv: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
     """``FMBlock.net(x) + x`` (shufflemixer.py:129-130) in one launch: stages = SMLayer0.mlp1, .mlp2,
-    SMLayer1.mlp1, .mlp2; dw0 / dw1 = the two SMLayers' depthwise convs (weight, bias)."""
+    SMLayer1.mlp1, .mlp2; dw0 / dw1 = the two SMLayers' depthwise convs (weight, bias).  With ``conv`` =
+    (conv0 weight [C+16, C, 3, 3], bias, conv2 weight [C, C+16, 1, 1], bias) the whole FMBlock
+    (shufflemixer.py:129-131: ``t = net(x) + x; conv(t) + t``) is the one launch."""
     require_device(x, "fmnet input")
     if not x.is_contiguous():
         raise ValueError("fmnet: input must be contiguous")
@@ -695,6 +700,18 @@ def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple
         d.stage[i].fc2_w, d.stage[i].fc2_b = st.fc2_w.data_ptr(), st.fc2_b.data_ptr()
         ctx.hold(st.ln_w, st.fc0_w, st.fc0_b, st.fc2_w, st.fc2_b)
     d.B, d.C, d.H, d.W = B, C, H, W
+    if conv is not None:
+        w0, b0, w2, b2 = conv
+        hid = int(w0.shape[0])
+        if tuple(w0.shape) != (hid, C, 3, 3) or tuple(w2.shape[:2]) != (C, hid) or hid != C + 16:
+            raise ValueError("fmnet: FMBlock.conv must be Conv2d(C, C+16, 3) and Conv2d(C+16, C, 1)")
+        for t in conv:
+            if not t.is_contiguous():
+                raise ValueError("fmnet: conv weights must be contiguous")
+        require_on(x.device, "fmnet conv", *conv)
+        d.conv0_w, d.conv0_b, d.conv2_w, d.conv2_b = (t.data_ptr() for t in conv)
+        d.hid = hid
+        ctx.hold(*conv)
     ctx.hold(x, out, *dw0, *dw1)
     npix = B * H * W
     ctx.meta.append(dict(name=tag, kind="fmnet", flops=npix * (2 * C * C * 4 + 2 * 2 * C * d.dw_k ** 2),

@@ -18,8 +18,8 @@ from typing import List
 import torch
 import torch.nn as nn
 
-from .engine import (ACT_NONE, ACT_SILU, FMNET_ENABLED, Ctx, SmixStage, pack_conv, param_token, run_conv_pair,
-                     run_fmnet, run_smix)
+from .engine import (ACT_NONE, ACT_SILU, FMBLOCK_FUSED, FMNET_ENABLED, Ctx, SmixStage, pack_conv, param_token,
+                     run_conv_pair, run_fmnet, run_smix)
 
 __all__ = ["BiasFree_LayerNorm", "LayerNorm", "SplitPointMlp", "SMLayer", "FMBlock"]
 
@@ -110,14 +110,22 @@ class FMBlock(nn.Module):
             l0, l1 = self.net[0], self.net[1]
             a1, a2 = l0.stages()
             b1, b2 = l1.stages()
-            self._esm = (tok, dict(a1=a1, a2=a2, b1=b1, b2=b2, dw0=l0.dw(), dw1=l1.dw(),
-                                   c0=pack_conv(self.conv[0], act=ACT_SILU), c2=pack_conv(self.conv[2], act=ACT_NONE)))
+            c0, c2 = self.conv[0], self.conv[2]
+            cw = None
+            if c0.bias is not None and c2.bias is not None and c0.out_channels == c0.in_channels + 16:
+                cw = tuple(t.detach().float().contiguous() for t in (c0.weight, c0.bias, c2.weight, c2.bias))
+            self._esm = (tok, dict(a1=a1, a2=a2, b1=b1, b2=b2, dw0=l0.dw(), dw1=l1.dw(), cw=cw,
+                                   c0=pack_conv(c0, act=ACT_SILU), c2=pack_conv(c2, act=ACT_NONE)))
         return self._esm[1]
 
     def emit(self, ctx: Ctx, x: torch.Tensor) -> torch.Tensor:
         p = self._packed()
         me = getattr(self, "_esm_name", "FMBlock")
         if FMNET_ENABLED and int(x.shape[1]) in (8, 16) and int(p["dw0"][0].shape[-1]) == 7:
+            if FMBLOCK_FUSED and p["cw"] is not None:
+                # the whole block (net + x, then conv + residual) as one launch
+                return run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"],
+                                 tag=f"{me}")
             # the two SMLayers + x as one launch (the same operations as the three below)
             t3 = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], tag=f"{me}.net")
         else:

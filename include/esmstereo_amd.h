@@ -183,6 +183,15 @@ typedef struct {
     int32_t reserved;
     esm_smix_stage stage[4];
     int32_t B, C, H, W;
+    /* optional, conv0_w != NULL: FMBlock.conv fused behind net (shufflemixer.py:124-131), out =
+     * conv2(silu(conv0(t) + conv0_b)) + conv2_b + t with t = net(x) + x; conv0_w [hid][C][3][3] (zero
+     * padding 1), conv0_w/b [hid], conv2_w [C][hid], conv2_b [C]; hid = C + 16 */
+    const float* conv0_w;
+    const float* conv0_b;
+    const float* conv2_w;
+    const float* conv2_b;
+    int32_t hid;
+    int32_t reserved2;
 } esm_fmnet_desc;
 
 /* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,

@@ -905,6 +905,11 @@ def test_fmnet_fused_bitwise(C, H, W):
     t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"])
     t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x)
     assert rel(fused, t3) < 1e-6
+    # the whole block in one launch (FMBlock.conv fused behind net) vs net + the conv pair launch
+    from esmstereo_amd.engine import run_conv_pair
+    whole = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"])
+    ref = run_conv_pair(ctx, p["c0"], [t3], p["c2"], res=t3)
+    assert rel(whole, ref) < 1e-5
 
 
 @pytest.mark.parametrize("cout,k,s,p,H,W", [(16, 3, 2, 1, 384, 1248), (16, 5, 1, 0, 96, 312), (32, 5, 1, 0, 37, 50),
