@@ -26,9 +26,13 @@ struct SmixLayout {
     static constexpr int STAGE = F2B + H2;  // floats per stage
 };
 
+// One LN -> SplitPointMlp -> shuffle -> residual stage on a pixel's C channels.  The weights come
+// either from LDS (smix_kernel) or straight from global memory through wave-uniform addresses
+// (fmnet_kernel: the compiler turns them into scalar loads, no LDS read per weight).
 template <int C>
-__device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict__ w) {
-    using Lyt = SmixLayout<C>;
+__device__ __forceinline__ void mix_stage_w(float (&t)[C], const float* __restrict__ ln_w, const float* __restrict__ fc0_w,
+                                            const float* __restrict__ fc0_b, const float* __restrict__ fc2_w,
+                                            const float* __restrict__ fc2_b) {
     constexpr int H2 = C / 2;
     constexpr int DD = C / 8;
     float mu = 0.f;
@@ -47,21 +51,21 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict
     const float inv = __builtin_amdgcn_rsqf(var + 1e-5f);
     float n[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) * inv * w[Lyt::LN + c];
+    for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) * inv * ln_w[c];
     float h[C];
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-        float s = w[Lyt::F0B + j];
+        float s = fc0_b[j];
 #pragma unroll
-        for (int i = 0; i < H2; ++i) s += w[Lyt::F0W + j * H2 + i] * n[i];
+        for (int i = 0; i < H2; ++i) s += fc0_w[j * H2 + i] * n[i];
         h[j] = silu_fast(s);
     }
     float cat[C];
 #pragma unroll
     for (int i = 0; i < H2; ++i) {
-        float s = w[Lyt::F2B + i];
+        float s = fc2_b[i];
 #pragma unroll
-        for (int j = 0; j < C; ++j) s += w[Lyt::F2W + i * C + j] * h[j];
+        for (int j = 0; j < C; ++j) s += fc2_w[i * C + j] * h[j];
         cat[i] = s;
     }
 #pragma unroll
@@ -74,6 +78,17 @@ __device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict
         for (int d = 0; d < DD; ++d) o[d * 8 + g] = cat[g * DD + d] + t[d * 8 + g];
 #pragma unroll
     for (int c = 0; c < C; ++c) t[c] = o[c];
+}
+
+template <int C>
+__device__ __forceinline__ void mix_stage(float (&t)[C], const float* __restrict__ w) {
+    using Lyt = SmixLayout<C>;
+    mix_stage_w<C>(t, w + Lyt::LN, w + Lyt::F0W, w + Lyt::F0B, w + Lyt::F2W, w + Lyt::F2B);
+}
+
+template <int C>
+__device__ __forceinline__ void mix_stage_g(float (&t)[C], const esm_smix_stage& g) {
+    mix_stage_w<C>(t, g.ln_w, g.fc0_w, g.fc0_b, g.fc2_w, g.fc2_b);
 }
 
 template <int C, int K>
@@ -227,9 +242,46 @@ constexpr int kFThreads = 512;
 // + t3, t3 = net(x) + x.  conv0 is 3x3 zero-padded, so t3 is computed on the tile plus a 1-pixel ring
 // (zero outside the image) and kept in LDS; the tile is 2 x 16 so that the t1 region (2 + 2 + 12) x
 // (16 + 2 + 12) = 480 pixels stays one pass.  HID = conv0's output channels (dim + 16).
+// Depthwise K x K (+ bias) of an OH x OW region, reading the [C][SH][SWP] LDS image `src` (row r
+// of the region reads source rows r .. r + K - 1), into dst [C][OH * OW].  A wave owns a channel
+// (wave-uniform: its K*K weights and bias are scalar loads from global memory) and a lane owns SEG
+// consecutive outputs of a row, so each source value read from LDS feeds up to K outputs.  Per output
+// the products are summed over ky, then kx, as in smix_kernel.  Lanes of the last segment of a row
+// compute (and drop) up to SEG - 1 outputs past OW: src needs SEG + K - 2 floats of slack at its end.
+template <int C, int K, int OH, int OW, int SH, int SWP, int SEG>
+__device__ __forceinline__ void dw_region(const float* src, float* dst, const float* __restrict__ gw,
+                                          const float* __restrict__ gb, int wave, int lane) {
+    constexpr int NSEG = (OW + SEG - 1) / SEG;
+    constexpr int ITEMS = OH * NSEG;
+    constexpr int NWAVES = kFThreads / 64;
+    for (int c = wave; c < C; c += NWAVES) {
+        const float* w = gw + c * K * K;
+        const float bias = gb[c];
+        for (int it = lane; it < ITEMS; it += 64) {
+            const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
+            float acc[SEG];
+#pragma unroll
+            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                float row[SEG + K - 1];
+                const float* sr = src + (c * SH + py + ky) * SWP + px0;
+#pragma unroll
+                for (int j = 0; j < SEG + K - 1; ++j) row[j] = sr[j];
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * K + kx] * row[j + kx];
+            }
+#pragma unroll
+            for (int j = 0; j < SEG; ++j)
+                if (px0 + j < OW) dst[c * OH * OW + py * OW + px0 + j] = acc[j] + bias;
+        }
+    }
+}
+
 template <int C, int K, bool CONV, int HID>
 __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
-    using Lyt = SmixLayout<C>;
     constexpr int R = K / 2;
     constexpr int TH = CONV ? 2 : 4, TW = kFTW;                        // output tile
     constexpr int HC = CONV ? 1 : 0;                                    // t3 ring for conv0
@@ -237,55 +289,26 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int BH = CH + 2 * R, BW = CW + 2 * R, BP = BH * BW;      // t2 region
     constexpr int AH = CH + 4 * R, AW = CW + 4 * R, AP = AH * AW;      // t1 region
     constexpr int AWP = AW + 1, BWP = BW + 1;
-    constexpr int DW0 = 4 * Lyt::STAGE, DW1 = DW0 + C * K * K + C;
-    constexpr int CV0 = DW1 + C * K * K + C;                            // conv0 w [HID][C][9], b [HID]
-    constexpr int CV2 = CV0 + (CONV ? HID * C * 9 + HID : 0);           // conv2 w [C][HID], b [C]
-    constexpr int NW = CV2 + (CONV ? C * HID + C : 0);
+    constexpr int SEG = 4;
+    constexpr int SLACK = SEG + K;                                      // dw_region's over-read
+    constexpr int NWAVES = kFThreads / 64;
+    constexpr int NPX = TH * TW;
     static_assert(AP <= kFThreads, "one t1 pixel per thread");
-    __shared__ float wsh[NW];
-    __shared__ float s1[C * AH * AWP];  // t1 image, then t2 image ([C][BH][BWP])
-    __shared__ float s2[C * BP];        // depthwise results: region B, then region C
+    static_assert(!CONV || (HID % NWAVES == 0 && NPX <= 64), "conv0: HID / 8 hidden channels per wave, one pixel per lane");
+    // Weights are never staged: every weight index below is wave-uniform, so they are scalar loads
+    // (the LDS then only carries activations: one read per operand of the depthwise / 3x3 convs)
+    __shared__ float s1[C * AH * AWP + SLACK];  // t1 image, then t2 image ([C][BH][BWP])
+    __shared__ float s2[C * BP];                // depthwise results: region B, then region C
     __shared__ float s3[CONV ? C * CP : 1];           // t3 on region C
-    __shared__ float sh[CONV ? HID * TH * TW : 1];    // silu(conv0(t3)) on the tile
+    __shared__ float sh[CONV ? HID * NPX : 1];        // silu(conv0(t3)) on the tile
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
     const int H = a.H, W = a.W;
     const int b = blockIdx.z;
     const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
 
-    // one round trip for everything this workgroup reads from memory: its t1 pixel and every weight
-    // (stage s = ln | fc0_w | fc0_b | fc2_w | fc2_b for s = 0..3, dw0 w, b, dw1 w, b[, conv0 w, b, conv2 w, b]),
-    // all loads issued before the first LDS store
-    constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
-    float rw[NWR];
-#pragma unroll
-    for (int k = 0; k < NWR; ++k) {
-        const int i = tid + k * kFThreads;
-        const float* p = nullptr;
-        int off = 0;
-        if (i < DW0) {
-            const esm_smix_stage& g = a.stage[i / Lyt::STAGE];
-            const int j = i % Lyt::STAGE;
-            p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
-            off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
-        } else if (i < CV0) {
-            const int l = i < DW1 ? 0 : 1;
-            const int j = i - (l ? DW1 : DW0);
-            p = j < C * K * K ? a.dw_w[l] : a.dw_b[l];
-            off = j < C * K * K ? j : j - C * K * K;
-        } else if (CONV && i < CV2) {
-            const int j = i - CV0;
-            p = j < HID * C * 9 ? a.conv0_w : a.conv0_b;
-            off = j < HID * C * 9 ? j : j - HID * C * 9;
-        } else if (CONV && i < NW) {
-            const int j = i - CV2;
-            p = j < C * HID ? a.conv2_w : a.conv2_b;
-            off = j < C * HID ? j : j - C * HID;
-        }
-        const float v = (p ? p : a.x)[p ? off : 0];  // unconditional load, then select
-        rw[k] = p ? v : 0.f;
-    }
     const int q = tid;  // this thread's t1 pixel (region A)
     const int aly = q / AW, alx = q - (q / AW) * AW;
     const int agy = y0 - HC - 2 * R + aly, agx = x0 - HC - 2 * R + alx;
@@ -296,30 +319,15 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         const float v = xb[ain ? c * plane + agy * W + agx : 0];
         t1[c] = ain ? v : 0.f;
     }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < NWR; ++k)
-        if (tid + k * kFThreads < NW) wsh[tid + k * kFThreads] = rw[k];
-    __syncthreads();
     // t1 = SMLayer0.mlp1 (x) on region A
     if (q < AP) {
-        if (ain) mix_stage<C>(t1, wsh);
+        if (ain) mix_stage_g<C>(t1, a.stage[0]);
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
     __syncthreads();
     // dw0 (t1) on region B
-    for (int i = tid; i < C * BP; i += kFThreads) {
-        const int c = i / BP, p = i - (i / BP) * BP;
-        const int py = p / BW, px = p - (p / BW) * BW;
-        const float* w = wsh + DW0 + c * K * K;
-        float sacc = 0.f;
-#pragma unroll
-        for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < K; ++kx) sacc += w[ky * K + kx] * s1[(c * AH + py + ky) * AWP + px + kx];
-        s2[c * BP + p] = sacc + wsh[DW0 + C * K * K + c];
-    }
+    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, a.dw_w[0], a.dw_b[0], wave, lane);
     __syncthreads();
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
     for (int p = tid; p < BP; p += kFThreads) {
@@ -330,25 +338,15 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * BP + p];
         if (in) {
-            mix_stage<C>(t, wsh + Lyt::STAGE);
-            mix_stage<C>(t, wsh + 2 * Lyt::STAGE);
+            mix_stage_g<C>(t, a.stage[1]);
+            mix_stage_g<C>(t, a.stage[2]);
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
     }
     __syncthreads();
     // dw1 (t2) on region C
-    for (int i = tid; i < C * CP; i += kFThreads) {
-        const int c = i / CP, p = i - (i / CP) * CP;
-        const int py = p / CW, px = p - (p / CW) * CW;
-        const float* w = wsh + DW1 + c * K * K;
-        float sacc = 0.f;
-#pragma unroll
-        for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < K; ++kx) sacc += w[ky * K + kx] * s1[(c * BH + py + ky) * BWP + px + kx];
-        s2[c * CP + p] = sacc + wsh[DW1 + C * K * K + c];
-    }
+    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, a.dw_w[1], a.dw_b[1], wave, lane);
     __syncthreads();
     // t3 = SMLayer1.mlp2 (dw1) + x on region C
     if constexpr (!CONV) {
@@ -359,7 +357,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         float t[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
-        mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
+        mix_stage_g<C>(t, a.stage[3]);
         const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
@@ -374,7 +372,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
             for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
             if (in) {
-                mix_stage<C>(t, wsh + 3 * Lyt::STAGE);
+                mix_stage_g<C>(t, a.stage[3]);
                 const long long pix = static_cast<long long>(y) * W + x;
 #pragma unroll
                 for (int c = 0; c < C; ++c) t[c] += xb[pix + c * plane];
@@ -384,33 +382,47 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             for (int c = 0; c < C; ++c) s3[c * CP + tid] = in ? t[c] : 0.f;
         }
         __syncthreads();
-        // h = silu(conv0(t3) + b0) on the tile: (hidden channel, pixel) items
-        for (int i = tid; i < HID * TH * TW; i += kFThreads) {
-            const int hc = i / (TH * TW), p = i - hc * (TH * TW);
-            const int py = p / TW, px = p - (p / TW) * TW;
-            const float* w = wsh + CV0 + hc * C * 9;
-            float sacc = 0.f;
+        // h = silu(conv0(t3) + b0) on the tile: a wave owns HID / 8 hidden channels (scalar weight
+        // loads), a lane one pixel; each t3 value read from LDS feeds all of the wave's channels
+        constexpr int HPW = HID / NWAVES;
+        if (lane < NPX) {
+            const int py = lane / TW, px = lane - (lane / TW) * TW;
+            float acc[HPW];
+#pragma unroll
+            for (int j = 0; j < HPW; ++j) acc[j] = 0.f;
+            const float* w0 = a.conv0_w + wave * HPW * C * 9;
 #pragma unroll
             for (int c = 0; c < C; ++c)
 #pragma unroll
                 for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) sacc += w[(c * 3 + ky) * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
-            sh[hc * TH * TW + p] = silu(sacc + wsh[CV0 + HID * C * 9 + hc]);
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const float v = s3[(c * CH + py + ky) * CW + px + kx];
+#pragma unroll
+                        for (int j = 0; j < HPW; ++j) acc[j] += w0[(j * C + c) * 9 + ky * 3 + kx] * v;
+                    }
+#pragma unroll
+            for (int j = 0; j < HPW; ++j) {
+                const int hc = wave * HPW + j;
+                sh[hc * NPX + lane] = silu(acc[j] + a.conv0_b[hc]);
+            }
         }
         __syncthreads();
-        // out = conv2(h) + b2 + t3 on the tile: (channel, pixel) items
-        for (int i = tid; i < C * TH * TW; i += kFThreads) {
-            const int c = i / (TH * TW), p = i - c * (TH * TW);
-            const int py = p / TW, px = p - (p / TW) * TW;
+        // out = conv2(h) + b2 + t3 on the tile: a wave owns C / 8 output channels, a lane one pixel
+        if (lane < NPX) {
+            const int py = lane / TW, px = lane - (lane / TW) * TW;
             const int y = y0 + py, x = x0 + px;
-            if (y >= H || x >= W) continue;
-            const float* w = wsh + CV2 + c * HID;
-            float sacc = 0.f;
+            if (y < H && x < W) {
 #pragma unroll
-            for (int hc = 0; hc < HID; ++hc) sacc += w[hc] * sh[hc * TH * TW + p];
-            const float v = sacc + wsh[CV2 + C * HID + c] + s3[(c * CH + py + HC) * CW + px + HC];
-            a.out[static_cast<long long>(b) * C * plane + c * plane + static_cast<long long>(y) * W + x] = v;
+                for (int c = wave; c < C; c += NWAVES) {
+                    const float* w = a.conv2_w + c * HID;
+                    float sacc = 0.f;
+#pragma unroll
+                    for (int hc = 0; hc < HID; ++hc) sacc += w[hc] * sh[hc * NPX + lane];
+                    const float v = sacc + a.conv2_b[c] + s3[(c * CH + py + HC) * CW + px + HC];
+                    a.out[static_cast<long long>(b) * C * plane + c * plane + static_cast<long long>(y) * W + x] = v;
+                }
+            }
         }
     }
 }
