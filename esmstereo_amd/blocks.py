@@ -23,8 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token,
-                     run_conv, run_conv_pair, run_shuffle_tail)
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, dmstack_auto, pack_conv, pack_shuffle_tail,
+                     param_token, run_conv, run_conv_pair, run_dmstack, run_shuffle_tail)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -250,9 +250,13 @@ class _ESMUpsampler(nn.Module):
         n = len(self.STAGES)
         for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
             dm = getattr(self, f"dm{tag}")
-            d = dm[0].emit(ctx, [prev])
-            d = _pair(ctx, dm[1], [d], dm[2])
-            d = dm[3].emit(ctx, [d])
+            dml, dmw = [m.packed() for m in dm], [m.conv.weight for m in dm]
+            if dmstack_auto(dml, dmw, prev):
+                d = run_dmstack(ctx, dml, dmw, prev, tag=getattr(dm, "_esm_name", f"{me}.dm{tag}"))
+            else:
+                d = dm[0].emit(ctx, [prev])
+                d = _pair(ctx, dm[1], [d], dm[2])
+                d = dm[3].emit(ctx, [d])
             spx = getattr(self, f"spx_{tag}")
             c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c

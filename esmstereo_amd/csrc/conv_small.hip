@@ -56,9 +56,10 @@ __global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, u
 
     const int Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
-    const int x0 = blockIdx.x * 16;
-    const int ys = blockIdx.y;
-    const int zz = blockIdx.z;
+    const Blk3 bk_ = xcd_block();
+    const int x0 = bk_.x * 16;
+    const int ys = bk_.y;
+    const int zz = bk_.z;
     const int r1 = fast_div(zz, m_ds);
     const int zs = zz - r1 * Ds;
     const int r2 = fast_div(r1, m_b);

@@ -42,9 +42,10 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
     const int n16 = lane & 15, kq = lane >> 4;
     const int kh = KS == 2 ? (wave & 1) : 0;  // which half of the channel groups
     const int gb = kh * NGW;                  // first channel group of this wave
-    const int x0 = (blockIdx.x * (4 / KS) + wave / KS) * 16;
-    const int y0 = blockIdx.y * R;
-    const int b = blockIdx.z;
+    const Blk3 bk_ = xcd_block();
+    const int x0 = (bk_.x * (4 / KS) + wave / KS) * 16;
+    const int y0 = bk_.y * R;
+    const int b = bk_.z;
     const int cob = 0;  // Cout <= 16 * MT: one cout tile
 
     // ---- weights -> VGPRs: w[tap][cin_pad][cout_pad], lane (kq, n16) = k row 4g + kq, cout n16

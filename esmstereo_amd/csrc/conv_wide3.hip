@@ -37,11 +37,12 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
     const int kpart = wave % KSW, zpart = wave / KSW;
-    const int x0 = blockIdx.x * 16;
-    const int y = blockIdx.y;
+    const Blk3 bk_ = xcd_block();
+    const int x0 = bk_.x * 16;
+    const int y = bk_.y;
     const int nzb = (a.Do + ZB - 1) / ZB;
-    const int b = blockIdx.z / nzb;
-    const int z0 = (blockIdx.z - b * nzb) * ZB + zpart * ZW;  // this wave's first output plane
+    const int b = bk_.z / nzb;
+    const int z0 = (bk_.z - b * nzb) * ZB + zpart * ZW;  // this wave's first output plane
 
     // ---- weights of the wave's groups -> VGPRs: w[tap][cin_pad][cout_pad], tap = (dz*3 + dy)*3 + dx
     constexpr int NWS = PZ ? 4 : 3;  // weight sets: tap planes dz (or the pair-relative planes r)
@@ -138,7 +139,7 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
         a.out + b * a.ob, static_cast<short>(0),
         4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
         0x00020000);
-    const int zbase = (blockIdx.z - b * nzb) * ZB;
+    const int zbase = (bk_.z - b * nzb) * ZB;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         const int idx = e * kW3Threads + static_cast<int>(threadIdx.x);  // over (zp, z, j, lane)

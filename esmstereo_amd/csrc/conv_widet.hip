@@ -26,9 +26,10 @@ __global__ void __launch_bounds__(kWtThreads) wtconv_kernel(const esm_conv_desc 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
-    const int x0 = (blockIdx.x * 4 + wave) * 16;  // input-grid column of lane 0
-    const int y0 = blockIdx.y * R;
-    const int b = blockIdx.z;
+    const Blk3 bk_ = xcd_block();
+    const int x0 = (bk_.x * 4 + wave) * 16;  // input-grid column of lane 0
+    const int y0 = bk_.y * R;
+    const int b = bk_.z;
 
     // ---- weights -> VGPRs: packed w[cls][tap][cin_pad][cout_pad], cls = qh*2 + qw, tap = th*2 + tw
     float wv[4][4][NG][MT];

@@ -48,8 +48,9 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
 
     const int tid = threadIdx.x;
     const int H = a.H, W = a.W, HO = H * R, WO = W * R;
-    const int b = blockIdx.z;
-    const int Y0 = blockIdx.y * TH, X0 = blockIdx.x * kTW;
+    const Blk3 bk_ = xcd_block();
+    const int b = bk_.z;
+    const int Y0 = bk_.y * TH, X0 = bk_.x * kTW;
     const int ly0 = Y0 / R - 1, lx0 = X0 / R - 1;  // low-res pixel of lr[.][0][0]
     const float* xb = a.x + b * a.xb;
 

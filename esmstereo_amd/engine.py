@@ -255,6 +255,12 @@ class Ctx:
         else:
             check(lib.esm_fmnet_f32(ctypes.byref(d), self.stream), "fmnet")
 
+    def dmstack(self, d) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_dmstack(self.plan, ctypes.byref(d)), "plan_add_dmstack")
+        else:
+            check(lib.esm_dmstack_f32(ctypes.byref(d), self.stream), "dmstack")
+
     def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
         if self.plan:
             check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
@@ -718,6 +724,61 @@ def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple
                          bytes=4 * npix * C * 2, shape=f"C{C} {H}x{W} dw{d.dw_k} x2",
                          reads=_spans(x), writes=_spans(out)))
     ctx.fmnet(d)
+    return out
+
+
+# The upsamplers' dm<tag> stack (four BasicConv2d) as one launch (esm_dmstack_f32), opt-in with
+# ESM_DMSTACK=1: measured no faster than the four conv launches at S-K / M-K
+DMSTACK_ENABLED = os.environ.get("ESM_DMSTACK", "0") != "0"
+# largest map (H * W) it is used on by default (larger maps run the four conv launches)
+DMSTACK_MAX_PIX = int(os.environ.get("ESM_DMSTACK_MAX_PIX", "2048"))
+
+
+def dmstack_supported(layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor) -> bool:
+    """Whether esm_dmstack_f32 runs ``layers`` (the packed dm<tag> BasicConvs) over ``x``."""
+    if len(layers) != 4 or x.dim() != 4 or int(x.shape[1]) != 1 or x.stride(-1) != 1:
+        return False
+    geo = [(p.nd, p.transposed, p.k, p.stride, p.pad, p.act) for p in layers]
+    if geo != [(2, False, 5, 1, 1, ACT_GELU), (2, False, 3, 1, 1, ACT_GELU), (2, False, 3, 1, 1, ACT_GELU),
+               (2, False, 1, 1, 1, ACT_GELU)]:
+        return False
+    C = layers[0].cout
+    if C != 16 or any(p.cout != C for p in layers) or [p.cin for p in layers] != [1, C, C, C]:
+        return False
+    if any(p.scale is None or p.shift is None for p in layers) or any(not w.is_contiguous() for w in raw):
+        return False
+    return int(x.shape[2]) >= 3 and int(x.shape[3]) >= 3
+
+
+def dmstack_auto(layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor) -> bool:
+    """The hot path's choice: the fused stack where supported and the map is small."""
+    return DMSTACK_ENABLED and dmstack_supported(layers, raw, x) and int(x.shape[2]) * int(x.shape[3]) <= DMSTACK_MAX_PIX
+
+
+def run_dmstack(ctx: Ctx, layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor,
+                tag: str = "dm") -> torch.Tensor:
+    """The dm<tag> stack (ESMStereo.py:250-253: BasicConv k5 p1 1->C, k3 p1, k3 p1, k1 p1, each BN + GELU)
+    over the disparity ``x`` [B, 1, H, W] in one launch; ``raw`` = the four conv weights in PyTorch
+    layout, ``layers`` their packed forms (folded BN scale / shift)."""
+    require_device(x, "dmstack input")
+    if not dmstack_supported(layers, raw, x):
+        raise ValueError("dmstack: unsupported layer stack or input")
+    B, _, H, W = (int(v) for v in x.shape)
+    C = layers[0].cout
+    out = ctx.empty(B, C, H, W)
+    d = _lib.EsmDmstackDesc()
+    d.x, d.xb, d.xh = x.data_ptr(), x.stride(0), x.stride(2)
+    d.out = out.data_ptr()
+    for i, (p, w) in enumerate(zip(layers, raw)):
+        d.w[i], d.scale[i], d.shift[i] = w.data_ptr(), p.scale.data_ptr(), p.shift.data_ptr()
+    require_on(x.device, "dmstack", x, out, *raw, *[t for p in layers for t in (p.scale, p.shift)])
+    d.B, d.C, d.H, d.W = B, C, H, W
+    ctx.hold(x, out, *raw, *[t for p in layers for t in (p.scale, p.shift)])
+    hd, wd = H - 2, W - 2
+    flops = 2 * B * (hd * wd * C * 25 + 2 * hd * wd * C * C * 9 + hd * wd * C * C)
+    ctx.meta.append(dict(name=tag, kind="dmstack", flops=flops, bytes=4 * B * (H * W + C * H * W),
+                         shape=f"dm C{C} {H}x{W}", reads=_spans(x), writes=_spans(out)))
+    ctx.dmstack(d)
     return out
 
 

@@ -19,6 +19,7 @@
  *                             129-509 with their fused neighbours (crop+cat :172,177,230,234;
  *                             PixelShuffle+SiLU :265-268; bilinear-upsample + add :307,316;
  *                             `* att` :703; residual adds of models/shufflemixer.py:130-131)
+ *   esm_dmstack_f32           models/ESMStereo.py:250-253 the upsamplers' dm<tag> stack (four BasicConv2d)
  *   esm_fmnet_f32             models/shufflemixer.py:100-112,129-130 FMBlock.net (two SMLayers) + x
  *   esm_smix_f32              models/shufflemixer.py:23-112 LayerNorm('BiasFree') +
  *                             SplitPointMlp + channel shuffle + residual, optionally preceded
@@ -194,6 +195,21 @@ typedef struct {
     int32_t reserved2;
 } esm_fmnet_desc;
 
+/* The ESM upsamplers' disparity-feature stack dm<tag> (models/ESMStereo.py:250-253): four BasicConv2d
+ * (conv bias=False -> folded BN -> exact GELU) k5 p1 1->C, k3 p1 C->C, k3 p1 C->C, k1 p1 C->C in one
+ * launch (halo recomputation).  x: [B, 1, H, W] with strides xb, xh (innermost 1), H, W >= 3;
+ * out: [B, C, H, W] contiguous; w[l]: the conv weights in PyTorch layout ([C][1][5][5],
+ * [C][C][3][3] x 2, [C][C][1][1]); scale/shift[l]: the folded BN (y = acc * scale + shift).  C = 16. */
+typedef struct {
+    const float* x;
+    int64_t xb, xh;
+    float* out;
+    const float* w[4];
+    const float* scale[4];
+    const float* shift[4];
+    int32_t B, C, H, W;
+} esm_dmstack_desc;
+
 /* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,
  * silu(pixel_shuffle(conv1x1(up_w, x) + up_b, r))), zero padding 1.  (nf, r) in
  * {(8,2), (8,4), (16,2), (16,4)}.  x: [B, nf, H, W] with strides xb, xc, xh (innermost 1);
@@ -214,7 +230,8 @@ typedef struct {
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc;
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc,
+ * 7 esm_dmstack_desc;
  * -1 for an unknown id. */
 int esm_struct_size(int which);
 
@@ -232,6 +249,7 @@ int esm_topk2_regression_f32(const float* cost, const float* samples, float* out
 int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
 int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream);
+int esm_dmstack_f32(const esm_dmstack_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
 /* out_b = epilogue_b(conv_b(epilogue_a(conv_a(src_a)))): `a` describes the first conv (its sources,
  * weights, BN/bias, activation; a->out is not written, a->res must be NULL), `b` the second (its
@@ -290,6 +308,7 @@ void esm_plan_destroy(esm_plan* plan);
 int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
 int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
+int esm_plan_add_dmstack(esm_plan* plan, const esm_dmstack_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
 int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
@@ -303,7 +322,7 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet, 10 = conf */
+ * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet, 10 = conf, 11 = dmstack */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

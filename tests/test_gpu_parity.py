@@ -942,3 +942,42 @@ def test_gelu_epilogue_branch_free_erf():
         assert bool(((y - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all()), hex(hint)
         yt = F.gelu(x.to(DEV)).double().cpu()  # torch's own fp32 GELU meets the same bound
         assert bool(((yt - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all())
+
+
+@pytest.mark.parametrize("B,H,W", [(1, 24, 78), (2, 96, 312), (1, 3, 3), (1, 7, 13), (2, 30, 41)])
+def test_dmstack_fused(B, H, W):
+    """The upsamplers' dm<tag> stack (ESMStereo.py:250-253: BasicConv2d k5 p1 1->16, k3 p1, k3 p1,
+    k1 p1, each BN + GELU) in one launch (esm_dmstack_f32, halo recomputation) vs fp64 torch of the
+    four layers (relative 1e-5, the conv forms' tolerance) and vs the four-launch chain."""
+    from esmstereo_amd.blocks import _dm
+    from esmstereo_amd.engine import dmstack_supported, run_dmstack
+
+    torch.manual_seed(H * 1000 + W)
+    dm = _dm(16).eval()
+    with torch.no_grad():
+        for m in dm:
+            m.conv.weight.uniform_(-0.4, 0.4)
+            m.bn.weight.uniform_(0.5, 1.5)
+            m.bn.bias.uniform_(-0.3, 0.3)
+            m.bn.running_mean.uniform_(-0.2, 0.2)
+            m.bn.running_var.uniform_(0.5, 1.5)
+    x = torch.randn(B, 1, H, W) * 4
+    ref = x.double()
+    with torch.no_grad():
+        for m in dm:
+            c, bn = m.conv, m.bn
+            y = F.conv2d(ref, c.weight.double(), None, c.stride, c.padding)
+            y = F.batch_norm(y, bn.running_mean.double(), bn.running_var.double(), bn.weight.double(),
+                             bn.bias.double(), False, 0.0, bn.eps)
+            ref = F.gelu(y)
+    dm = dm.to(DEV)
+    layers, raw = [m.packed() for m in dm], [m.conv.weight for m in dm]
+    xd = x.to(DEV)
+    assert dmstack_supported(layers, raw, xd)
+    ctx = Ctx(DEV)
+    got = run_dmstack(ctx, layers, raw, xd)
+    torch.cuda.synchronize()
+    assert got.shape == (B, 16, H, W)
+    assert rel(got, ref.float()) < 1e-5
+    chain = dm[3].emit(ctx, [dm[2].emit(ctx, [dm[1].emit(ctx, [dm[0].emit(ctx, [xd])])])])
+    assert rel(got, chain) < 1e-5
