@@ -237,6 +237,10 @@ constexpr int kFTW = 16;
 // 512 threads: the t1 region is one pass (448 / 480 pixels), the t2 region one pass, the depthwise
 // phases half the iterations of a 256-thread workgroup
 constexpr int kFThreads = 512;
+#ifndef ESM_FMBLOCK_TH
+#define ESM_FMBLOCK_TH 2
+#endif
+constexpr int kFConvTH = ESM_FMBLOCK_TH;  // output rows per workgroup of the whole-FMBlock form
 
 // CONV: FMBlock.conv fused behind net (shufflemixer.py:124-131): out = conv2(silu(conv0(t3) + b0)) + b2
 // + t3, t3 = net(x) + x.  conv0 is 3x3 zero-padded, so t3 is computed on the tile plus a 1-pixel ring
@@ -283,7 +287,7 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
 template <int C, int K, bool CONV, int HID>
 __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
     constexpr int R = K / 2;
-    constexpr int TH = CONV ? 2 : 4, TW = kFTW;                        // output tile
+    constexpr int TH = CONV ? kFConvTH : 4, TW = kFTW;                        // output tile
     constexpr int HC = CONV ? 1 : 0;                                    // t3 ring for conv0
     constexpr int CH = TH + 2 * HC, CW = TW + 2 * HC, CP = CH * CW;    // t3 region
     constexpr int BH = CH + 2 * R, BW = CW + 2 * R, BP = BH * BW;      // t2 region
@@ -512,7 +516,7 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
     const bool conv = a.conv0_w != nullptr;
     if (conv && (!a.conv0_b || !a.conv2_w || !a.conv2_b || a.hid != a.C + 16))
         return arg_error("fmnet: the fused FMBlock.conv needs conv0/conv2 weights and biases, hid = C + 16");
-    const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, conv ? 2 : 4), a.B);
+    const dim3 grid(ceil_div(a.W, kFTW), ceil_div(a.H, conv ? kFConvTH : 4), a.B);
     if (a.C == 8) {
         if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24>), grid, dim3(kFThreads), 0, s, a);
         else hipLaunchKernelGGL((fmnet_kernel<8, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
