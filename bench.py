@@ -1,32 +1,33 @@
 """Benchmark: stereo pairs/sec of the ESMStereo hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A "step" is one pass of the hot path (models/ESMStereo.py:700-745: cost volume -> 3-D stems ->
 3-D hourglass -> regression -> ESM/ShuffleMixer upsampler -> x4) over one batch of synthetic
-input that is already resident in HBM: the workload is BASELINE.json configs[1], ESMStereo-S
-(mobilenetv2_100 channel ladder, cv_scale 16, gwc volume) at KITTI 384x1248, maxdisp 192,
-batch 1 per GPU.  The backbone side that produces the matching features is out of scope
- and runs once, before timing.  Each rank processes its own batch (weak
-scaling); with N > 1 the disparity maps are all-gathered over RCCL every step.
+matching features already resident in HBM: by default BASELINE.json configs[1], ESMStereo-S
+(mobilenetv2_100 channel ladder, cv_scale 16, gwc volume) at KITTI 384x1248, maxdisp 192, batch 1
+per GPU.  The backbone side that produces the features is out of scope; the inputs
+are tests/helpers.py fullsize_inputs (at configs[1] exactly the reference fixture's).  Each rank
+runs its own batch (weak scaling; --config 3 splits a global batch: strong); with N > 1 the
+disparity maps are all-gathered over RCCL every step.  The multi-rank loop (shards, gather, barrier,
+max-over-ranks time) is esmstereo_amd.dist, which tests/test_dist.py runs under gloo.
 
 Printed (rank 0, one JSON line): the contract fields, plus
-  roofline      dominant kernel of the step (longest back-to-back launch of the probe's shortlist), its algorithmic
-                FLOPs or bytes / its average duration, measured right after the timed region as
-                K back-to-back launches of that op between one hipEvent pair on its stream
-                (per-launch event pairs are kept as avg_us_event_pair_per_launch), against the
-                fp32 MFMA or HBM peak; traffic = PMC FETCH/WRITE bytes from profiles/;
-  roofline_cost_volume  the gwc cost-volume kernel at KITTI full res for ESMStereo-L
-                (the north_star headline: HBM fraction of the volume kernel);
-  cpu_baseline  the CPU oracle (oracle/esm_oracle.py, PyTorch fp32 on the host cores) timed
-                on a bounded sample of the same workload, rank 0 at N = 1 only;
-  epe_vs_oracle mean |disparity_HIP - disparity_oracle| on the benchmark input (and relative to
-                mean |disparity_oracle|: random-init weights give disparities of thousands of px);
-  concurrent    (N = 1) serving-style side measurement: --streams independent hot-path instances
-                (own buffers and graphs, same batch per instance) replayed concurrently on as many
-                HIP streams.  `value` stays the single-stream rate.
+  roofline        the dominant op: the largest in-graph duration, measured as its marginal cost in
+                  the replayed graph (step minus the step with the op dropped), against the fp32
+                  MFMA or HBM peak by its algorithmic intensity; traffic = PMC bytes from profiles/;
+  roofline_mfma   the same for group_stem (the MFMA-bound 3-D stem);
+  roofline_step   the whole step: sum over ops of max(flops / MFMA peak, bytes / HBM peak) vs the
+                  measured step, and the algorithmic-bytes-only HBM fraction (north_star);
+  roofline_cost_volume  the gwc cost-volume kernel at KITTI full res for ESMStereo-L (cache-proof);
+  cpu_baseline    the CPU oracle (oracle/esm_oracle.py, PyTorch fp32 on the host cores) on a bounded
+                  sample of the same workload, rank 0 at N = 1 only;
+  epe_vs_oracle   mean |disparity_HIP - disparity_oracle| (px) on the benchmark input;
+  epe_vs_reference  the reference's own full-size fixture (tests/golden/full_*.npz);
+  concurrent      (N = 1) --streams independent hot-path instances replayed on as many HIP streams;
+  forward_e2e     (N = 1) model(left, right, False) end to end, backbone included.
 """
 from __future__ import annotations
 
@@ -34,16 +35,18 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import esmstereo_amd as E  # noqa: E402
+from esmstereo_amd import dist as D  # noqa: E402
+from esmstereo_amd._lib import lib  # noqa: E402
 
 VARIANTS = {"S": ("mobilenetv2_100", 16), "M": ("efficientnet_b2", 8), "L": ("efficientnet_b2", 4)}
 METRIC = "stereo pairs/sec at 384×1248 maxdisp=192; EPE vs reference"
@@ -121,34 +124,61 @@ def pmc_traffic(name: str, workload: str):
     return None if e is None else e.get("hbm_bytes_per_launch")
 
 
-def find_dominant(hp: E.HotPath, reps: int = 5, top: int = 6, batch: int = 20) -> tuple:
-    """The step's dominant kernel: per-op hipEvent probes (eager, median of ``reps``) shortlist the
-    ``top`` longest ops; each of those is then timed as ``batch`` back-to-back launches between one
-    event pair (the way the roofline's ``avg_us`` is measured), and the longest wins.  The probes
-    alone carry ~3 us of event overhead per launch, which reorders ops within a few us of each other."""
-    graph = hp.graph
-    hp.graph = False
-    times = []
+def _replay_us(hp: E.HotPath, reps: int) -> float:
+    """us per graph replay over ``reps`` back-to-back replays between one hipEvent pair."""
+    for _ in range(2):
+        hp.launch()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        hp.launch()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+def marginal_costs(hp: E.HotPath, rounds: int = 3, window_ms: float = 6.0) -> tuple:
+    """Each op's duration INSIDE the replayed graph, as its marginal cost: the step time of the graph
+    minus the step time of the same graph with that op dropped (``esm_plan_set_repeat(i, 0)``; the
+    median of ``rounds`` interleaved windows each).  This counts what the op costs the chain: its own
+    device time with the caches the chain leaves it, and its launch boundary.  No event nodes sit in
+    the measured graphs (they perturb the chain).  Returns (per-op us, full step us)."""
+    plan = hp.ctx.plan
+    hp._graph_ready = False
+    base0 = _replay_us(hp, 10)
+    reps = max(8, int(window_ms * 1e3 / base0))
+    base_all, out = [], []
     for i in range(hp.num_ops):
-        hp.set_probe(i, reps + 1)
-        for _ in range(reps + 1):
-            hp.launch()
-        torch.cuda.synchronize()
-        t = sorted(hp.probe_read()[1:])
-        times.append(t[len(t) // 2])
-    hp.set_probe(-1, 1)
-    hp.graph = graph
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    b2b = {}
-    for i in sorted(range(len(times)), key=lambda i: -times[i])[:top]:
-        hp.run_op(i, 3)
-        ev0.record()
-        hp.run_op(i, batch)
-        ev1.record()
-        torch.cuda.synchronize()
-        b2b[i] = ev0.elapsed_time(ev1) / batch
-    dom = max(b2b, key=b2b.get)
-    return dom, times
+        base, drop = [], []
+        for _ in range(rounds):
+            hp._graph_ready = False
+            base.append(_replay_us(hp, reps))
+            lib.esm_plan_set_repeat(plan, i, 0)
+            hp._graph_ready = False
+            drop.append(_replay_us(hp, reps))
+            lib.esm_plan_set_repeat(plan, i, 1)
+        out.append(statistics.median(base) - statistics.median(drop))
+        base_all += base
+    hp._graph_ready = False
+    return out, statistics.median(base_all)
+
+
+def step_roofline(meta: list, step_ms: float, pairs: int) -> dict:
+    """The whole step against the roofs (north_star: pairs/s "as fraction of the HBM roofline"): each
+    op's roof time is max(algorithmic flops / fp32 MFMA peak, algorithmic bytes / HBM peak) and the ops
+    run one after the other (the path's DAG has width 1), so the step's roof time is their sum."""
+    flops = sum(m["flops"] for m in meta)
+    byts = sum(m["bytes"] for m in meta)
+    roof_s = sum(max(m["flops"] / (PEAK_F32_MFMA_TFS * 1e12), m["bytes"] / (PEAK_HBM_GBS * 1e9)) for m in meta)
+    hbm_s = byts / (PEAK_HBM_GBS * 1e9)
+    step_s = step_ms * 1e-3
+    return {"flops_per_pair": round(flops / pairs), "bytes_per_pair": round(byts / pairs),
+            "roof_us_per_step": round(roof_s * 1e6, 2), "roof_pairs_per_s": round(pairs / roof_s, 1),
+            "frac": round(roof_s / step_s, 4),
+            "hbm_roof_pairs_per_s": round(pairs / hbm_s, 1), "hbm_frac": round(hbm_s / step_s, 4),
+            "launches": len(meta),
+            "rule": "sum over ops of max(flops / 157.3 TF/s, bytes / 8 TB/s) vs the measured step; "
+                    "hbm_* = algorithmic bytes only"}
 
 
 INFINITY_CACHE_BYTES = 256 << 20  # MI355X die-level L3 (MI355X_MICROARCH.md)
@@ -316,9 +346,13 @@ def load_seeded_weights(model: torch.nn.Module, variant: str, cv: str) -> None:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import load_spec, seeded_state
 
+    import warnings
+
     sd = seeded_state(load_spec(f"spec_{variant}_{cv}.json"), WEIGHT_SEED[(variant, cv)])
-    missing, unexpected = model.load_state_dict({k: v for k, v in sd.items() if not k.startswith("feature.")},
-                                                strict=False)
+    with warnings.catch_warnings():  # the backbone deliberately keeps its random init here
+        warnings.filterwarnings("ignore", message=".*backbone.*", category=RuntimeWarning)
+        missing, unexpected = model.load_state_dict({k: v for k, v in sd.items() if not k.startswith("feature.")},
+                                                    strict=False)
     assert not unexpected and all(k.startswith("feature.") for k in missing), (missing, unexpected)
 
 
@@ -349,11 +383,58 @@ def epe_vs_reference(model, args, dev):
         init = E.regression_topk(cost, None, 2) if m["cv_scale"] == 4 else \
             E.disparity_regression(cost, D).unsqueeze(1)
         disp0 = model.hot_path(ml, mr, att, up)[0]
-    rep = check_fullsize(name, m, g, cost, init, disp0)
+        d_ref_init = model.upsample_module.emit(E.engine.Ctx(dev), up, T(g["init_pred"]), final_scale=4.0)[0]
+    rep = check_fullsize(name, m, g, cost, init, disp0, disp0_from_ref_init=d_ref_init[:, 0])
     d = rep.get("disp0")
     epe = d["epe_outside_mask"] if d else rep["disp0_sub_epe"]
     return {"epe_px": epe, "fixture": "tests/golden/" + name, "pixels": "every 4th row and column of disp_0",
+            "epe_px_upsampler_on_reference_init": rep["disp0_sub_epe_ref_init"],
             "top2_flips": None if d is None else d["flips"], "cost_rel": max(rep["cost_sample_rel"], rep["cost_l2_rel"])}
+
+
+def bench_inputs(variant: str, cv: str, B: int, H: int, W: int, maxdisp: int, seed: int, dev) -> tuple:
+    """Synthetic hot-path inputs: matching features of a smooth texture with the right
+    view shifted by a planar disparity field inside [0.1, 0.8] x maxdisp, attention weights (S) and
+    smooth upsampler feature maps, as tests/helpers.py fullsize_inputs (the generator of the reference's
+    full-size fixtures: at configs[1] with seed 101 the input IS tests/golden/full_S_gwc_K.npz's)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import fullsize_inputs
+
+    cvs = VARIANTS[variant][1]
+    ml, mr, att, up = fullsize_inputs(cvs, B, H, W, maxdisp, seed, att=cvs == 16)
+    T = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
+    return T(ml), T(mr), T(att), [T(u) for u in up]
+
+
+INPUT_SEED = {1: 101, 2: 201, 3: 102, 4: 401}  # configs[1] / [3]: the reference fixtures' input seeds
+
+
+def forward_e2e(model, args, dev, iters: int = 10) -> dict:
+    """The public forward end to end: ``model(left, right, False)`` on a synthetic
+    image pair, backbone side (PyTorch/MIOpen, out of the hot path) included, plus the host cost of one
+    ``hot_path()`` call on resident features (plan-cache key, input copies, graph launch, output clone)."""
+    left, right = synthetic_pair(args.batch, args.height, args.width, args.maxdisp, 7, dev)
+    with torch.no_grad():
+        for _ in range(2):
+            model(left, right, False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model(left, right, False)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / iters
+        ml, mr, att, up = model.prefix(left, right)
+        model.hot_path(ml, mr, att, up)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model.hot_path(ml, mr, att, up)
+        torch.cuda.synchronize()
+        hp_ms = (time.perf_counter() - t0) / iters * 1e3
+    return {"value": round(args.batch / el, 2), "unit": "pairs/s", "ms_per_forward": round(el * 1e3, 3),
+            "hot_path_call_ms": round(hp_ms, 4),
+            "what": "model(left, right, False) with the random-init backbone; hot_path_call_ms = one "
+                    "model.hot_path() call on resident features, host work included"}
 
 
 def main() -> None:
@@ -375,8 +456,10 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the side measurements (cost-volume rooflines, "
-                    "concurrent streams, EPE vs the reference fixture)")
-    ap.add_argument("--kernel-table", default="", help="write the per-op probe table (json) here")
+                    "concurrent streams, EPE vs the reference fixture, end-to-end forward)")
+    ap.add_argument("--no-marginal", action="store_true", help="skip the per-op in-graph marginal costs (the "
+                    "dominant op is then the longest back-to-back launch)")
+    ap.add_argument("--kernel-table", default="", help="write the per-op table (json) here")
     ap.add_argument("--streams", type=int, default=2,
                     help="side measurement: independent B-pair instances on this many concurrent streams")
     args = ap.parse_args()
@@ -389,31 +472,24 @@ def main() -> None:
         args.batch = cfg.get("batch")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    if args.global_batch is not None:  # strong scaling: the global batch is split over the ranks
-        from esmstereo_amd.dist import shard_range
-
-        if args.global_batch % world:
-            raise SystemExit(f"--global-batch {args.global_batch} must split evenly over {world} GPUs")
-        lo, hi = shard_range(args.global_batch, world, rank)
-        args.batch = hi - lo
-        scaling = "strong"
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    world, rank = D.world_info()
+    if args.global_batch is not None:
+        args.batch, scaling, total_batch = D.local_batch(world, rank, global_batch=args.global_batch)
     else:
-        scaling = "weak"
+        args.batch, scaling, total_batch = D.local_batch(world, rank, batch=args.batch)
 
     backbone, cvs = VARIANTS[args.variant]
     model = E.ESMStereo(args.maxdisp, args.cv == "gwc", args.cv == "nc", backbone, cvs)
-    seeded_init(model, 1234)
+    seeded_init(model, 1234)  # the backbone side (only the end-to-end side measurement runs it)
     load_seeded_weights(model, args.variant, args.cv)
     model = model.eval().to(dev)
-    left, right = synthetic_pair(args.batch, args.height, args.width, args.maxdisp, 100 + rank, dev)
-    with torch.no_grad():
-        ml, mr, att, up = model.prefix(left, right)
+    ml, mr, att, up = bench_inputs(args.variant, args.cv, args.batch, args.height, args.width, args.maxdisp,
+                                   INPUT_SEED.get(args.config, 500) + 1000 * rank, dev)
     B, C, h, w = (int(v) for v in ml.shape)
     hp = E.HotPath(model, B, h, w, 0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], dev,
                    graph=not args.no_graph, channels=C)
@@ -421,98 +497,93 @@ def main() -> None:
     meta = hp.ctx.meta
     assert len(meta) == hp.num_ops, (len(meta), hp.num_ops)
 
-    dom, op_ms = find_dominant(hp)
+    # the dominant op: the longest inside the replayed graph (marginal cost), before the timed region
+    marg = None
+    if hp.graph and not args.no_marginal:
+        marg, _ = marginal_costs(hp)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def b2b_ms(i: int, reps: int) -> float:
+        hp.run_op(i, 3)
+        ev0.record()
+        hp.run_op(i, reps)
+        ev1.record()
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / reps
+
+    if marg is not None:
+        dom = max(range(hp.num_ops), key=lambda i: marg[i])
+    else:
+        dom = max(range(hp.num_ops), key=lambda i: b2b_ms(i, 10))
     if args.kernel_table and rank == 0:
         with open(args.kernel_table, "w") as f:
-            json.dump([dict(m, median_ms=t) for m, t in zip(meta, op_ms)], f, indent=1)
-        # launches after the last whole step (the dominant-kernel batch below), for the
-        # position-based trace mapping of scripts/prof_ops.py / pmc_traffic.py
+            json.dump([dict(m, marginal_us=None if marg is None else round(marg[i], 3))
+                       for i, m in enumerate(meta)], f, indent=1)
+        # the timed region's whole steps, and the launches after them (the dominant op's
+        # back-to-back batch), for the position-based trace mapping of scripts/prof_ops.py / pmc_traffic.py
         with open(args.kernel_table + ".meta.json", "w") as f:
-            json.dump({"trailing_dispatches": 3 + args.steps}, f)
-    # The timed region is the plain plan (a hipGraph): hipEvent-record nodes spliced into the graph
-    # perturb it (measured +110 us per step and +15 us on the probed kernel, disagreeing with
-    # rocprofv3), so the dominant kernel is timed by a hipEvent pair recorded around it on its
-    # stream while the same K steps are replayed eagerly right after the timed region.
-    hp.set_probe(-1, 1)
-    gbuf = None
-    if world > 1 and not args.no_gather:
-        gbuf = torch.empty((world,) + tuple(hp.outputs[0].shape), device=dev)
-    for _ in range(args.warmup):
+            json.dump({"timed_steps": args.steps, "trailing_dispatches": 3 + args.steps}, f)
+
+    # the timed region: the plain plan (one hipGraph per step) + the per-step disparity all-gather
+    gather = D.DisparityGather(hp.outputs[0]) if world > 1 and not args.no_gather else None
+
+    def step():
         hp.launch()
-        if gbuf is not None:
-            dist.all_gather_into_tensor(gbuf, hp.outputs[0])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        hp.launch()
-        if gbuf is not None:
-            dist.all_gather_into_tensor(gbuf, hp.outputs[0])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    graph = hp.graph
-    hp.graph = False
-    hp.set_probe(dom, args.steps + 8)
-    for _ in range(args.steps):
-        hp.launch()
-    torch.cuda.synchronize()
-    ktimes = hp.probe_read()
-    hp.set_probe(-1, 1)
-    hp.graph = graph
-    # the dominant kernel alone, K launches back to back between one hipEvent pair on its stream
-    # (per-launch event pairs add their own overhead to a ~10-40 us kernel)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    hp.run_op(dom, 3)
-    ev0.record()
-    hp.run_op(dom, args.steps)
-    ev1.record()
-    torch.cuda.synchronize()
-    batch_ms = ev0.elapsed_time(ev1) / args.steps
-    probe_mode, probe_error = "back-to-back batch", None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        if gather is not None:
+            gather(hp.outputs[0])
+
+    elapsed = D.timed_steps(step, args.steps, args.warmup, dev)
+    batch_ms = b2b_ms(dom, args.steps)  # the dominant op alone, K launches back to back, warm caches
 
     if rank == 0:
-        pair_kms = sum(ktimes) / max(1, len(ktimes))
-        avg_kms = batch_ms
-        roof = kernel_roofline(meta[dom], avg_kms)
+        ms_step = elapsed / args.steps * 1e3
+        dom_ms = marg[dom] * 1e-3 if marg is not None else batch_ms
+        roof = kernel_roofline(meta[dom], dom_ms)
         workload = f"ESMStereo-{args.variant} {args.cv} {args.height}x{args.width} md{args.maxdisp} B{args.batch}"
         roof.update({"traffic": pmc_traffic(meta[dom]["name"], workload), "kernel": meta[dom]["name"],
-                     "kernel_shape": meta[dom].get("shape", ""), "avg_us": round(avg_kms * 1e3, 2),
-                     "launches_timed": args.steps, "probe": probe_mode, "probe_error": probe_error,
-                     "avg_us_event_pair_per_launch": round(pair_kms * 1e3, 2),
+                     "kernel_shape": meta[dom].get("shape", ""), "avg_us": round(dom_ms * 1e3, 2),
+                     "timing": "marginal cost inside the replayed graph (step time minus the step with this op "
+                               "dropped; median of 3 interleaved windows): the op's in-chain duration incl. its "
+                               "launch boundary" if marg is not None else "back-to-back launches, warm caches",
+                     "avg_us_back_to_back_warm": round(batch_ms * 1e3, 2),
                      "algorithmic_flops_per_launch": meta[dom]["flops"],
                      "algorithmic_bytes_per_launch": meta[dom]["bytes"]})
-        total = args.batch * world * args.steps  # every rank holds the same batch (even split)
         line = {
             "metric": METRIC,
-            "value": round(total / elapsed, 2),
+            "value": round(total_batch * args.steps / elapsed, 2),
             "unit": "pairs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (sinusoid-texture stereo pair, planar disparity; seeded random-init weights, "
-                    "tests/helpers.py seeded_state)",
+            "data": "synthetic (matching features of a smooth texture shifted by a planar disparity field, "
+                    "tests/helpers.py fullsize_inputs; seeded random-init weights, tests/helpers.py seeded_state)",
             "config": {"workload": "hot path: cost volume -> 3D stems -> 3D hourglass -> regression -> "
                                    "ESM upsampler (models/ESMStereo.py:700-745), " + workload,
                        "baseline_config": f"configs[{args.config}]: {cfg['name']}",
-                       "variant": args.variant, "cv": args.cv, "global_batch": args.batch * world,
+                       "variant": args.variant, "cv": args.cv, "global_batch": total_batch,
                        "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                        "parallelism": f"dp{world}", "graph": hp.graph,
                        "launches_per_step": hp.num_ops},
             "roofline": roof,
+            "roofline_step": step_roofline(meta, ms_step, args.batch),
         }
+        mf = [i for i, m in enumerate(meta) if m["name"] == "group_stem"]
+        if mf and marg is not None:
+            r = kernel_roofline(meta[mf[0]], marg[mf[0]] * 1e-3)
+            r.update({"kernel": "group_stem", "kernel_shape": meta[mf[0]].get("shape", ""),
+                      "avg_us": round(marg[mf[0]], 2), "timing": "marginal cost inside the replayed graph",
+                      "avg_us_back_to_back_warm": round(b2b_ms(mf[0], 20) * 1e3, 2),
+                      "traffic": pmc_traffic("group_stem", workload)})
+            line["roofline_mfma"] = r
+        if marg is not None:
+            top = sorted(range(len(marg)), key=lambda i: -marg[i])[:8]
+            line["top_ops_in_graph"] = [{"op": meta[i]["name"], "us": round(marg[i], 2)} for i in top]
+            line["sum_of_marginals_us"] = round(sum(marg), 1)
         if not args.no_extra:
             line["epe_vs_reference"] = epe_vs_reference(model, args, dev)
             line["roofline_cost_volume"] = cost_volume_roofline(dev)
@@ -522,19 +593,19 @@ def main() -> None:
             if world == 1 and args.streams > 1:
                 line["concurrent"] = concurrent_streams(model, ml, mr, att, up, args.streams, args.steps, args.warmup,
                                                         dev)
+            if world == 1:
+                line["forward_e2e"] = forward_e2e(model, args, dev)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref = cpu_baseline(model, ml, mr, att, up, args, args.cpu_seconds)
             line["cpu_baseline"] = cb
             got = hp.outputs[0][:1].detach().cpu()  # the oracle ran the batch's first pair
             line["epe_vs_oracle"] = float((got - ref).abs().mean())
-            # the random-init weights give unnormalised disparity_regression outputs (the reference sums
-            # cost * d without a softmax, submodule.py:211-216): thousands of px, so also relative
-            line["epe_vs_oracle_rel"] = float((got - ref).abs().mean() / ref.abs().mean().clamp_min(1e-12))
+            line["disparity_range_oracle"] = [round(float(ref.min()), 3), round(float(ref.max()), 3)]
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

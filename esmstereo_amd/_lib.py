@@ -66,12 +66,6 @@ class EsmFmnetDesc(Structure):
                 ("hid", c_int32), ("reserved2", c_int32)]
 
 
-class EsmDmstackDesc(Structure):
-    _fields_ = [("x", c_void_p), ("xb", c_int64), ("xh", c_int64), ("out", c_void_p),
-                ("w", c_void_p * 4), ("scale", c_void_p * 4), ("shift", c_void_p * 4),
-                ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32)]
-
-
 class EsmShuffleTailDesc(Structure):
     _fields_ = [("x", c_void_p), ("xb", c_int64), ("xc", c_int64), ("xh", c_int64),
                 ("up_w", c_void_p), ("up_b", c_void_p), ("tail_w", c_void_p), ("tail_b", c_void_p),
@@ -95,13 +89,12 @@ SIGNATURES = {
     "esm_normcorr_volume_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "esm_disp_regression_f32": (c_int, [c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
     "esm_topk2_regression_f32": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
+    "esm_topk_regression_f32": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "esm_conv_f32": (c_int, [POINTER(EsmConvDesc), c_void_p]),
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
     "esm_fmnet_f32": (c_int, [POINTER(EsmFmnetDesc), c_void_p]),
-    "esm_dmstack_f32": (c_int, [POINTER(EsmDmstackDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
     "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
-    "esm_conv_pair_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "esm_node_filter_u16": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_float, c_void_p]),
@@ -110,9 +103,7 @@ SIGNATURES = {
     "esm_plan_add_conv": (c_int, [c_void_p, POINTER(EsmConvDesc)]),
     "esm_plan_add_smix": (c_int, [c_void_p, POINTER(EsmSmixDesc)]),
     "esm_plan_add_fmnet": (c_int, [c_void_p, POINTER(EsmFmnetDesc)]),
-    "esm_plan_add_dmstack": (c_int, [c_void_p, POINTER(EsmDmstackDesc)]),
     "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
-    "esm_plan_add_conv_pair": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
@@ -146,7 +137,7 @@ def _load() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc, EsmShuffleTailDesc, EsmFmnetDesc,
-                                    EsmConfDesc, EsmDmstackDesc)):
+                                    EsmConfDesc)):
         if lib.esm_struct_size(which) != ctypes.sizeof(st):
             raise ImportError(f"esmstereo_amd: ABI mismatch for {st.__name__}: "
                               f"C {lib.esm_struct_size(which)} vs ctypes {ctypes.sizeof(st)}")

@@ -23,8 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, dmstack_auto, pack_conv, pack_shuffle_tail,
-                     param_token, run_conv, run_conv_pair, run_dmstack, run_shuffle_tail)
+from .engine import ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv, run_shuffle_tail
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -101,12 +100,13 @@ def _up(cin: int, cout: int, is_3d: bool, last: bool = False) -> BasicConv:
 
 def _pair(ctx: Ctx, first: BasicConv, srcs: Sequence[torch.Tensor], second, second_packed: Optional[PackedConv] = None,
           **kw) -> torch.Tensor:
-    """``second(first(cat(srcs)))`` as one fused launch where the pair has a fused form (2-D,
-    stride 1), else two launches (engine.run_conv_pair)."""
+    """``second(first(cat(srcs)))``: two launches.  (Fused two-conv forms measured slower than two
+    register-weight launches on MI355X and were retired)"""
     n0 = getattr(first, "_esm_name", "BasicConv")
     n1 = getattr(second, "_esm_name", "conv") if second is not None else "conv"
     pb = second_packed if second_packed is not None else second.packed()
-    return run_conv_pair(ctx, first.packed(), srcs, pb, tag=f"{n0}+{n1.rsplit('.', 1)[-1]}", tags=(n0, n1), **kw)
+    mid = run_conv(ctx, first.packed(), srcs, tag=n0)
+    return run_conv(ctx, pb, [mid], tag=n1, **kw)
 
 
 def _crop_like(t: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
@@ -250,13 +250,9 @@ class _ESMUpsampler(nn.Module):
         n = len(self.STAGES)
         for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
             dm = getattr(self, f"dm{tag}")
-            dml, dmw = [m.packed() for m in dm], [m.conv.weight for m in dm]
-            if dmstack_auto(dml, dmw, prev):
-                d = run_dmstack(ctx, dml, dmw, prev, tag=getattr(dm, "_esm_name", f"{me}.dm{tag}"))
-            else:
-                d = dm[0].emit(ctx, [prev])
-                d = _pair(ctx, dm[1], [d], dm[2])
-                d = dm[3].emit(ctx, [d])
+            d = dm[0].emit(ctx, [prev])
+            d = _pair(ctx, dm[1], [d], dm[2])
+            d = dm[3].emit(ctx, [d])
             spx = getattr(self, f"spx_{tag}")
             c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c

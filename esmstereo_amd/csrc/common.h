@@ -70,34 +70,18 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-// SiLU as nn.SiLU: x / (1 + exp(-x))
-// XCD-aware workgroup order for a 3-D grid (opt-in, ESM_XCD_REMAP builds): the dispatcher deals
-// workgroups (x fastest, then y, z) round-robin over the 8 XCDs, so neighbouring tiles, which read
-// each other's halo rows / planes, sit in different XCDs' L2s and each fetches the shared lines from
-// memory again.  Remapped bijectively, XCD k runs a contiguous range of logical tiles (a contiguous
-// slab of rows / planes) and the halo stays in its own L2.  Measured on the wide / small / 3-D /
-// transposed / shuffle-tail forms: memory-side bytes fall to 1.0-2.1x the algorithmic (from up to
-// 6.6x), yet the S-K step is 13 us slower and L-K 27 us, so the hardware
-// order is the default.
+// Workgroup coordinates in the hardware's dispatch order.  An XCD-slab remap of this order
+// (neighbouring tiles on one XCD so halo rows stay in its L2) cut memory-side bytes to 1.0-2.1x the
+// algorithmic but made the S-K step 13 us and L-K 27 us slower on these latency-bound forms
+// (round 2); halo reuse now happens inside a workgroup instead.
 struct Blk3 {
     int x, y, z;
 };
 __device__ __forceinline__ Blk3 xcd_block() {
-#ifndef ESM_XCD_REMAP
     return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
-#else
-    const unsigned gx = gridDim.x, gy = gridDim.y;
-    const unsigned nwg = gx * gy * gridDim.z;
-    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    unsigned wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-    const int x = static_cast<int>(wg % gx);
-    wg /= gx;
-    const int y = static_cast<int>(wg % gy);
-    return {x, y, static_cast<int>(wg / gy)};
-#endif
 }
 
+// SiLU as nn.SiLU: x / (1 + exp(-x))
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 // SiLU with the hardware exp2 / reciprocal (a few ulp): per-pixel chains where the libm forms'

@@ -10,7 +10,6 @@ namespace conv {
 bool stem_ok(const esm_conv_desc& a);                    // conv_stem.hip
 bool stem_auto(const esm_conv_desc& a);                  // conv_stem.hip
 int launch_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
-int launch_gwc_stem(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 bool c1in_ok(const esm_conv_desc& a);                    // conv_stem.hip
 int launch_c1in(const esm_conv_desc& a, hipStream_t s);  // conv_stem.hip
 bool small_ok(const esm_conv_desc& a);                   // conv_small.hip
@@ -26,7 +25,6 @@ int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
 constexpr int kHintNoStem = 1 << 18;  // automatic choice among the other forms
-constexpr int kHintGwcStem = 1 << 19;  // input = the virtual gwc volume of src[0..2] (conv_stem.hip)
 constexpr int kHintC1in = 1 << 20;     // force the VALU single-input-channel form (conv_stem.hip)
 constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound layers (conv_small.hip)
 constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
@@ -36,7 +34,6 @@ constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 f
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
     const esm_conv_desc& a = *d;
-    if (a.hint & kHintGwcStem) return conv::launch_gwc_stem(a, s);  // validates its own sources
     if (!a.w || !a.out) return arg_error("conv: null weights/output");
     if (a.nsrc < 1 || a.nsrc > ESM_MAX_SRC) return arg_error("conv: nsrc must be 1..3");
     int cin = 0;

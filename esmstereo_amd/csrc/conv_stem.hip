@@ -34,23 +34,9 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
-// One group-wise correlation voxel exactly as build_gwc_volume computes it (gwc_kernel,
-// volumes.hip): mean of the 2 channel products, each rounded, then `* att` (S variant).
-__device__ __forceinline__ float gwc_voxel(float l0, float l1, float r0, float r1, float at, bool ok) {
-#pragma clang fp contract(off)
-    float s = l0 * r0;
-    s = s + l1 * r1;
-    const float v = (s * 0.5f) * at;
-    return ok ? v : 0.f;
-}
-
 // KS: the 4 waves split the input-channel chunks of ONE 4-row tile (grids far below one
 // workgroup per CU) and add their partial sums in LDS in a fixed order.
-// GV: the input is the VIRTUAL gwc volume [B, G, D, h, w] of features L = src[0], R = src[1]
-// (2 channels per group) and the optional attention weights att = src[2] (S variant,
-// models/ESMStereo.py:711): each B operand is computed from the features in registers, so the
-// cost volume of build_gwc_volume -> group_stem (ESMStereo.py:708-711) never reaches HBM.
-template <bool D3, int CG, int CK, bool KS, bool GV = false>
+template <bool D3, int CG, int CK, bool KS>
 __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
     constexpr int K = 3;
     constexpr int KDT = D3 ? 3 : 1;
@@ -103,96 +89,21 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
             roff[td][th] = ok ? 4u * ((D3 ? zi * sd : 0) + yi * sh + xi) : kOOB;
         }
 
-    // raw operands of one chunk: the B values themselves, or (GV) the feature / att values they
-    // are computed from (L and att do not depend on the disparity tap td: loaded once per row)
-    constexpr int NRAW = GV ? CK * K * 3 + CK * KDT * K * 2 : NB;
-    const esm_src& sR = a.src[1];
-    const esm_src& sA = a.src[2];
-    const bool has_att = GV && sA.ptr != nullptr;
-    __amdgpu_buffer_rsrc_t rsR = rs, rsA = rs;
-    unsigned lof[K], aof[K], rof[KDT][K];
-    bool vok[KDT][K];
-    if constexpr (GV) {
-        rsR = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sR.ptr + b * sR.sb), static_cast<short>(0),
-                                                4 * ((sR.C - 1) * static_cast<int>(sR.sc) + (a.Hi - 1) * static_cast<int>(sR.sh) + a.Wi),
-                                                0x00020000);
-        if (has_att)
-            rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sA.ptr + b * sA.sb), static_cast<short>(0),
-                                                    4 * ((sA.C - 1) * static_cast<int>(sA.sc) + (a.Hi - 1) * static_cast<int>(sA.sh) + a.Wi),
-                                                    0x00020000);
-#pragma unroll
-        for (int th = 0; th < K; ++th) {
-            const int yi = oy - 1 + th;
-            const bool yok = zok && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-            lof[th] = yok ? 4u * (yi * sh + xi) : kOOB;
-            aof[th] = yok ? 4u * (yi * static_cast<int>(sA.sh) + xi) : kOOB;
-#pragma unroll
-            for (int td = 0; td < KDT; ++td) {
-                const int zi = oz - 1 + td;  // disparity of the tap
-                const bool ok = yok && zi >= 0 && zi < a.Di && xi >= zi;  // x < d: zero (submodule.py:156-159)
-                vok[td][th] = ok;
-                rof[td][th] = ok ? 4u * (yi * static_cast<int>(sR.sh) + xi - zi) : kOOB;
-            }
-        }
-    }
-    auto load_chunk = [&](float (&raw)[NRAW], int cc) {
+    auto load_chunk = [&](float (&bv)[NB], int cc) {
 #pragma unroll
         for (int k = 0; k < CK; ++k) {
-            const int c = cc + k;
-            if constexpr (GV) {
-                const bool cok = c < a.Cin;
-                const unsigned l0 = cok ? 4u * (2 * c) * sc : kOOB, l1 = cok ? 4u * (2 * c + 1) * sc : kOOB;
-                const unsigned r0 = cok ? 4u * (2 * c) * static_cast<int>(sR.sc) : kOOB;
-                const unsigned r1 = cok ? 4u * (2 * c + 1) * static_cast<int>(sR.sc) : kOOB;
-                const unsigned ac = cok ? 4u * c * static_cast<int>(sA.sc) : kOOB;
+            const unsigned co = cc + k < a.Cin ? 4u * (cc + k) * sc : kOOB;
 #pragma unroll
-                for (int th = 0; th < K; ++th) {
-                    raw[(k * K + th) * 3 + 0] = buf_load_s(rs, lof[th] + l0, 0);
-                    raw[(k * K + th) * 3 + 1] = buf_load_s(rs, lof[th] + l1, 0);
-                    raw[(k * K + th) * 3 + 2] = has_att ? buf_load_s(rsA, aof[th] + ac, 0) : 1.f;
-                }
+            for (int td = 0; td < KDT; ++td)
 #pragma unroll
-                for (int td = 0; td < KDT; ++td)
-#pragma unroll
-                    for (int th = 0; th < K; ++th) {
-                        raw[CK * K * 3 + ((k * KDT + td) * K + th) * 2 + 0] = buf_load_s(rsR, rof[td][th] + r0, 0);
-                        raw[CK * K * 3 + ((k * KDT + td) * K + th) * 2 + 1] = buf_load_s(rsR, rof[td][th] + r1, 0);
-                    }
-            } else {
-                const unsigned co = c < a.Cin ? 4u * c * sc : kOOB;
-#pragma unroll
-                for (int td = 0; td < KDT; ++td)
-#pragma unroll
-                    for (int th = 0; th < K; ++th) raw[(k * KDT + td) * K + th] = buf_load_s(rs, roff[td][th] + co, 0);
-            }
-        }
-    };
-    auto finish_chunk = [&](const float (&raw)[NRAW], float (&bv)[NB]) {
-        if constexpr (GV) {
-#pragma unroll
-            for (int k = 0; k < CK; ++k)
-#pragma unroll
-                for (int td = 0; td < KDT; ++td)
-#pragma unroll
-                    for (int th = 0; th < K; ++th) {
-                        const float* lr = raw + (k * K + th) * 3;
-                        const float* rr = raw + CK * K * 3 + ((k * KDT + td) * K + th) * 2;
-                        bv[(k * KDT + td) * K + th] = gwc_voxel(lr[0], lr[1], rr[0], rr[1], lr[2], vok[td][th]);
-                    }
-        } else {
-#pragma unroll
-            for (int i = 0; i < NB; ++i) bv[i] = raw[i];
+                for (int th = 0; th < K; ++th) bv[(k * KDT + td) * K + th] = buf_load_s(rs, roff[td][th] + co, 0);
         }
     };
 
     constexpr int CSTEP = KS ? 4 * CK : CK;  // channel step of one wave
     const int c_first = KS ? wave * CK : 0;
     float bcur[NB];
-    {
-        float raw0[NRAW];
-        load_chunk(raw0, c_first);
-        finish_chunk(raw0, bcur);
-    }
+    load_chunk(bcur, c_first);
     // weights -> LDS: wl[((ci * TAPS + tap) * 4 + i) * CGP + g] = w[tap][ci][4g + i]
     const int cst = (a.Cin + CK - 1) / CK * CK;  // staged channels (whole chunks; past Cin: zeros)
     {
@@ -239,7 +150,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
         for (int g = 0; g < CG; ++g) acc[c][g] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     for (int cc = c_first; cc < cst; cc += CSTEP) {
-        float bnext[NRAW];
+        float bnext[NB];
         if (cc + CSTEP < cst) load_chunk(bnext, cc + CSTEP);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -272,14 +183,16 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
                                 av[2 * j + 1] = w2.y;
                             }
                         }
-                        // chain by tap only: the accumulation order is then independent of the
-                        // chunk size (the fused gwc form is bitwise equal to volume -> stem)
+                        // chain by tap only: the accumulation order is independent of the chunk size
                         const int ch = ((td * K + th) * K + tw) % NCH;
 #pragma unroll
                         for (int g = 0; g < CG; ++g) acc[ch][g] = mfma4(av[g], bs, acc[ch][g]);
                     }
                 }
-        if (cc + CSTEP < cst) finish_chunk(bnext, bcur);
+        if (cc + CSTEP < cst) {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) bcur[i] = bnext[i];
+        }
     }
 
     float sum[CG][4];
@@ -330,7 +243,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
         }
 }
 
-template <bool D3, int CG, bool KS, bool GV = false>
+template <bool D3, int CG, bool KS>
 int launch_sconv_ks(const esm_conv_desc& a, hipStream_t s, int ck, long long nwg) {
     constexpr int TAPS = D3 ? 27 : 9;
     constexpr int CGP = CG == 3 ? 4 : CG;
@@ -338,14 +251,7 @@ int launch_sconv_ks(const esm_conv_desc& a, hipStream_t s, int ck, long long nwg
     const size_t lds = static_cast<size_t>(cst) * TAPS * 4 * CGP * sizeof(float);
     if (nwg > 0x7fffffffLL) return arg_error("conv: grid too large");
     const dim3 grid(static_cast<unsigned>(nwg));
-    if constexpr (GV) {
-        if (ck == 1)
-            hipLaunchKernelGGL((sconv_kernel<D3, CG, 1, KS, true>), grid, dim3(256), lds, s, a);
-        else if (ck == 2)
-            hipLaunchKernelGGL((sconv_kernel<D3, CG, 2, KS, true>), grid, dim3(256), lds, s, a);
-        else
-            hipLaunchKernelGGL((sconv_kernel<D3, CG, 4, KS, true>), grid, dim3(256), lds, s, a);
-    } else if (ck == 1)
+    if (ck == 1)
         hipLaunchKernelGGL((sconv_kernel<D3, CG, 1, KS>), grid, dim3(256), lds, s, a);
     else if (ck == 2)
         hipLaunchKernelGGL((sconv_kernel<D3, CG, 2, KS>), grid, dim3(256), lds, s, a);
@@ -354,48 +260,22 @@ int launch_sconv_ks(const esm_conv_desc& a, hipStream_t s, int ck, long long nwg
     return check_launch("conv(stem)");
 }
 
-// Grid / channel-chunk choice, shared by the plain and the fused-gwc launchers (the same choice
-// gives the same accumulation order, so the two are bitwise equal): small grids split the
-// channel chunks over the 4 waves (4x the workgroups) when there are at least 4 chunks.
-template <bool D3, int CG, bool GV = false>
+// Grid / channel-chunk choice: small grids split the channel chunks over the 4 waves (4x the
+// workgroups) when there are at least 4 chunks.
+template <bool D3, int CG>
 int launch_sconv(const esm_conv_desc& a, hipStream_t s) {
     const long long tiles_w = (a.Wo + 13) / 14;
     const long long plain = tiles_w * (D3 ? (a.Ho + 3) / 4 * ((a.Do + 3) / 4) : (a.Ho + 15) / 16) * a.B;
     const int ck_ks = a.Cin >= 16 ? 4 : (a.Cin >= 8 ? 2 : 1);
     if (plain < 512 && (a.Cin + ck_ks - 1) / ck_ks >= 4) {
         const long long nwg = tiles_w * ((a.Ho + 3) / 4) * (D3 ? a.Do : 1) * a.B;
-        return launch_sconv_ks<D3, CG, true, GV>(a, s, ck_ks, nwg);
+        return launch_sconv_ks<D3, CG, true>(a, s, ck_ks, nwg);
     }
-    // plain form: the chunk size does not change the order; the fused form's raw feature operands
-    // are 3x the B values, so it takes chunks of 2 groups
-    const int ck = GV ? 2 : (a.Cin <= 1 ? 1 : (a.Cin <= 2 ? 2 : 4));
-    return launch_sconv_ks<D3, CG, false, GV>(a, s, ck, plain);
+    const int ck = a.Cin <= 1 ? 1 : (a.Cin <= 2 ? 2 : 4);  // the chunk size does not change the order
+    return launch_sconv_ks<D3, CG, false>(a, s, ck, plain);
 }
 
 }  // namespace
-
-// build_gwc_volume + group_stem in one launch (esm_conv_desc.hint bit 19, see the header).
-int launch_gwc_stem(const esm_conv_desc& a, hipStream_t s) {
-    const esm_src &L = a.src[0], &R = a.src[1], &A = a.src[2];
-    if (!L.ptr || !R.ptr || !a.w || !a.out) return arg_error("gwc_stem: null pointer");
-    if (a.transposed || a.stride != 1 || a.kd != 3 || a.kh != 3 || a.kw != 3 || a.pd != 1 || a.ph != 1 || a.pw != 1)
-        return arg_error("gwc_stem: the stem is a 3x3x3 stride-1 conv with padding 1");
-    if (a.Cout != 8) return arg_error("gwc_stem: group_stem has 8 output channels");
-    if (a.B <= 0 || a.Cin <= 0 || L.C != 2 * a.Cin || R.C != 2 * a.Cin)
-        return arg_error("gwc_stem: features must have 2 channels per group (C = 2 * Cin)");
-    if (A.ptr && A.C != a.Cin) return arg_error("gwc_stem: att must have one channel per group");
-    if (a.Do != a.Di || a.Ho != a.Hi || a.Wo != a.Wi || a.Di <= 0 || a.Hi <= 0 || a.Wi <= 0)
-        return arg_error("gwc_stem: output extent must equal the volume extent (D, h, w)");
-    if (a.cin_pad % 16 || a.cin_pad < a.Cin || a.cout_pad % 32 || a.cout_pad < a.Cout) return arg_error("gwc_stem: bad weight padding");
-    if (a.shuffle > 1 || a.up || a.nsrc != (A.ptr ? 3 : 2)) return arg_error("gwc_stem: unsupported epilogue / sources");
-    for (const esm_src* p : {&L, &R, &A}) {
-        if (!p->ptr) continue;
-        const long long last = (p->C - 1) * p->sc + (a.Hi - 1) * p->sh + a.Wi;
-        if (4 * last >= kOOB || p->sc > (1 << 28) || p->sh > (1 << 28)) return arg_error("gwc_stem: source too large");
-    }
-    if (static_cast<long long>((a.Cin + 3) / 4 * 4) * 27 * 4 * 2 * 4 > 64 * 1024) return arg_error("gwc_stem: weight slab exceeds LDS");
-    return launch_sconv<true, 2, true>(a, s);
-}
 
 // Single-input-channel 2-D convs on the VALU: the refinement heads' first layer (BasicConv(1, C,
 // 3, s2, p1), models/ESMStereo.py:190-191) and the disparity feature heads dmNx.0 (BasicConv(1, C,

@@ -16,12 +16,8 @@ int launch_regression(int, const float*, const float*, float*, int, int, int, in
 int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
 int launch_fmnet(const esm_fmnet_desc*, hipStream_t);
-int launch_dmstack(const esm_dmstack_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 int launch_conf(const esm_conf_desc*, hipStream_t);
-namespace conv {
-int launch_conv_pair(const esm_conv_desc*, const esm_conv_desc*, hipStream_t);
-}
 
 namespace {
 thread_local std::string g_error;
@@ -36,7 +32,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kConvPair = 8, kFmnet = 9, kConf = 10, kDmstack = 11 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10 };
 
 struct VolArgs {
     const float* L;
@@ -57,10 +53,8 @@ struct RegArgs {
 struct Op {
     int kind = 0;
     esm_conv_desc conv{};
-    esm_conv_desc conv2{};
     esm_smix_desc smix{};
     esm_fmnet_desc fm{};
-    esm_dmstack_desc dm{};
     esm_shuffle_tail_desc st{};
     VolArgs vol{};
     RegArgs reg{};
@@ -73,9 +67,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kConv: return esm::launch_conv(&op.conv, s);
         case kSmix: return esm::launch_smix(&op.smix, s);
         case kFmnet: return esm::launch_fmnet(&op.fm, s);
-        case kDmstack: return esm::launch_dmstack(&op.dm, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
-        case kConvPair: return esm::conv::launch_conv_pair(&op.conv, &op.conv2, s);
         case kConf: return esm::launch_conf(&op.cf, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
@@ -205,7 +197,6 @@ int esm_struct_size(int which) {
         case 4: return static_cast<int>(sizeof(esm_shuffle_tail_desc));
         case 5: return static_cast<int>(sizeof(esm_fmnet_desc));
         case 6: return static_cast<int>(sizeof(esm_conf_desc));
-        case 7: return static_cast<int>(sizeof(esm_dmstack_desc));
         default: return -1;
     }
 }
@@ -245,28 +236,11 @@ int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc) {
     return add_op(plan, std::move(op));
 }
 
-int esm_plan_add_dmstack(esm_plan* plan, const esm_dmstack_desc* desc) {
-    if (!desc) return esm::arg_error("plan: null dmstack desc");
-    Op op;
-    op.kind = kDmstack;
-    op.dm = *desc;
-    return add_op(plan, std::move(op));
-}
-
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc) {
     if (!desc) return esm::arg_error("plan: null shuffle_tail desc");
     Op op;
     op.kind = kShuffleTail;
     op.st = *desc;
-    return add_op(plan, std::move(op));
-}
-
-int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b) {
-    if (!a || !b) return esm::arg_error("plan: null conv pair desc");
-    Op op;
-    op.kind = kConvPair;
-    op.conv = *a;
-    op.conv2 = *b;
     return add_op(plan, std::move(op));
 }
 

@@ -68,3 +68,92 @@ def sharded_forward(model, left: torch.Tensor, right: torch.Tensor, group=None) 
         with torch.no_grad():
             disp = model(left[lo:hi], right[lo:hi], False)[0]
     return gather_disparities(disp, int(left.shape[0]), group)
+
+
+# ----------------------------------------------------------------------------- timed multi-rank steps
+# The measurement loop of bench.py, kept here so that the same code runs under RCCL on the GPU node
+# and under gloo in the CPU tests (tests/test_dist.py): W untimed warm-up steps, a barrier +
+# device synchronisation, K timed steps, a barrier + synchronisation, and the elapsed time reduced
+# to its maximum over the ranks.
+
+
+def world_info(group=None) -> Tuple[int, int]:
+    """(world size, rank); (1, 0) when torch.distributed is not initialised."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def local_batch(world: int, rank: int, batch: Optional[int] = None,
+                global_batch: Optional[int] = None) -> Tuple[int, str, int]:
+    """(pairs this rank runs per step, "weak" | "strong", pairs all ranks run per step).
+
+    weak scaling: every rank runs ``batch`` pairs; strong scaling: ``global_batch`` pairs split
+    into contiguous shards (``shard_range``), which must split evenly so every rank's step is the
+    same work."""
+    if (batch is None) == (global_batch is None):
+        raise ValueError("local_batch: give exactly one of batch (weak) and global_batch (strong)")
+    if global_batch is not None:
+        if global_batch % world:
+            raise ValueError(f"global batch {global_batch} must split evenly over {world} ranks")
+        lo, hi = shard_range(global_batch, world, rank)
+        return hi - lo, "strong", global_batch
+    return batch, "weak", batch * world
+
+
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+class DisparityGather:
+    """Per-step exchange of the ranks' disparity maps into one preallocated ``[world, *shape]``
+    buffer: ``all_gather_into_tensor`` over RCCL, the list form over gloo.  Every rank holds the
+    same number of pairs (``local_batch`` enforces it), so no padding is needed on the hot loop."""
+
+    def __init__(self, local: torch.Tensor, group=None):
+        self.group = group
+        self.world, _ = world_info(group)
+        self.buf = local.new_empty((self.world,) + tuple(local.shape))
+        self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
+
+    def __call__(self, local: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            self.buf[0].copy_(local)
+        elif self.nccl:
+            dist.all_gather_into_tensor(self.buf, local, group=self.group)
+        else:
+            dist.all_gather(list(self.buf.unbind(0)), local, group=self.group)
+        return self.buf
+
+
+def max_over_ranks(value: float, device: torch.device, group=None) -> float:
+    """The largest ``value`` over the ranks (the slowest rank bounds a synchronous step)."""
+    world, _ = world_info(group)
+    if world == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def timed_steps(step, steps: int, warmup: int, device: torch.device, group=None) -> float:
+    """Run ``step()`` ``warmup`` times untimed, then ``steps`` times between two
+    barrier + synchronise brackets; returns the max-over-ranks wall time of the timed steps (s)."""
+    import time
+
+    world, _ = world_info(group)
+    for _ in range(warmup):
+        step()
+    _sync(device)
+    if world > 1:
+        dist.barrier(group=group)
+    _sync(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync(device)
+    if world > 1:
+        dist.barrier(group=group)
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks(elapsed, device, group)

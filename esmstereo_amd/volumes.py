@@ -81,18 +81,23 @@ def disparity_regression(x: torch.Tensor, maxdisp: int) -> torch.Tensor:
 
 
 def regression_topk(cost: torch.Tensor, disparity_samples: torch.Tensor, k: int) -> torch.Tensor:
-    """``regression_topk`` (submodule.py:218-225) -> [B, 1, H, W]; k = 2 (the ESMStereo call)."""
-    if k != 2:
-        raise NotImplementedError("esmstereo_amd implements regression_topk for k=2 (models/ESMStereo.py:721)")
+    """``regression_topk`` (submodule.py:218-225) -> [B, 1, H, W]: the top-k costs over D (value
+    descending; ties -> lowest index, NaN first), softmax over them, the probability-weighted sum of
+    ``disparity_samples`` at their indices (``None``: arange(D)).  The reference slices the sorted
+    indices (``ind[:, :k]``), so k follows Python slicing: k > D takes all D, k <= -D or k = 0 none
+    (a zero map)."""
     require_device(cost, "regression_topk cost")
+    if cost.dim() != 4:
+        raise RuntimeError(f"regression_topk: expected a [B, D, H, W] cost, got shape {tuple(cost.shape)}")
     B, D, H, W = (int(v) for v in cost.shape)
-    if D < k:
-        raise RuntimeError(f"selected index k out of range (D={D}, k={k})")
+    ke = len(range(D)[:int(k)])
+    out = torch.empty(B, 1, H, W, device=cost.device, dtype=torch.float32)
+    if ke == 0 or out.numel() == 0:
+        return out.zero_()
     cost = cost.contiguous()
     samples = None
     if disparity_samples is not None:
         require_device(disparity_samples, "disparity_samples")
         samples = disparity_samples.expand(B, D, H, W).contiguous()
-    out = torch.empty(B, 1, H, W, device=cost.device, dtype=torch.float32)
-    Ctx(cost.device).regression(1, cost, out, B, D, H, W, samples=samples)
+    Ctx(cost.device).regression(1, cost, out, B, D, H, W, samples=samples, k=ke)
     return out

@@ -14,12 +14,12 @@
  *   esm_normcorr_volume_f32   models/submodule.py:187-200 build_norm_correlation_volume
  *   esm_disp_regression_f32   models/submodule.py:211-216 disparity_regression
  *   esm_topk2_regression_f32  models/submodule.py:218-225 regression_topk(cost, arange, k=2)
+ *   esm_topk_regression_f32   models/submodule.py:218-225 regression_topk(cost, samples, k), any k
  *   esm_conv_f32              models/submodule.py:12-38 BasicConv (Conv2d/3d, ConvTranspose2d/3d,
  *                             eval BatchNorm, GELU) and the plain convs of models/ESMStereo.py:
  *                             129-509 with their fused neighbours (crop+cat :172,177,230,234;
  *                             PixelShuffle+SiLU :265-268; bilinear-upsample + add :307,316;
  *                             `* att` :703; residual adds of models/shufflemixer.py:130-131)
- *   esm_dmstack_f32           models/ESMStereo.py:250-253 the upsamplers' dm<tag> stack (four BasicConv2d)
  *   esm_fmnet_f32             models/shufflemixer.py:100-112,129-130 FMBlock.net (two SMLayers) + x
  *   esm_smix_f32              models/shufflemixer.py:23-112 LayerNorm('BiasFree') +
  *                             SplitPointMlp + channel shuffle + residual, optionally preceded
@@ -28,10 +28,6 @@
  *                             upsample16 twins): `upsampling` (Conv2d 1x1 nf -> nf*r*r + bias,
  *                             PixelShuffle(r), SiLU) followed by `tail` (Conv2d 3x3 nf -> 1 +
  *                             bias) as one kernel; the shuffled map is never materialised
- *   esm_conv_pair_f32         two stride-1 2-D convs in one launch, the intermediate kept on chip:
- *                             agg_0 / agg_1 of up_refinement (models/ESMStereo.py:214-218,228-235),
- *                             spx_* (:256-259,283-286 and twins), dmNx.1 -> dmNx.2 (:250-253),
- *                             FMBlock.conv (models/shufflemixer.py:124-131)
  *   esm_conf_f32              the per-pixel stages of the confidence head LAFNet_ESM /
  *                             conf_upsample (models/ESMStereo_confidence.py:511-744) between its
  *                             convs (which run through esm_conv_f32): cost features, attention,
@@ -117,11 +113,6 @@ typedef struct {
     int32_t hint; /* 0 = automatic tile choice; else NT | KS << 4 | C1 << 8 | DIRECT << 9 | ROWS << 10 |
                      rows-per-wave << 12 | C1T << 16 | STEM << 17 (16-block 4x4x1 MFMA form for
                      3x3(x3) s1 convs with 8/12/16/24/32 couts) | NO_STEM << 18 (automatic, without it) |
-                     GWC_STEM << 19: the input is the VIRTUAL gwc volume (build_gwc_volume, 2 channels per
-                     group, models/submodule.py:151-161; `* att` of ESMStereo.py:711) of src[0] = L and
-                     src[1] = R ([B, 2*Cin, h, w]) and src[2] = att ([B, Cin, h, w] or ptr NULL); Di/Hi/Wi =
-                     D/h/w; a 3x3x3 s1 p1 stem with 8 couts; bitwise equal to esm_gwc_volume_f32 followed
-                     by esm_conv_f32 on the volume, without storing the volume |
                      C1IN << 20: force the VALU form for 2-D convs with one input channel
                      (tuning sweeps / tests; see conv_impl.h launch_geom) |
                      SMALL << 21: the lean K-split form for latency-bound layers (conv_small.hip;
@@ -135,9 +126,7 @@ typedef struct {
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
                      sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
                      split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
-                     8 waves per workgroup splitting K (layers with more than 4 channel groups).
-                     Bit 23 is read from a PAIR's first descriptor: the LDS-weight pair kernel instead of the lean
-                     1x1 -> 3x3 form (A/B measurements) */
+                     8 waves per workgroup splitting K (layers with more than 4 channel groups). */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;
@@ -195,21 +184,6 @@ typedef struct {
     int32_t reserved2;
 } esm_fmnet_desc;
 
-/* The ESM upsamplers' disparity-feature stack dm<tag> (models/ESMStereo.py:250-253): four BasicConv2d
- * (conv bias=False -> folded BN -> exact GELU) k5 p1 1->C, k3 p1 C->C, k3 p1 C->C, k1 p1 C->C in one
- * launch (halo recomputation).  x: [B, 1, H, W] with strides xb, xh (innermost 1), H, W >= 3;
- * out: [B, C, H, W] contiguous; w[l]: the conv weights in PyTorch layout ([C][1][5][5],
- * [C][C][3][3] x 2, [C][C][1][1]); scale/shift[l]: the folded BN (y = acc * scale + shift).  C = 16. */
-typedef struct {
-    const float* x;
-    int64_t xb, xh;
-    float* out;
-    const float* w[4];
-    const float* scale[4];
-    const float* shift[4];
-    int32_t B, C, H, W;
-} esm_dmstack_desc;
-
 /* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,
  * silu(pixel_shuffle(conv1x1(up_w, x) + up_b, r))), zero padding 1.  (nf, r) in
  * {(8,2), (8,4), (16,2), (16,4)}.  x: [B, nf, H, W] with strides xb, xc, xh (innermost 1);
@@ -230,8 +204,7 @@ typedef struct {
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc,
- * 7 esm_dmstack_desc;
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc;
  * -1 for an unknown id. */
 int esm_struct_size(int which);
 
@@ -246,20 +219,14 @@ int esm_disp_regression_f32(const float* cost, float* out, int B, int D, int H, 
 /* samples: [B, D, H, W] disparity_samples, or NULL for arange(D) (the ESMStereo call). */
 int esm_topk2_regression_f32(const float* cost, const float* samples, float* out, int B, int D, int H, int W,
                              void* stream);
+/* regression_topk for any k >= 1 (models/submodule.py:218-225): the reference slices the sorted
+ * indices, so k > D selects all D.  Ties rank the lower index first; NaN ranks first. */
+int esm_topk_regression_f32(const float* cost, const float* samples, float* out, int B, int D, int H, int W, int k,
+                            void* stream);
 int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
 int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream);
-int esm_dmstack_f32(const esm_dmstack_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
-/* out_b = epilogue_b(conv_b(epilogue_a(conv_a(src_a)))): `a` describes the first conv (its sources,
- * weights, BN/bias, activation; a->out is not written, a->res must be NULL), `b` the second (its
- * src[] is ignored: its input is a's output; weights, BN/bias, activation, optional residual and
- * post_scale, output).  Both stride 1, k in {1, 3} with same padding, 2-D, Cout <= 32 each,
- * a->Cin <= 96 (split on 4-channel boundaries when a has several sources), no shuffle / mul / up /
- * out2.  Returns ESM_ERR_UNSUPPORTED (no launch) for a pair without a fused form: run the two convs
- * with esm_conv_f32 instead. */
-int esm_conv_pair_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
-
 /* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
  *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D <= 64) -> out [B,7,H,W]: the 7 largest of
  *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
@@ -308,9 +275,7 @@ void esm_plan_destroy(esm_plan* plan);
 int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
 int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
-int esm_plan_add_dmstack(esm_plan* plan, const esm_dmstack_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
-int esm_plan_add_conv_pair(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
@@ -322,7 +287,7 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 8 = conv_pair, 9 = fmnet, 10 = conf, 11 = dmstack */
+ * 7 = shuffle_tail, 9 = fmnet, 10 = conf (8 and 11 were retired fused forms) */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

@@ -83,6 +83,21 @@ def regression_topk2(cost: torch.Tensor) -> torch.Tensor:
     return torch.sum(idx.to(cost.dtype) * prob, dim=1, keepdim=True)
 
 
+def regression_topk(cost: torch.Tensor, disparity_samples, k: int) -> torch.Tensor:
+    """``regression_topk(cost, disparity_samples, k)`` (submodule.py:218-225) for any k: the sorted
+    indices sliced ``[:, :k]`` (Python slicing: k > D keeps all D), the gathered costs' softmax, the
+    probability-weighted sum of the gathered samples (``None``: arange(D)).  Ties -> lowest index
+    (stable sort; the reference's ``cost.sort`` is unstable, so tie order is this build's)."""
+    _, ind = torch.sort(cost, dim=1, descending=True, stable=True)
+    idx = ind[:, :k]
+    if disparity_samples is None:
+        samples = idx.to(cost.dtype)
+    else:
+        samples = torch.gather(disparity_samples.expand_as(cost), 1, idx)
+    prob = F.softmax(torch.gather(cost, 1, idx), 1)
+    return torch.sum(samples * prob, dim=1, keepdim=True)
+
+
 # ----------------------------------------------------------------------------- BasicConv
 
 

@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-from pmc_traffic import OURS, assign, trailing
+from pmc_traffic import OURS, assign, timed_steps, trailing
 
 
 def per_dispatch(d: str):
@@ -40,7 +40,7 @@ def main():
     per = {}
     for d in dirs:
         for c, seq in per_dispatch(d).items():
-            per[c] = assign(seq[:len(seq) - tr], n)
+            per[c] = assign(seq[:len(seq) - tr], n, timed_steps(ops_json))
     out = []
     for i, op in enumerate(ops):
         row = {"op": i, "name": op["name"], "median_us": round(op.get("median_ms", 0) * 1e3, 2)}

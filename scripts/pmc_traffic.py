@@ -41,11 +41,16 @@ def per_dispatch(d: str, counter: str):
     return [vals[k] for k in order]
 
 
-def assign(seq, n):
+def assign(seq, n, timed=0):
+    """Average per launch-list position over the timed steps (``timed`` of them, the last whole
+    steps before the trailing dispatches; 0 = every whole step but the oldest)."""
     steps = len(seq) // n
     if steps == 0:
         raise SystemExit("fewer dispatches than one step")
-    tail = seq[-(steps - 1) * n:] if steps > 1 else seq[-n:]
+    if timed:
+        tail = seq[-min(timed, steps) * n:]
+    else:
+        tail = seq[-(steps - 1) * n:] if steps > 1 else seq[-n:]
     acc = defaultdict(list)
     for i, v in enumerate(tail):
         acc[i % n].append(v)
@@ -54,11 +59,20 @@ def assign(seq, n):
 
 def trailing(ops_json: str) -> int:
     """Dispatches bench.py issued after its last whole step (written next to the op table)."""
+    return _meta(ops_json).get("trailing_dispatches", 0)
+
+
+def timed_steps(ops_json: str) -> int:
+    """Whole steps of the timed region (bench.py runs marginal-cost replays with dropped ops before it)."""
+    return _meta(ops_json).get("timed_steps", 0)
+
+
+def _meta(ops_json: str) -> dict:
     meta = ops_json + ".meta.json"
     if not os.path.exists(meta):
-        return 0
+        return {}
     with open(meta) as f:
-        return int(json.load(f).get("trailing_dispatches", 0))
+        return {k: int(v) for k, v in json.load(f).items()}
 
 
 def main():
@@ -67,8 +81,8 @@ def main():
     n = len(ops)
     tr = trailing(ops_json)
     fs, ws = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
-    fetch = assign(fs[:len(fs) - tr], n)
-    write = assign(ws[:len(ws) - tr], n)
+    fetch = assign(fs[:len(fs) - tr], n, timed_steps(ops_json))
+    write = assign(ws[:len(ws) - tr], n, timed_steps(ops_json))
     tab = json.load(open(out)) if os.path.exists(out) else {}
     rows = {}
     for i, op in enumerate(ops):

@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 OURS = ("esm", "conv_kernel", "smix_kernel", "gwc_kernel", "concat_kernel", "normcorr_kernel", "l2norm_kernel",
-        "dispreg_kernel", "topk2_kernel")
+        "dispreg_kernel", "topk_kernel")
 
 
 def load_trace(d: str):
@@ -35,13 +35,8 @@ def load_trace(d: str):
     return rows
 
 
-def trailing(ops_json: str) -> int:
-    """Dispatches bench.py issued after its last whole step (written next to the op table)."""
-    meta = ops_json + ".meta.json"
-    if not os.path.exists(meta):
-        return 0
-    with open(meta) as f:
-        return int(json.load(f).get("trailing_dispatches", 0))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_traffic import timed_steps, trailing  # noqa: E402
 
 
 def main():
@@ -53,7 +48,11 @@ def main():
     steps = len(rows) // n
     if steps == 0:
         raise SystemExit("trace shorter than one step")
-    tail = rows[-(steps - 1) * n:] if steps > 1 else rows[-n:]  # drop the oldest partial/probe block
+    timed = timed_steps(ops_json)
+    if timed:  # the timed region only (bench.py replays graphs with dropped ops before it)
+        tail = rows[-min(timed, steps) * n:]
+    else:
+        tail = rows[-(steps - 1) * n:] if steps > 1 else rows[-n:]  # drop the oldest partial/probe block
     nsteps = len(tail) // n
     dur = defaultdict(list)
     gaps = []

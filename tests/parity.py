@@ -27,6 +27,10 @@ from helpers import GOLDEN_DIR, digest, fullsize_inputs, load_golden
 EPE_TOL = 1e-3          # px, north_star: "EPE within 1e-3 of the PyTorch reference"
 COST_REL_TOL = 1e-5     # aggregated cost, relative to its max |value| (fp32, different summation orders)
 TOPK_MARGIN_TOL = 1e-4  # a top-2 flip is legitimate only where the reference's v2 - v3 <= this
+# The flip mask may hide at most this share of the image, unless every flip sits on a reference
+# margin <= MASK_TIE_TOL (a tie at fp32 resolution, where either top-2 set is the reference's answer)
+MASK_MAX_FRAC = 0.25
+MASK_TIE_TOL = 1e-6
 # Exact support of one low-res init pixel's influence on the final disparity, in low-res pixels,
 # for upsample4 (ESMStereo-L, models/ESMStereo.py:242-318): dm2x (4) + spx_2x (2) + to_feat (1) +
 # 2 FMBlocks (2 x (2 x 3 depthwise 7x7 + 1)) = 21 at 1/4 res; x2 -> 42 + tail2x 1 + ref2x's
@@ -64,6 +68,7 @@ def flip_masked(name: str, got: torch.Tensor, ref: torch.Tensor, flips: torch.Te
            "epe_outside_mask": e, "epe_all": e_all,
            "max_flip_margin": float(margin.cpu()[flips].max()) if n else 0.0}
     assert e <= EPE_TOL, (name, rep)
+    assert rep["masked_frac"] <= MASK_MAX_FRAC or rep["max_flip_margin"] <= MASK_TIE_TOL, (name, rep)
     return rep
 
 
@@ -91,10 +96,13 @@ def fullsize_case(name: str):
 
 
 def check_fullsize(name: str, m: dict, g: Dict[str, np.ndarray], cost: torch.Tensor, init: torch.Tensor,
-                   disp0: torch.Tensor) -> Dict[str, float]:
+                   disp0: torch.Tensor, disp0_from_ref_init: Optional[torch.Tensor] = None) -> Dict[str, float]:
     """cost [B, D, h, w], init [B, 1, h, w], disp0 [B, H, W] from the path under test vs the
     reference fixture.  S (continuous disparity_regression): EPE <= 1e-3 on init and on the
-    subsampled disp_0; L: the flip-masked metric on both."""
+    subsampled disp_0; L: the flip-masked metric on both.  ``disp0_from_ref_init`` [B, H, W]: the
+    upsampler under test run on the REFERENCE's own init_pred (g["init_pred"]), which carries every
+    top-2 decision the reference made, so it must match disp_0 at EVERY pixel (EPE <= 1e-3, no mask):
+    this pins the upsampler where the flip mask would hide it."""
     cost = cost.detach().double().cpu()
     flat = cost.reshape(-1)
     amax = float(g["cost_absmax"])
@@ -108,6 +116,11 @@ def check_fullsize(name: str, m: dict, g: Dict[str, np.ndarray], cost: torch.Ten
     ref_sub = torch.from_numpy(g["disp0_sub"])
     d0 = disp0.detach().double().cpu()
     rep["disp0_l2_rel"] = abs(float(d0.norm()) - float(g["disp0_l2"])) / float(g["disp0_l2"])
+    if disp0_from_ref_init is not None:
+        dr = disp0_from_ref_init.detach()[:, ::4, ::4].double().cpu()
+        rep["disp0_sub_epe_ref_init"] = float((dr - ref_sub.double()).abs().mean())
+        rep["disp0_sub_max_err_ref_init"] = float((dr - ref_sub.double()).abs().max())
+        assert rep["disp0_sub_epe_ref_init"] <= EPE_TOL, (name, rep)
     if m["cv_scale"] == 4:
         flips = (top2_sets(cost) != torch.sort(torch.from_numpy(g["top3_idx"][:, :2]).long(), 1)[0]).any(1)
         tv = torch.from_numpy(g["top3_val"])

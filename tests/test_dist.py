@@ -1,5 +1,7 @@
-"""Multi-process (gloo, world size 2, CPU) tests of the batch-sharding / gather logic used by
-bench.py and esmstereo_amd.dist.sharded_forward."""
+"""Multi-process (gloo, world size 2, CPU) tests of the batch-sharding / gather / timing logic used by
+bench.py and esmstereo_amd.dist.sharded_forward.  bench.py's multi-rank step is
+esmstereo_amd.dist.{local_batch, DisparityGather, timed_steps}: the same functions run here under
+gloo with a per-pair stand-in for the HIP hot path."""
 from __future__ import annotations
 
 import os
@@ -10,7 +12,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from esmstereo_amd.dist import gather_disparities, shard, shard_range, sharded_forward
+from esmstereo_amd.dist import (DisparityGather, gather_disparities, local_batch, max_over_ranks, shard, shard_range,
+                                sharded_forward, timed_steps)
 
 
 def test_shard_range_covers_batch_contiguously():
@@ -75,3 +78,67 @@ def test_gloo_world2_gather_and_sharded_forward(batch):
     for rank, ok1, ok2, shape in res:
         assert ok1 and ok2, (rank, ok1, ok2)
         assert shape == (batch, 8, 16)
+
+
+def test_local_batch_weak_and_strong():
+    assert local_batch(8, 3, batch=1) == (1, "weak", 8)
+    assert local_batch(8, 7, global_batch=32) == (4, "strong", 32)
+    assert local_batch(1, 0, global_batch=32) == (32, "strong", 32)
+    with pytest.raises(ValueError):
+        local_batch(3, 0, global_batch=32)  # uneven shards: ranks would time different work
+    with pytest.raises(ValueError):
+        local_batch(2, 0)
+
+
+def _bench_worker(rank, world, port, mode, q):
+    """bench.py's measured loop with a CPU stand-in step: each rank runs its shard of synthetic pairs
+    through a per-pair function, the disparities are gathered every step, rank 1 is made slower."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b, scaling, total = local_batch(world, rank, **({"batch": 2} if mode == "weak" else {"global_batch": 6}))
+        g = torch.Generator().manual_seed(100 + rank)  # per-rank synthetic input, as bench.py
+        left, right = torch.randn(b, 3, 8, 16, generator=g), torch.randn(b, 3, 8, 16, generator=g)
+        model = _PairModel()
+        out = torch.empty(b, 8, 16)
+        gather = DisparityGather(out)
+        calls = []
+
+        def step():
+            out.copy_(model(left, right, False)[0])
+            gather(out)
+            calls.append(1)
+            if rank == 1:
+                time.sleep(0.02)
+
+        el = timed_steps(step, steps=5, warmup=2, device=torch.device("cpu"))
+        # every rank's gathered buffer holds every rank's result, in rank order
+        allL = [torch.empty(b, 3, 8, 16) for _ in range(world)]
+        allR = [torch.empty(b, 3, 8, 16) for _ in range(world)]
+        dist.all_gather(allL, left)
+        dist.all_gather(allR, right)
+        ok = all(torch.equal(gather.buf[r], model(allL[r], allR[r], False)[0]) for r in range(world))
+        q.put((rank, ok, el, len(calls), b, scaling, total, max_over_ranks(float(rank), torch.device("cpu"))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["weak", "strong"])
+def test_gloo_world2_bench_step(mode):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    els = [r[2] for r in res]
+    assert els[0] == els[1] and els[0] >= 5 * 0.02  # max over ranks: both report the slow rank's time
+    for rank, ok, el, ncalls, b, scaling, total, mx in res:
+        assert ok and ncalls == 7 and mx == 1.0
+        assert scaling == mode and (b, total) == ((2, 4) if mode == "weak" else (3, 6))

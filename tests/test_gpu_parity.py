@@ -88,6 +88,37 @@ def test_topk_nan_ranks_first():
     assert rel(got[ok], ref[ok]) < 1e-6
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8, 9, 16, 48, 60])
+def test_regression_topk_any_k(k):
+    """regression_topk for any k (register top-k for k <= 8, selection passes above): vs the oracle
+    (stable descending sort sliced [:, :k]) with exact ties and NaN planes, and vs the REFERENCE's
+    own outputs (tests/golden/topk_k.npz, tie-free costs, random disparity samples) where the fixture
+    holds k.  Relative 1e-6 (softmax and the weighted sum in rank order)."""
+    gen = torch.Generator().manual_seed(100 + k)
+    cost = torch.randn(2, 48, 9, 21, generator=gen)
+    cost[0, 5, 0, :4] = cost[0, 9, 0, :4] = cost[0, 30, 0, :4] = 10.0  # 3-way exact ties
+    cost[1, :, 3, 3] = 0.25  # a whole tied column: the lowest k indices
+    cost[1, 7, 4, 4] = float("nan")
+    samples = torch.rand(2, 48, 9, 21, generator=gen) * 48
+    for smp in (None, samples):
+        got = E.regression_topk(cost.to(DEV), None if smp is None else smp.to(DEV), k).cpu()
+        ref = O.regression_topk(cost, smp, k)
+        assert torch.equal(torch.isnan(got), torch.isnan(ref)), k
+        ok = ~torch.isnan(ref)
+        assert rel(got[ok], ref[ok]) < 1e-6, (k, smp is None)
+    g = load_golden("topk_k.npz")
+    if k in g["ks"].tolist():
+        got = E.regression_topk(cu(g[f"cost_{k}"]), cu(g[f"samples_{k}"]), k)
+        assert rel(got, g[f"out_{k}"]) < 1e-6, k
+    # Python slicing of the sorted indices: k = 0 selects nothing (zeros), k = -1 all but the last
+    assert torch.equal(E.regression_topk(cost.to(DEV), None, 0).cpu(), torch.zeros(2, 1, 9, 21))
+    if k == 1:
+        got = E.regression_topk(cost.to(DEV), None, -1).cpu()
+        ref = O.regression_topk(cost, None, -1)
+        ok = ~torch.isnan(ref)
+        assert rel(got[ok], ref[ok]) < 1e-6
+
+
 @pytest.mark.parametrize("B,C,H,W,D,G", [(1, 64, 24, 78, 12, 32), (2, 64, 7, 13, 9, 32), (1, 64, 5, 3, 8, 32),
                                           (3, 32, 6, 10, 5, 4), (1, 64, 96, 312, 48, 32), (1, 8, 4, 6, 1, 8)])
 def test_volumes_vs_oracle(B, C, H, W, D, G):
@@ -499,65 +530,6 @@ def test_shuffle_tail(nf, r, H, W):
     assert rel(y, ref) < 1e-5
 
 
-@pytest.mark.parametrize("ka,kb,cins,cm,cout,act_a,act_b,res,H,W", [
-    (1, 3, (16, 16, 24), 16, 16, ACT_GELU, ACT_GELU, False, 130, 270),  # ref4x.agg_1
-    (1, 3, (16, 16, 32), 16, 16, ACT_GELU, ACT_GELU, False, 13, 29),   # ref2x.agg_0
-    (3, 3, (16, 24), 16, 8, ACT_GELU, ACT_GELU, False, 21, 45),        # spx_4x
-    (3, 3, (16,), 16, 16, ACT_GELU, ACT_GELU, False, 17, 40),          # dm.1 -> dm.2
-    (3, 1, (8,), 24, 8, ACT_SILU, ACT_NONE, True, 9, 33),              # FMBlock.conv (+ residual)
-    (1, 3, (32, 32, 32), 32, 32, ACT_GELU, ACT_GELU, False, 11, 37),   # L widths: no fused form (LDS) -> two launches
-])
-def test_conv_pair(ka, kb, cins, cm, cout, act_a, act_b, res, H, W):
-    """Fused pair (esm_conv_pair_f32) vs fp64 torch of the two layers; rel <= 1e-5.  Ragged
-    extents (tiles of 12-14 valid columns, rows not a multiple of the wave's run)."""
-    from esmstereo_amd.engine import PAIR_K1, run_conv_pair, pair_supported
-    bias_a = act_a == ACT_SILU
-    ca, ba = _mk(2, sum(cins), cm, ka, 1, ka // 2, bias=bias_a, bn=not bias_a, seed=21)
-    cb, bb = _mk(2, cm, cout, kb, 1, kb // 2, bias=res, bn=not res, seed=22)
-    xs = [torch.randn(2, c, H, W) for c in cins]
-    mid = _ref_conv(xs, ca, ba, act_a)
-    resid = torch.randn(2, cout, H, W) if res else None
-    ref = _ref_conv([mid], cb, bb, act_b, res=resid)
-    pa, pb = pk(ca, ba, act_a), pk(cb, bb, act_b)
-    big = 2 * H * W >= 65536
-    assert pair_supported(pa, pb, [x.to(DEV) for x in xs]) == ((cm <= 16 or cout <= 16) and
-                                                               ((ka == 1 and big and PAIR_K1) or kb == 1))
-    y = run_conv_pair(Ctx(DEV), pa, [x.to(DEV) for x in xs], pb, res=resid.to(DEV) if res else None)
-    assert rel(y, ref) < 1e-5
-    if not pair_supported(pa, pb, [x.to(DEV) for x in xs]) and (cm <= 16 or cout <= 16):
-        # the kernel itself (the host prefers two launches for this shape)
-        from esmstereo_amd.engine import _conv_desc
-        ctx = Ctx(DEV)
-        xd = [x.to(DEV) for x in xs]
-        da, _, _ = _conv_desc(ctx, pa, xd, alloc_out=False)
-        db, out, _ = _conv_desc(ctx, pb, [], virtual_in=(2, cm, H, W))
-        ctx.pair(da, db)
-        assert rel(out, ref) < 1e-5
-
-
-@pytest.mark.parametrize("cins,cout,H,W", [((16, 16, 24), 16, 130, 270), ((16, 16, 24), 16, 192, 624),
-                                           ((56,), 16, 37, 61), ((16, 32), 32, 23, 80), ((6,), 16, 5, 9),
-                                           ((16, 16, 32), 16, 48, 156)])
-def test_conv_pair_lean_vs_lds(cins, cout, H, W):
-    """The lean 1x1 -> 3x3 pair (register weights, one descriptor over the concat sources, compile-time
-    rows) and the LDS-weight pair kernel (forced by hint bit 23) vs fp64 torch (1e-5 relative), batch 2,
-    ragged extents, one and two B cout tiles."""
-    from esmstereo_amd.engine import _conv_desc
-    ca, ba = _mk(2, sum(cins), 16, 1, 1, 0, seed=31)
-    cb, bb = _mk(2, 16, cout, 3, 1, 1, seed=32)
-    xs = [torch.randn(2, c, H, W) for c in cins]
-    ref = _ref_conv([_ref_conv(xs, ca, ba, ACT_GELU)], cb, bb, ACT_GELU)
-    pa, pb = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
-    xd = [x.to(DEV) for x in xs]
-    for hint in (0, 1 << 23):
-        ctx = Ctx(DEV)
-        da, _, _ = _conv_desc(ctx, pa, xd, alloc_out=False)
-        da.hint = hint
-        db, out, _ = _conv_desc(ctx, pb, [], virtual_in=(2, 16, H, W))
-        ctx.pair(da, db)
-        assert rel(out, ref) < 1e-5, hex(hint)
-
-
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
@@ -793,7 +765,8 @@ def test_hot_path_full_size_vs_oracle(var, cv, B, H, W, maxdisp, noise):
 def test_hot_path_fullsize_vs_reference(name):
     """BASELINE KITTI size pinned to the REFERENCE itself (not only the oracle): the HIP plan on the
     seeded feature inputs of tests/golden/full_*.npz vs the reference's cost summaries, init_pred and
-    disp_0 (tests/parity.py check_fullsize; L flip-masked)."""
+    disp_0 (tests/parity.py check_fullsize; L flip-masked), and the HIP upsampler run on the
+    reference's OWN init_pred vs disp_0 at every (subsampled) pixel, no mask."""
     m, g, (ml, mr, att, up) = fullsize_case(name)
     model, sd, _ = _model_from_manifest(f"hot_{m['variant']}_{m['cv']}.npz", maxdisp=m["maxdisp"])
     model.load_state_dict(seeded_state(load_spec(m["spec"]), m["weight_seed"]))
@@ -805,7 +778,10 @@ def test_hot_path_fullsize_vs_reference(name):
     with torch.no_grad():
         init = E.regression_topk(cost, None, 2) if m["cv_scale"] == 4 else E.disparity_regression(cost, D)
     disp0 = model.hot_path(ml, mr, att, up)[0]
-    rep = check_fullsize(name, m, g, cost, init.view(m["B"], 1, *cost.shape[-2:]), disp0)
+    with torch.no_grad():  # upsample_module on the reference's init_pred (models/ESMStereo.py:722-735)
+        d_ref_init = model.upsample_module.emit(E.engine.Ctx(DEV), up, cu(g["init_pred"]), final_scale=4.0)[0]
+    rep = check_fullsize(name, m, g, cost, init.view(m["B"], 1, *cost.shape[-2:]), disp0,
+                         disp0_from_ref_init=d_ref_init[:, 0])
     print(name, rep)
 
 
@@ -860,31 +836,6 @@ def test_expected_raises():
                 model(left, left, False)
 
 
-@pytest.mark.parametrize("B,G,D,h,w,att", [(1, 32, 12, 24, 78, True), (2, 32, 5, 7, 13, False), (1, 32, 48, 20, 60, False),
-                                           (1, 4, 6, 9, 31, True)])
-def test_gwc_stem_fused(B, G, D, h, w, att):
-    """build_gwc_volume (+ `* att`) fused into group_stem (conv_stem.hip, GV form) vs the oracle volume
-    through an fp64 conv (1e-5 relative), and bitwise vs the two-launch path."""
-    from esmstereo_amd.engine import run_gwc_stem
-
-    L, R = feature_pair(B, 2 * G, h, w, 9, max(D, 2))
-    a = torch.rand(B, G, h, w) + 0.5 if att else None
-    conv, bn = _mk(3, G, 8, 3, 1, 1, seed=6)
-    p = pk(conv, bn, ACT_GELU)
-    V = O.gwc_volume(L, R, D, G)
-    if a is not None:
-        V = V * a.unsqueeze(2)
-    ref = _ref_conv([V], conv, bn, ACT_GELU)
-    ctx = Ctx(DEV)
-    y = run_gwc_stem(ctx, p, L.to(DEV), R.to(DEV), a.to(DEV) if a is not None else None, D, G)
-    assert rel(y, ref) < 1e-5
-    V2 = torch.empty(B, G, D, h, w, device=DEV)
-    ctx.gwc(L.to(DEV), R.to(DEV), a.to(DEV) if a is not None else None, V2, B, 2 * G, h, w, D, G)
-    # same voxel values, same chunking and accumulation order: bitwise equal to volume -> the 16-block
-    # stem form (forced: the automatic / tuned choice for this shape may be another form)
-    assert torch.equal(y, run_conv(ctx, p, [V2], hint=HINT_STEM))
-
-
 @pytest.mark.parametrize("C,H,W", [(8, 24, 78), (8, 7, 13), (16, 96, 312), (16, 5, 40), (8, 1, 1)])
 def test_fmnet_fused_bitwise(C, H, W):
     """FMBlock.net + x in one launch (esm_fmnet_f32, halo recomputation) vs the three smix launches:
@@ -905,10 +856,9 @@ def test_fmnet_fused_bitwise(C, H, W):
     t2 = run_smix(ctx, t1, [p["a2"], p["b1"]], dw=p["dw0"])
     t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x)
     assert rel(fused, t3) < 1e-6
-    # the whole block in one launch (FMBlock.conv fused behind net) vs net + the conv pair launch
-    from esmstereo_amd.engine import run_conv_pair
+    # the whole block in one launch (FMBlock.conv fused behind net) vs net + the two conv launches
     whole = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"])
-    ref = run_conv_pair(ctx, p["c0"], [t3], p["c2"], res=t3)
+    ref = run_conv(ctx, p["c2"], [run_conv(ctx, p["c0"], [t3])], res=t3)
     assert rel(whole, ref) < 1e-5
 
 
@@ -942,42 +892,3 @@ def test_gelu_epilogue_branch_free_erf():
         assert bool(((y - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all()), hex(hint)
         yt = F.gelu(x.to(DEV)).double().cpu()  # torch's own fp32 GELU meets the same bound
         assert bool(((yt - ref).abs() <= 2.5e-7 * x.double().abs() + 1e-37).all())
-
-
-@pytest.mark.parametrize("B,H,W", [(1, 24, 78), (2, 96, 312), (1, 3, 3), (1, 7, 13), (2, 30, 41)])
-def test_dmstack_fused(B, H, W):
-    """The upsamplers' dm<tag> stack (ESMStereo.py:250-253: BasicConv2d k5 p1 1->16, k3 p1, k3 p1,
-    k1 p1, each BN + GELU) in one launch (esm_dmstack_f32, halo recomputation) vs fp64 torch of the
-    four layers (relative 1e-5, the conv forms' tolerance) and vs the four-launch chain."""
-    from esmstereo_amd.blocks import _dm
-    from esmstereo_amd.engine import dmstack_supported, run_dmstack
-
-    torch.manual_seed(H * 1000 + W)
-    dm = _dm(16).eval()
-    with torch.no_grad():
-        for m in dm:
-            m.conv.weight.uniform_(-0.4, 0.4)
-            m.bn.weight.uniform_(0.5, 1.5)
-            m.bn.bias.uniform_(-0.3, 0.3)
-            m.bn.running_mean.uniform_(-0.2, 0.2)
-            m.bn.running_var.uniform_(0.5, 1.5)
-    x = torch.randn(B, 1, H, W) * 4
-    ref = x.double()
-    with torch.no_grad():
-        for m in dm:
-            c, bn = m.conv, m.bn
-            y = F.conv2d(ref, c.weight.double(), None, c.stride, c.padding)
-            y = F.batch_norm(y, bn.running_mean.double(), bn.running_var.double(), bn.weight.double(),
-                             bn.bias.double(), False, 0.0, bn.eps)
-            ref = F.gelu(y)
-    dm = dm.to(DEV)
-    layers, raw = [m.packed() for m in dm], [m.conv.weight for m in dm]
-    xd = x.to(DEV)
-    assert dmstack_supported(layers, raw, xd)
-    ctx = Ctx(DEV)
-    got = run_dmstack(ctx, layers, raw, xd)
-    torch.cuda.synchronize()
-    assert got.shape == (B, 16, H, W)
-    assert rel(got, ref.float()) < 1e-5
-    chain = dm[3].emit(ctx, [dm[2].emit(ctx, [dm[1].emit(ctx, [dm[0].emit(ctx, [xd])])])])
-    assert rel(got, chain) < 1e-5

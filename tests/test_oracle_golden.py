@@ -79,3 +79,15 @@ def test_oracle_fullsize_vs_reference(name):
                          None if att is None else _t(att), [_t(u) for u in up])
     rep = check_fullsize(name, m, g, out["cost"][:, 0], out["init_pred"], out["disp_0"])
     print(name, rep)
+
+
+def test_oracle_regression_topk_any_k_vs_reference():
+    """oracle.regression_topk for k != 2 against the reference's own regression_topk outputs
+    (tests/golden/topk_k.npz, tie-free costs; make_golden_topk.py), k > D included."""
+    g = load_golden("topk_k.npz")
+    for k in g["ks"].tolist():
+        c, s = torch.from_numpy(g[f"cost_{k}"]), torch.from_numpy(g[f"samples_{k}"])
+        got = O.regression_topk(c, s, k)
+        assert torch.allclose(got, torch.from_numpy(g[f"out_{k}"]), rtol=1e-6, atol=1e-6), k
+    c = torch.randn(2, 12, 3, 5)
+    assert torch.equal(O.regression_topk(c, None, 2), O.regression_topk2(c))
