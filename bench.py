@@ -309,7 +309,7 @@ def cpu_baseline(model, ml, mr, att, up, args, budget_s: float) -> tuple:
     _, cvs = VARIANTS[args.variant]
     times, t0, out = [], time.perf_counter(), None
     with torch.no_grad():
-        while len(times) < 3 or (time.perf_counter() - t0 < budget_s and len(times) < 50):
+        while len(times) < 3 or (time.perf_counter() - t0 < budget_s and len(times) < 400):
             t1 = time.perf_counter()
             out = O.hot_path(sd, cvs, args.maxdisp, args.cv == "gwc", *ins)
             times.append(time.perf_counter() - t1)
