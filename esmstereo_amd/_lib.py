@@ -74,6 +74,12 @@ class EsmShuffleTailDesc(Structure):
                 ("reserved", c_int32)]
 
 
+class EsmShuffleConvDesc(Structure):
+    _fields_ = [("st", EsmShuffleTailDesc), ("w", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
+                ("out", c_void_p), ("ob", c_int64), ("oc", c_int64), ("oh", c_int64),
+                ("C", c_int32), ("cin_pad", c_int32), ("cout_pad", c_int32), ("reserved", c_int32)]
+
+
 class EsmConfDesc(Structure):
     _fields_ = [("op", c_int32), ("B", c_int32), ("C", c_int32), ("D", c_int32), ("H", c_int32), ("W", c_int32),
                 ("x", c_void_p * 4), ("out", c_void_p)]
@@ -94,6 +100,7 @@ SIGNATURES = {
     "esm_smix_f32": (c_int, [POINTER(EsmSmixDesc), c_void_p]),
     "esm_fmnet_f32": (c_int, [POINTER(EsmFmnetDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
+    "esm_shuffle_conv_f32": (c_int, [POINTER(EsmShuffleConvDesc), c_void_p]),
     "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
@@ -104,6 +111,7 @@ SIGNATURES = {
     "esm_plan_add_smix": (c_int, [c_void_p, POINTER(EsmSmixDesc)]),
     "esm_plan_add_fmnet": (c_int, [c_void_p, POINTER(EsmFmnetDesc)]),
     "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
+    "esm_plan_add_shuffle_conv": (c_int, [c_void_p, POINTER(EsmShuffleConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
@@ -136,8 +144,8 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    for which, st in enumerate((EsmSrc, EsmConvDesc, EsmSmixStage, EsmSmixDesc, EsmShuffleTailDesc, EsmFmnetDesc,
-                                    EsmConfDesc)):
+    for which, st in ((0, EsmSrc), (1, EsmConvDesc), (2, EsmSmixStage), (3, EsmSmixDesc), (4, EsmShuffleTailDesc),
+                      (5, EsmFmnetDesc), (6, EsmConfDesc), (8, EsmShuffleConvDesc)):
         if lib.esm_struct_size(which) != ctypes.sizeof(st):
             raise ImportError(f"esmstereo_amd: ABI mismatch for {st.__name__}: "
                               f"C {lib.esm_struct_size(which)} vs ctypes {ctypes.sizeof(st)}")

@@ -23,7 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv, run_shuffle_tail
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv,
+                     run_shuffle_conv, run_shuffle_tail, shuffle_conv_supported)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -131,9 +132,12 @@ class _Hourglass(nn.Module):
         self.agg_0 = nn.Sequential(_bc(cat0, c2, d3, k=1, p=0), _bc(c2, c2, d3))
         self.agg_1 = nn.Sequential(_bc(cat1, c1, d3, k=1, p=0), _bc(c1, c1, d3))
 
-    def _emit(self, ctx: Ctx, x: torch.Tensor, extra0: Sequence[torch.Tensor] = (),
-              extra1: Sequence[torch.Tensor] = (), crop1: bool = True, **last) -> torch.Tensor:
-        c1 = self.conv1[1].emit(ctx, [self.conv1[0].emit(ctx, [x])])
+    def _emit(self, ctx: Ctx, x: Optional[torch.Tensor], extra0: Sequence[torch.Tensor] = (),
+              extra1: Sequence[torch.Tensor] = (), crop1: bool = True, c10: Optional[torch.Tensor] = None,
+              **last) -> torch.Tensor:
+        """``c10``: conv1[0]'s output, when the caller fused that layer into its producer (then ``x`` is
+        not read)."""
+        c1 = self.conv1[1].emit(ctx, [self.conv1[0].emit(ctx, [x]) if c10 is None else c10])
         c2 = self.conv2[1].emit(ctx, [self.conv2[0].emit(ctx, [c1])])
         c3 = self.conv3[1].emit(ctx, [self.conv3[0].emit(ctx, [c2])])
         u3 = self.conv3_up.emit(ctx, [c3])
@@ -178,9 +182,9 @@ class up_refinement(_Hourglass):
         super().__init__()
         self._build(1, C, C, C, 2 * C + cf1, 2 * C + cf2)
 
-    def emit(self, ctx: Ctx, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor,
-             **last) -> torch.Tensor:
-        return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, **last)
+    def emit(self, ctx: Ctx, disp: Optional[torch.Tensor], left_f1x: torch.Tensor, left_f2x: torch.Tensor,
+             c10: Optional[torch.Tensor] = None, **last) -> torch.Tensor:
+        return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, c10=c10, **last)
 
     def forward(self, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor) -> torch.Tensor:
         return self.emit(Ctx(disp.device), disp, left_f1x, left_f2x)
@@ -260,16 +264,25 @@ class _ESMUpsampler(nn.Module):
                 x = run_conv(ctx, p["to_feat"], [x], tag=f"{me}.to_feat")
                 for blk in self.blocks:
                     x = blk.emit(ctx, x)
-            # upsampling (1x1 -> PixelShuffle -> SiLU) + tail (3x3 -> 1): one launch
-            x = run_shuffle_tail(ctx, x, p[f"up_{tag}"], tag=f"{me}.upsampling{tag[:-1]}+tail{tag}")
+            # upsampling (1x1 -> PixelShuffle -> SiLU) + tail (3x3 -> 1): one launch, with the refinement
+            # hourglass's first conv fused behind it where the kernel has the shape
+            ref = getattr(self, f"ref{tag}")
+            c10 = None
+            if shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed()):
+                c10 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(),
+                                       tag=f"{me}.upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1.0")
+                x = None
+            else:
+                x = run_shuffle_tail(ctx, x, p[f"up_{tag}"], tag=f"{me}.upsampling{tag[:-1]}+tail{tag}")
             last = i == n - 1
             epi = dict(up=prev, up_f=r, post_scale=final_scale if last else 1.0)
             if scaled_copies is not None and not last:
-                B, _, H, W = x.shape
-                cp = ctx.empty(B, 1, H, W)
+                B, _, H, W = prev.shape
+                r_ = p[f"up_{tag}"].r
+                cp = ctx.empty(B, 1, H * r_, W * r_)
                 epi.update(out2=cp, post_scale2=scaled_copies)
                 copies.append(cp)
-            prev = getattr(self, f"ref{tag}").emit(ctx, x, feats[ra], feats[rb], **epi)
+            prev = ref.emit(ctx, x, feats[ra], feats[rb], c10=c10, **epi)
             outs.append(prev)
         outs.reverse()
         copies.reverse()

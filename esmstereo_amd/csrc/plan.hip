@@ -17,6 +17,7 @@ int launch_conv(const esm_conv_desc*, hipStream_t);
 int launch_smix(const esm_smix_desc*, hipStream_t);
 int launch_fmnet(const esm_fmnet_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
+int launch_shuffle_conv(const esm_shuffle_conv_desc*, hipStream_t);
 int launch_conf(const esm_conf_desc*, hipStream_t);
 
 namespace {
@@ -32,7 +33,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12 };
 
 struct VolArgs {
     const float* L;
@@ -56,6 +57,7 @@ struct Op {
     esm_smix_desc smix{};
     esm_fmnet_desc fm{};
     esm_shuffle_tail_desc st{};
+    esm_shuffle_conv_desc sc{};
     VolArgs vol{};
     RegArgs reg{};
     esm_conf_desc cf{};
@@ -68,6 +70,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kSmix: return esm::launch_smix(&op.smix, s);
         case kFmnet: return esm::launch_fmnet(&op.fm, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
+        case kShuffleConv: return esm::launch_shuffle_conv(&op.sc, s);
         case kConf: return esm::launch_conf(&op.cf, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
@@ -197,6 +200,7 @@ int esm_struct_size(int which) {
         case 4: return static_cast<int>(sizeof(esm_shuffle_tail_desc));
         case 5: return static_cast<int>(sizeof(esm_fmnet_desc));
         case 6: return static_cast<int>(sizeof(esm_conf_desc));
+        case 8: return static_cast<int>(sizeof(esm_shuffle_conv_desc));
         default: return -1;
     }
 }
@@ -241,6 +245,14 @@ int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc)
     Op op;
     op.kind = kShuffleTail;
     op.st = *desc;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc) {
+    if (!desc) return esm::arg_error("plan: null shuffle_conv desc");
+    Op op;
+    op.kind = kShuffleConv;
+    op.sc = *desc;
     return add_op(plan, std::move(op));
 }
 

@@ -11,7 +11,7 @@
 // LDS broadcasts), then runs the 3x3 conv from LDS, 4 consecutive outputs per thread and one
 // 16-byte store.  Arithmetic per element is the unfused order: bias + sum_i w*x, SiLU, then
 // bias + sum over (channel, ky, kx) of w*v.
-#include "conv_epilogue.h"
+#include "conv_direct.h"
 
 namespace esm {
 namespace {
@@ -232,6 +232,202 @@ int launch_nr(const esm_shuffle_tail_desc& a, hipStream_t s) {
     return big >= 256 ? launch_tile<NF, R, TH, 64>(a, s) : launch_tile<NF, R, 8, 32>(a, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// shuffle_tail followed by the refinement hourglass's first conv, in one launch:
+//   x  = tail(SiLU(PixelShuffle(r)(up(lowres))))              (the 1-channel map, never stored)
+//   c1 = GELU(BN(Conv2d(1, C, 3, stride 2, pad 1)(x)))          (up_refinement.conv1[0])
+// (models/ESMStereo.py:301-303 / :311-313: `x = self.tail(self.upsampling(x))`, then
+// `self.ref(x, ...)` whose first layer is BasicConv(1, C, 3, 2, 1) at :190-191).  A workgroup owns a
+// TH2 x 16 tile of c1 (all C channels); it stages the low-resolution window under the tile, builds
+// the shuffled map on it with MFMA (M = the r*r sub-pixels of 16/(r*r) channels, N = 16 low-res pixels,
+// K = nf), runs the 3x3 tail on the (2*TH2 + 1) x 33 x window, then conv1 from LDS.  The x map (1.9 MB
+// at S-K) and its re-read by a separate conv launch disappear.  Arithmetic per element follows the
+// two unfused kernels (shuffle_tail_kernel, conv_stem.hip c1in_kernel).
+template <int NF, int R, int C, int TH2>
+struct ScGeo {
+    static constexpr int TW2 = 16;
+    static constexpr int RR = R * R;
+    static constexpr int NUP = NF * RR;
+    static constexpr int LRH = 2 * TH2 / R + 2, LRW = 2 * TW2 / R + 2;  // low-res window
+    static constexpr int PIX = LRH * LRW;
+    static constexpr int MR = LRH * R, MC = LRW * R + 4;                 // shuffled window (padded row)
+    static constexpr int XH = 2 * TH2 + 1, XW = 2 * TW2 + 1, XWP = 36;  // x window
+    static constexpr int CPT = 16 / RR;                                  // channels per MFMA M-tile
+    static constexpr int NMT = NF / CPT;
+    static constexpr int NNT = (PIX + 15) / 16;
+    // weights: up_w [NUP][NF], up_b [NUP], tail_w [NF*9], tail_b, c1 w [9][C], scale [C], shift [C]
+    static constexpr int OW_UB = NUP * NF, OW_TW = OW_UB + NUP, OW_TB = OW_TW + NF * 9, OW_CW = OW_TB + 1,
+                         OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, WN = OW_SH + C;
+};
+
+template <int NF, int R, int C, int TH2>
+__global__ void __launch_bounds__(kThreads) shuffle_conv_kernel(const esm_shuffle_conv_desc a) {
+    using G = ScGeo<NF, R, C, TH2>;
+    constexpr int TW2 = G::TW2, RR = G::RR, LRW = G::LRW, PIX = G::PIX, MR = G::MR, MC = G::MC;
+    constexpr int XH = G::XH, XW = G::XW, XWP = G::XWP, WN = G::WN;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ float lr[NF][PIX];
+    __shared__ __attribute__((aligned(16))) float mid[NF][MR][MC];
+    __shared__ float xs[XH][XWP];
+
+    const esm_shuffle_tail_desc& t = a.st;
+    const int tid = threadIdx.x;
+    const int H = t.H, W = t.W, HO = H * R, WO = W * R;
+    const int b = blockIdx.z;
+    const int y0 = blockIdx.y * TH2, x0 = blockIdx.x * TW2;  // c1 tile origin
+    const int ly0 = 2 * y0 / R - 1, lx0 = 2 * x0 / R - 1;    // low-res window origin (mid row 0 = ly0 * R)
+    const float* xb = t.x + b * t.xb;
+
+    // ---- stage weights and the low-res window (one round trip)
+    constexpr int WR = (WN + kThreads - 1) / kThreads;
+    constexpr int LN = NF * PIX;
+    constexpr int LR_ = (LN + kThreads - 1) / kThreads;
+    float rw[WR], rx[LR_];
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        const int i = tid + k * kThreads;
+        const float* p;
+        int off;
+        if (i < G::OW_UB) { p = t.up_w; off = i; }
+        else if (i < G::OW_TW) { p = t.up_b; off = i - G::OW_UB; }
+        else if (i < G::OW_TB) { p = t.tail_w; off = i - G::OW_TW; }
+        else if (i < G::OW_CW) { p = t.tail_b; off = 0; }
+        else if (i < G::OW_SC) { p = a.w; off = (i - G::OW_CW) / C * a.cin_pad * a.cout_pad + (i - G::OW_CW) % C; }
+        else if (i < G::OW_SH) { p = a.scale; off = i - G::OW_SC; }
+        else { p = a.shift; off = i - G::OW_SH; }
+        const bool ok = i < WN && p != nullptr;
+        const float v = (ok ? p : t.up_w)[ok ? off : 0];
+        rw[k] = ok ? v : (i >= G::OW_SC && i < G::OW_SH ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < LR_; ++k) {
+        const int i = tid + k * kThreads;
+        const int c = i / PIX, rem = i - c * PIX;
+        const int yy = ly0 + rem / LRW, xx = lx0 + rem % LRW;
+        const bool ok = i < LN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        const float v = xb[ok ? c * t.xc + yy * t.xh + xx : 0];
+        rx[k] = ok ? v : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
+#pragma unroll
+    for (int k = 0; k < WR; ++k)
+        if (tid + k * kThreads < WN) wsh[tid + k * kThreads] = rw[k];
+#pragma unroll
+    for (int k = 0; k < LR_; ++k)
+        if (tid + k * kThreads < LN) (&lr[0][0])[tid + k * kThreads] = rx[k];
+    __syncthreads();
+
+    // ---- shuffled window: unit (M-tile mt, N-tile nt); lane (g, n): MFMA rows 4g + j = (channel
+    //      mt * CPT + m / RR, sub-pixel m % RR) of low-res pixel nt * 16 + n
+    {
+        const int wave = tid >> 6, lane = tid & 63, g = lane >> 4, n = lane & 15;
+        for (int u = wave; u < G::NMT * G::NNT; u += kThreads / 64) {
+            const int mt = u % G::NMT, nt = u / G::NMT;
+            const int p = nt * 16 + n;
+            const bool pin = p < PIX;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < NF / 4; ++kk) {
+                const float av = wsh[(mt * 16 + n) * NF + 4 * kk + g];  // A[m = n][k]: up_w row (channel, sub-pixel)
+                const float bv = lr[4 * kk + g][pin ? p : 0];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+            }
+            const int py = p / LRW, px = p - (p / LRW) * LRW;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int m = 4 * g + j;
+                const int c = mt * G::CPT + m / RR, sp = m % RR, sy = sp / R, sx = sp % R;
+                const int my = py * R + sy, mx = px * R + sx;  // window coordinates
+                const int Y = ly0 * R + my, X = lx0 * R + mx;
+                const float v = silu_fast(acc[j] + wsh[G::OW_UB + mt * 16 + m]);
+                if (pin) mid[c][my][mx] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? v : 0.f;  // tail zero padding
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- x window (rows 2*y0 - 1 ..., cols 2*x0 - 1 ...): 4 consecutive columns per thread
+    {
+        constexpr int QPR = (XW + 3) / 4;
+        const int XY0 = 2 * y0 - 1, XX0 = 2 * x0 - 1;
+        const int oy = XY0 - 1 - ly0 * R, ox = XX0 - 1 - lx0 * R;  // mid window position of x (0, 0)'s tap (0, 0)
+        const float tb = wsh[G::OW_TB];
+        for (int q = tid; q < XH * QPR; q += kThreads) {
+            const int r = q / QPR, g = q - (q / QPR) * QPR;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+            for (int c = 0; c < NF; ++c) {
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky) {
+                    float v[6];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) v[j] = mid[c][oy + r + ky][min(ox + 4 * g + j, MC - 1)];
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                    }
+                }
+            }
+            const int Y = XY0 + r;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int X = XX0 + 4 * g + j;
+                if (4 * g + j < XW) xs[r][4 * g + j] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc[j] + tb : 0.f;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- c1 = GELU(BN(conv 3x3 s2 p1 (x))): thread = (pixel, half of the channels)
+    {
+        constexpr int NPX = TH2 * TW2;
+        constexpr int CH = C * NPX / kThreads;  // channels per thread
+        const int pxi = tid % NPX, c0 = (tid / NPX) * CH;
+        const int yy = pxi / TW2, xx = pxi % TW2;
+        const int oy = y0 + yy, ox = x0 + xx;
+        float xv[9];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) xv[ky * 3 + kx] = xs[2 * yy + ky][2 * xx + kx];
+        const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
+        const bool ok = oy < Ho2 && ox < Wo2;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            a.out + b * a.ob, static_cast<short>(0),
+            static_cast<int>(4 * ((C - 1) * a.oc + (Ho2 - 1) * a.oh + Wo2)), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int co = c0 + k;
+            float acc = 0.f;
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) acc += wsh[G::OW_CW + tp * C + co] * xv[tp];
+            const float v = gelu_erf(acc * wsh[G::OW_SC + co] + wsh[G::OW_SH + co]);
+            const unsigned o = ok ? 4u * static_cast<unsigned>(co * a.oc + static_cast<long long>(oy) * a.oh + ox)
+                                  : conv::kOOB;
+            conv::store_b32(__float_as_uint(v), ro, static_cast<int>(o), 0);
+        }
+    }
+}
+
+template <int NF, int R, int C>
+int launch_sc(const esm_shuffle_conv_desc& a, hipStream_t s) {
+    const esm_shuffle_tail_desc& t = a.st;
+    const long long Ho2 = (static_cast<long long>(t.H) * R + 1) / 2, Wo2 = (static_cast<long long>(t.W) * R + 1) / 2;
+    // 8-row c1 tiles where that leaves the chip ~one workgroup per CU, else 4 rows
+    const long long big = ceil_div(Wo2, 16) * ceil_div(Ho2, 8) * t.B;
+    if (big >= 256) {
+        const dim3 grid(ceil_div(Wo2, 16), ceil_div(Ho2, 8), t.B);
+        if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
+        hipLaunchKernelGGL((shuffle_conv_kernel<NF, R, C, 8>), grid, dim3(kThreads), 0, s, a);
+    } else {
+        const dim3 grid(ceil_div(Wo2, 16), ceil_div(Ho2, 4), t.B);
+        hipLaunchKernelGGL((shuffle_conv_kernel<NF, R, C, 4>), grid, dim3(kThreads), 0, s, a);
+    }
+    return check_launch("shuffle_conv");
+}
+
 }  // namespace
 
 int launch_shuffle_tail(const esm_shuffle_tail_desc* d, hipStream_t s) {
@@ -249,8 +445,31 @@ int launch_shuffle_tail(const esm_shuffle_tail_desc* d, hipStream_t s) {
     return ESM_ERR_UNSUPPORTED;
 }
 
+int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
+    if (!d) return arg_error("shuffle_conv: null descriptor");
+    const esm_shuffle_conv_desc& a = *d;
+    const esm_shuffle_tail_desc& t = a.st;
+    if (!t.x || !t.up_w || !t.up_b || !t.tail_w || !a.w || !a.out) return arg_error("shuffle_conv: null pointer");
+    if (t.B <= 0 || t.H <= 0 || t.W <= 0) return arg_error("shuffle_conv: bad size");
+    if (t.xh < t.W || t.xc < static_cast<long long>(t.H) * t.xh) return arg_error("shuffle_conv: strides inconsistent");
+    if (a.cin_pad < 1 || a.cout_pad < a.C) return arg_error("shuffle_conv: bad conv weight padding");
+    const long long Ho2 = (static_cast<long long>(t.H) * t.r + 1) / 2, Wo2 = (static_cast<long long>(t.W) * t.r + 1) / 2;
+    if (a.oh < Wo2 || a.oc < Ho2 * a.oh || a.ob < a.C * a.oc) return arg_error("shuffle_conv: output strides");
+    if (4 * (a.C * a.oc) >= 0x7fffffffLL) return arg_error("shuffle_conv: output too large");
+    if (t.nf == 8 && t.r == 4 && a.C == 16) return launch_sc<8, 4, 16>(a, s);
+    if (t.nf == 8 && t.r == 2 && a.C == 16) return launch_sc<8, 2, 16>(a, s);
+    if (t.nf == 16 && t.r == 2 && a.C == 32) return launch_sc<16, 2, 32>(a, s);
+    if (t.nf == 16 && t.r == 4 && a.C == 32) return launch_sc<16, 4, 32>(a, s);
+    set_error("shuffle_conv: (nf, r, C) must be one of (8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)");
+    return ESM_ERR_UNSUPPORTED;
+}
+
 }  // namespace esm
 
 extern "C" int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream) {
     return esm::launch_shuffle_tail(desc, esm::as_stream(stream));
+}
+
+extern "C" int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream) {
+    return esm::launch_shuffle_conv(desc, esm::as_stream(stream));
 }

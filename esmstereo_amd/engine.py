@@ -22,8 +22,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleTailDesc,
-                   EsmSmixDesc, check, lib)
+from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleConvDesc,
+                   EsmShuffleTailDesc, EsmSmixDesc, check, lib)
 
 __all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_fmnet", "run_shuffle_tail", "pack_shuffle_tail",
            "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID"]
@@ -254,6 +254,12 @@ class Ctx:
             check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
         else:
             check(lib.esm_shuffle_tail_f32(ctypes.byref(d), self.stream), "shuffle_tail")
+
+    def shuffle_conv(self, d: EsmShuffleConvDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv")
+        else:
+            check(lib.esm_shuffle_conv_f32(ctypes.byref(d), self.stream), "shuffle_conv")
 
     def gwc(self, L, R, att, V, B, C, H, W, D, G) -> None:
         self.meta.append(dict(name="gwc_volume", kind="gwc", flops=2 * B * C * D * H * W,
@@ -642,4 +648,55 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
                          bytes=4 * (B * nf * H * W + npix), shape=f"nf{nf} r{r} in {H}x{W} out {H * r}x{W * r}",
                          reads=_spans(x), writes=_spans(out)))
     ctx.shuffle_tail(d)
+    return out
+
+
+# tail(upsampling(x)) and the refinement's first conv in one launch (esm_shuffle_conv_f32);
+# ESM_SHUFFLE_CONV=0 runs them as two launches (A/B measurements)
+SHUFFLE_CONV_ENABLED = os.environ.get("ESM_SHUFFLE_CONV", "1") != "0"
+
+
+def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv) -> bool:
+    return SHUFFLE_CONV_ENABLED and (p.nf, p.r, conv.cout) in ((8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)) and \
+        conv.nd == 2 and not conv.transposed and (conv.k, conv.stride, conv.pad, conv.cin) == (3, 2, 1, 1) and \
+        conv.act == ACT_GELU
+
+
+def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: PackedConv,
+                     tag: str = "shuffle_conv") -> torch.Tensor:
+    """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
+    3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
+    stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)]."""
+    require_device(x, "shuffle_conv input")
+    B, nf, H, W = (int(v) for v in x.shape)
+    r = p.r
+    if nf != p.nf:
+        raise RuntimeError(f"shuffle_conv: input has {nf} channels, layer expects {p.nf}")
+    if not shuffle_conv_supported(p, conv):
+        raise ValueError("shuffle_conv: unsupported head / conv geometry")
+    Ho2, Wo2 = (H * r + 1) // 2, (W * r + 1) // 2
+    out = ctx.empty(B, conv.cout, Ho2, Wo2)
+    require_on(x.device, "shuffle_conv", x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
+    d = EsmShuffleConvDesc()
+    t = d.st
+    t.x = x.data_ptr()
+    t.xb, t.xc, t.xh = x.stride(0), x.stride(1), x.stride(2)
+    t.up_w, t.up_b, t.tail_w = p.up_w.data_ptr(), p.up_b.data_ptr(), p.tail_w.data_ptr()
+    t.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
+    t.out = None
+    t.B, t.nf, t.H, t.W, t.r = B, nf, H, W, r
+    d.w = conv.w.data_ptr()
+    d.scale = conv.scale.data_ptr() if conv.scale is not None else None
+    d.shift = conv.shift.data_ptr() if conv.shift is not None else None
+    d.out = out.data_ptr()
+    d.ob, d.oc, d.oh = out.stride(0), out.stride(1), out.stride(2)
+    d.C, d.cin_pad, d.cout_pad = conv.cout, conv.cin_pad, conv.cout_pad
+    ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
+    npix = B * H * W * r * r
+    flops = 2 * npix * nf * (1 + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9
+    ctx.meta.append(dict(name=tag, kind="shuffle_conv", flops=flops,
+                         bytes=4 * (B * nf * H * W + B * conv.cout * Ho2 * Wo2),
+                         shape=f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}",
+                         reads=_spans(x), writes=_spans(out)))
+    ctx.shuffle_conv(d)
     return out

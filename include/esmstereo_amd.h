@@ -28,6 +28,8 @@
  *                             upsample16 twins): `upsampling` (Conv2d 1x1 nf -> nf*r*r + bias,
  *                             PixelShuffle(r), SiLU) followed by `tail` (Conv2d 3x3 nf -> 1 +
  *                             bias) as one kernel; the shuffled map is never materialised
+ *   esm_shuffle_conv_f32      the same head followed by up_refinement.conv1[0] (models/ESMStereo.py:
+ *                             190-191, the refinement's first BasicConv(1, C, 3, 2, 1)) in one kernel
  *   esm_conf_f32              the per-pixel stages of the confidence head LAFNet_ESM /
  *                             conf_upsample (models/ESMStereo_confidence.py:511-744) between its
  *                             convs (which run through esm_conv_f32): cost features, attention,
@@ -203,10 +205,27 @@ typedef struct {
     int32_t reserved;
 } esm_shuffle_tail_desc;
 
+/* `tail(upsampling(x))` (as esm_shuffle_tail_desc, st.out unused) followed by the refinement
+ * hourglass's first layer BasicConv(1, C, 3, stride 2, pad 1) + folded BN + exact GELU
+ * (up_refinement.conv1[0], models/ESMStereo.py:190-191), in one launch; the 1-channel map between
+ * them is never stored.  w: packed conv weights [9][cin_pad][cout_pad] (cin 1); scale/shift: the
+ * folded BN (scale NULL = 1); out: [B, C, ceil(r*H/2), ceil(r*W/2)] with strides ob, oc, oh.
+ * (nf, r, C) in {(8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)}. */
+typedef struct {
+    esm_shuffle_tail_desc st;
+    const float* w;
+    const float* scale;
+    const float* shift;
+    float* out;
+    int64_t ob, oc, oh;
+    int32_t C, cin_pad, cout_pad, reserved;
+} esm_shuffle_conv_desc;
+
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
- * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc;
+ * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc,
+ * 8 esm_shuffle_conv_desc;
  * -1 for an unknown id. */
 int esm_struct_size(int which);
 
@@ -229,6 +248,7 @@ int esm_conv_f32(const esm_conv_desc* desc, void* stream);
 int esm_smix_f32(const esm_smix_desc* desc, void* stream);
 int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
+int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
 /* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
  *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D <= 64) -> out [B,7,H,W]: the 7 largest of
  *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
@@ -278,6 +298,7 @@ int esm_plan_add_conv(esm_plan* plan, const esm_conv_desc* desc);
 int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
 int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
+int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
@@ -289,7 +310,7 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 9 = fmnet, 10 = conf (8 and 11 were retired fused forms) */
+ * 7 = shuffle_tail, 9 = fmnet, 10 = conf, 12 = shuffle_conv (8 and 11 were retired fused forms) */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

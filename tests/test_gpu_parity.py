@@ -556,6 +556,31 @@ def test_shuffle_tail(nf, r, H, W):
     assert rel(y, ref) < 1e-5
 
 
+@pytest.mark.parametrize("nf,r,C,H,W", [(8, 4, 16, 24, 78), (8, 4, 16, 96, 312), (8, 4, 16, 7, 13), (8, 2, 16, 13, 29),
+                                         (16, 2, 32, 17, 40), (16, 4, 32, 9, 21), (8, 2, 16, 48, 156)])
+def test_shuffle_conv_fused(nf, r, C, H, W):
+    """tail(upsampling(x)) + the refinement's first BasicConv(1, C, 3, 2, 1) in one launch
+    (esm_shuffle_conv_f32, models/ESMStereo.py:301-303 + :190-191) vs fp64 torch of the three reference
+    modules and vs the two-launch path (shuffle_tail, then the conv); relative 1e-5, batch 2, ragged."""
+    from esmstereo_amd.engine import pack_shuffle_tail, run_shuffle_conv, run_shuffle_tail
+    torch.manual_seed(nf * 1000 + r * 10 + H)
+    up = torch.nn.Conv2d(nf, nf * r * r, 1, 1, 0)
+    tail = torch.nn.Conv2d(nf, 1, 3, 1, 1)
+    conv, bn = _mk(2, 1, C, 3, 2, 1, seed=H)
+    x = torch.randn(2, nf, H, W)
+    t = F.conv2d(F.silu(F.pixel_shuffle(F.conv2d(x.double(), up.weight.double(), up.bias.double()), r)),
+                 tail.weight.double(), tail.bias.double(), 1, 1)
+    ref = _ref_conv([t], conv, bn, ACT_GELU)
+    p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), r)
+    pc = pk(conv, bn, ACT_GELU)
+    ctx = Ctx(DEV)
+    y = run_shuffle_conv(ctx, x.to(DEV), p, pc)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-5
+    two = run_conv(ctx, pc, [run_shuffle_tail(ctx, x.to(DEV), p)])
+    assert rel(y, two) < 1e-5
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
