@@ -101,6 +101,7 @@ SIGNATURES = {
     "esm_fmnet_f32": (c_int, [POINTER(EsmFmnetDesc), c_void_p]),
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
     "esm_shuffle_conv_f32": (c_int, [POINTER(EsmShuffleConvDesc), c_void_p]),
+    "esm_conv_pair2_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
@@ -112,6 +113,7 @@ SIGNATURES = {
     "esm_plan_add_fmnet": (c_int, [c_void_p, POINTER(EsmFmnetDesc)]),
     "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
     "esm_plan_add_shuffle_conv": (c_int, [c_void_p, POINTER(EsmShuffleConvDesc)]),
+    "esm_plan_add_conv_pair2": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),

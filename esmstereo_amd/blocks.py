@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv,
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv, run_pair2,
                      run_shuffle_conv, run_shuffle_tail, shuffle_conv_supported)
 from .mixer import FMBlock
 
@@ -101,11 +101,13 @@ def _up(cin: int, cout: int, is_3d: bool, last: bool = False) -> BasicConv:
 
 def _pair(ctx: Ctx, first: BasicConv, srcs: Sequence[torch.Tensor], second, second_packed: Optional[PackedConv] = None,
           **kw) -> torch.Tensor:
-    """``second(first(cat(srcs)))``: two launches.  (Fused two-conv forms measured slower than two
-    register-weight launches on MI355X and were retired)"""
+    """``second(first(cat(srcs)))``: one launch with the intermediate in LDS where conv_pair2.hip has the
+    shape (2-D, plain BN + GELU epilogues), else two launches."""
     n0 = getattr(first, "_esm_name", "BasicConv")
     n1 = getattr(second, "_esm_name", "conv") if second is not None else "conv"
     pb = second_packed if second_packed is not None else second.packed()
+    if not kw:
+        return run_pair2(ctx, first.packed(), srcs, pb, tags=(n0, n1))
     mid = run_conv(ctx, first.packed(), srcs, tag=n0)
     return run_conv(ctx, pb, [mid], tag=n1, **kw)
 
@@ -137,9 +139,9 @@ class _Hourglass(nn.Module):
               **last) -> torch.Tensor:
         """``c10``: conv1[0]'s output, when the caller fused that layer into its producer (then ``x`` is
         not read)."""
-        c1 = self.conv1[1].emit(ctx, [self.conv1[0].emit(ctx, [x]) if c10 is None else c10])
-        c2 = self.conv2[1].emit(ctx, [self.conv2[0].emit(ctx, [c1])])
-        c3 = self.conv3[1].emit(ctx, [self.conv3[0].emit(ctx, [c2])])
+        c1 = self.conv1[1].emit(ctx, [c10]) if c10 is not None else _pair(ctx, self.conv1[0], [x], self.conv1[1])
+        c2 = _pair(ctx, self.conv2[0], [c1], self.conv2[1])
+        c3 = _pair(ctx, self.conv3[0], [c2], self.conv3[1])
         u3 = self.conv3_up.emit(ctx, [c3])
         a0 = _pair(ctx, self.agg_0[0], [_crop_like(u3, c2), c2, *extra0], self.agg_0[1])
         u2 = self.conv2_up.emit(ctx, [a0])
@@ -254,9 +256,8 @@ class _ESMUpsampler(nn.Module):
         n = len(self.STAGES)
         for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
             dm = getattr(self, f"dm{tag}")
-            d = dm[0].emit(ctx, [prev])
-            d = _pair(ctx, dm[1], [d], dm[2])
-            d = dm[3].emit(ctx, [d])
+            d = _pair(ctx, dm[0], [prev], dm[1])
+            d = _pair(ctx, dm[2], [d], dm[3])
             spx = getattr(self, f"spx_{tag}")
             c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c

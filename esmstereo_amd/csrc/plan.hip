@@ -18,6 +18,9 @@ int launch_smix(const esm_smix_desc*, hipStream_t);
 int launch_fmnet(const esm_fmnet_desc*, hipStream_t);
 int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 int launch_shuffle_conv(const esm_shuffle_conv_desc*, hipStream_t);
+namespace conv {
+int launch_pair2(const esm_conv_desc&, const esm_conv_desc&, hipStream_t);
+}
 int launch_conf(const esm_conf_desc*, hipStream_t);
 
 namespace {
@@ -33,7 +36,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12, kPair2 = 13 };
 
 struct VolArgs {
     const float* L;
@@ -54,6 +57,7 @@ struct RegArgs {
 struct Op {
     int kind = 0;
     esm_conv_desc conv{};
+    esm_conv_desc conv2{};
     esm_smix_desc smix{};
     esm_fmnet_desc fm{};
     esm_shuffle_tail_desc st{};
@@ -71,6 +75,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kFmnet: return esm::launch_fmnet(&op.fm, s);
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
         case kShuffleConv: return esm::launch_shuffle_conv(&op.sc, s);
+        case kPair2: return esm::conv::launch_pair2(op.conv, op.conv2, s);
         case kConf: return esm::launch_conf(&op.cf, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
@@ -245,6 +250,15 @@ int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc)
     Op op;
     op.kind = kShuffleTail;
     op.st = *desc;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b) {
+    if (!a || !b) return esm::arg_error("plan: null conv pair desc");
+    Op op;
+    op.kind = kPair2;
+    op.conv = *a;
+    op.conv2 = *b;
     return add_op(plan, std::move(op));
 }
 

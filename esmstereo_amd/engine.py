@@ -255,6 +255,12 @@ class Ctx:
         else:
             check(lib.esm_shuffle_tail_f32(ctypes.byref(d), self.stream), "shuffle_tail")
 
+    def pair2(self, a: EsmConvDesc, b: EsmConvDesc) -> None:
+        if self.plan:
+            check(lib.esm_plan_add_conv_pair2(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair2")
+        else:
+            check(lib.esm_conv_pair2_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair2")
+
     def shuffle_conv(self, d: EsmShuffleConvDesc) -> None:
         if self.plan:
             check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv")
@@ -344,6 +350,11 @@ if os.path.exists(_TUNED_PATH) and not os.environ.get("ESM_NO_TUNED"):
         TUNED_HINTS = {k: int(v) for k, v in json.load(_f).get("hints", {}).items()}
 
 
+# The row-block LDS-staged form is the automatic choice for 3x3x3 stems with <= 8 couts; ESM_ROWS3=0 runs
+# the plane-streaming form instead (A/B measurements)
+ROWS3_ENABLED = os.environ.get("ESM_ROWS3", "1") != "0"
+
+
 def conv_key(d: EsmConvDesc, nd: int) -> str:
     """Shape key of a conv launch: geometry, source channel split, batch, input extent and the
     epilogue features that change the store path."""
@@ -378,8 +389,9 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
                mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
                up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
                out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
-               hint: int = 0):
-    """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta)."""
+               hint: int = 0, alloc_out: bool = True):
+    """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta).
+    ``alloc_out=False`` (the first conv of a fused pair) leaves the output pointer NULL."""
     nd = pc.nd
     d = EsmConvDesc()
     if not srcs or len(srcs) > _lib.MAX_SRC:
@@ -433,7 +445,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     d.act = pc.act
     r = int(shuffle)
     d.shuffle = r
-    if out is None:
+    if out is None and alloc_out:
         if r > 1:
             if pc.cout % (r * r):
                 raise ValueError("pixel shuffle: Cout not divisible by r^2")
@@ -477,6 +489,9 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
+    if not ROWS3_ENABLED and d.hint == 0 and nd == 3 and not pc.transposed and (pc.k, pc.stride, pc.pad) == (3, 1, 1) \
+            and pc.cout <= 8 and pc.cin % 4 == 0 and 4 <= pc.cin <= 32 and len(srcs) == 1:
+        d.hint = 1 << 24  # the plane-streaming form instead of the row-block form (A/B measurements)
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd
     if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap
@@ -491,6 +506,41 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
                       f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
                 reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint)
     return d, out, meta
+
+
+# Two consecutive 2-D BasicConvs as one launch (esm_conv_pair2_f32, conv_pair2.hip); ESM_PAIR2=0
+# runs every pair as two launches (A/B measurements)
+PAIR2_ENABLED = os.environ.get("ESM_PAIR2", "1") != "0"
+
+
+def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
+    """Python mirror of conv_pair2.hip pair2_ok (plus the on/off switch)."""
+    if not PAIR2_ENABLED or pa.nd != 2 or pb.nd != 2 or pa.transposed or pb.transposed:
+        return False
+    if pa.cout != 16 or pb.cin != 16 or pb.cout > 16 or pa.cin > (64 if pa.k == 1 else 48):
+        return False
+    if not ((pa.k == 3 and pa.stride in (1, 2)) or (pa.k in (1, 5) and pa.stride == 1)):
+        return False
+    if pb.stride != 1 or pb.k not in (1, 3) or pa.act != ACT_GELU or pb.act != ACT_GELU:
+        return False
+    return len(srcs) == 1 or all(int(t.shape[1]) % 4 == 0 for t in srcs)
+
+
+def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
+              tags: Tuple[str, str] = ("convA", "convB")) -> torch.Tensor:
+    """``pb(pa(cat(srcs)))`` (two BasicConvs, BN + GELU each) as one launch when supported, else two."""
+    if not pair2_supported(pa, pb, srcs):
+        return run_conv(ctx, pb, [run_conv(ctx, pa, srcs, tag=tags[0])], tag=tags[1])
+    da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
+    B = int(srcs[0].shape[0])
+    virt = srcs[0].as_strided((B, pa.cout, int(da.Ho), int(da.Wo)), (0, 0, 0, 1))  # geometry only, never read
+    db, out, mb = _conv_desc(ctx, pb, [virt], tag=tags[1])
+    mid = 4 * B * pa.cout * int(da.Ho) * int(da.Wo)
+    ctx.meta.append(dict(name=f"{tags[0]}+{tags[1].rsplit('.', 1)[-1]}", kind="conv_pair", flops=ma["flops"] + mb["flops"],
+                         bytes=ma["bytes"] - mid + mb["bytes"] - mid, shape=f"pair {ma['shape']} + {mb['shape']}",
+                         reads=ma["reads"], writes=mb["writes"], key=ma["key"] + " | " + mb["key"], hint=0))
+    ctx.pair2(da, db)
+    return out
 
 
 @dataclass

@@ -249,6 +249,14 @@ int esm_smix_f32(const esm_smix_desc* desc, void* stream);
 int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream);
 int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* stream);
 int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
+/* Two consecutive 2-D BasicConvs in one launch (the intermediate map stays in LDS; halo recomputed):
+ * out_b = GELU(BN_b(conv_b(GELU(BN_a(conv_a(cat(a->src))))))).  a: k 1/3/5 stride 1 or k 3 stride 2,
+ * 16 outputs, <= 48 input channels (64 for k 1) over 1..3 sources (4-channel multiples when several);
+ * a->out is not written.  b: k 1 or 3, stride 1, 16 inputs (its src[] is ignored: the input is a's
+ * output), <= 16 outputs, plain epilogue.  ESM_ERR_ARG for a pair outside that set.
+ * (models/ESMStereo.py:185-259: the refinement hourglasses' conv2 / conv3 pairs and the upsampler
+ * stages' dm<t> / spx_<t> pairs.) */
+int esm_conv_pair2_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
 /* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
  *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D <= 64) -> out [B,7,H,W]: the 7 largest of
  *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
@@ -299,6 +307,7 @@ int esm_plan_add_smix(esm_plan* plan, const esm_smix_desc* desc);
 int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
 int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc);
+int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
@@ -310,7 +319,8 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 9 = fmnet, 10 = conf, 12 = shuffle_conv (8 and 11 were retired fused forms) */
+ * 7 = shuffle_tail, 9 = fmnet, 10 = conf, 12 = shuffle_conv, 13 = conv_pair2 (8 and 11 were retired
+ * fused forms) */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */

@@ -581,6 +581,39 @@ def test_shuffle_conv_fused(nf, r, C, H, W):
     assert rel(y, two) < 1e-5
 
 
+PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones
+    ((1,), 5, 1, 1, 3, 1, 16, 24, 78),           # dm<t>.0 -> dm<t>.1
+    ((16,), 3, 1, 1, 1, 1, 16, 22, 76),          # dm<t>.2 -> dm<t>.3 (k1 p1: the GELU(shift) ring)
+    ((16, 32), 3, 1, 1, 3, 1, 16, 24, 78),       # spx_2x.0 -> spx_2x.1 (cat of d and a feature map)
+    ((16, 24), 3, 1, 1, 3, 1, 8, 96, 312),       # spx_4x.0 -> spx_4x.1 (16 -> 8)
+    ((16,), 3, 2, 1, 3, 1, 16, 48, 156),         # conv2.0 (s2) -> conv2.1
+    ((16,), 3, 2, 1, 3, 1, 16, 25, 79),          # odd extents
+    ((16, 16, 32), 1, 1, 0, 3, 1, 16, 24, 78),   # agg_0.0 (1x1 over three sources) -> agg_0.1
+    ((1,), 5, 1, 1, 3, 1, 16, 7, 9),
+    ((12,), 3, 1, 1, 3, 1, 12, 5, 40),
+]
+
+
+@pytest.mark.parametrize("cins,ka,sa,pa,kb,pb,coutb,H,W", PAIR2_CASES)
+def test_conv_pair2(cins, ka, sa, pa, kb, pb, coutb, H, W):
+    """Two BasicConvs in one launch (conv_pair2.hip: the intermediate in LDS, halo recomputed) vs fp64 torch of
+    the two layers and vs the two separate launches (relative 1e-5), batch 2."""
+    from esmstereo_amd.engine import pair2_supported, run_pair2
+    ca, ba = _mk(2, sum(cins), 16, ka, sa, pa, seed=31 + H)
+    cb, bb = _mk(2, 16, coutb, kb, 1, pb, seed=32 + W)
+    xs = [torch.randn(2, c, H, W) for c in cins]
+    ref = _ref_conv([_ref_conv(xs, ca, ba, ACT_GELU)], cb, bb, ACT_GELU)
+    pa_, pb_ = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
+    xd = [x.to(DEV) for x in xs]
+    assert pair2_supported(pa_, pb_, xd)
+    ctx = Ctx(DEV)
+    y = run_pair2(ctx, pa_, xd, pb_)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-5
+    two = run_conv(ctx, pb_, [run_conv(ctx, pa_, xd)])
+    assert rel(y, two) < 1e-5
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
