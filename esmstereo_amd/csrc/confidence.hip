@@ -18,8 +18,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kTopK = 7;
-constexpr int kMaxD = 64;
-
+// One thread per pixel, the disparity column re-read from L1/L2 in each pass (no per-thread array:
+// any D, no scratch).  Every pass recomputes -(x / nrm) * 100 with the same operations, so the values
+// are those of a single pass.
 __global__ void __launch_bounds__(kThreads) cost_features_kernel(const float* __restrict__ cost, float* __restrict__ out,
                                                                  int B, int D, int H, int W) {
     const long long plane = static_cast<long long>(H) * W;
@@ -27,30 +28,23 @@ __global__ void __launch_bounds__(kThreads) cost_features_kernel(const float* __
     if (i >= B * plane) return;
     const long long b = i / plane, p = i - b * plane;
     const float* c = cost + b * D * plane + p;
-    float v[kMaxD];
     float ss = 0.f;
     for (int d = 0; d < D; ++d) {
-        v[d] = c[d * plane];
-        ss += v[d] * v[d];
+        const float v = c[d * plane];
+        ss += v * v;
     }
     // x / (sum x^2 + 1e-6) ** 0.5, then softmax(-100 * .): max, exp, sum, divide (torch order)
     const float nrm = sqrtf(ss + 1e-6f);
     float mx = -INFINITY;
-    for (int d = 0; d < D; ++d) {
-        v[d] = -(v[d] / nrm) * 100.f;
-        mx = fmaxf(mx, v[d]);
-    }
+    for (int d = 0; d < D; ++d) mx = fmaxf(mx, -(c[d * plane] / nrm) * 100.f);
     float se = 0.f;
-    for (int d = 0; d < D; ++d) {
-        v[d] = expf(v[d] - mx);
-        se += v[d];
-    }
+    for (int d = 0; d < D; ++d) se += expf(-(c[d * plane] / nrm) * 100.f - mx);
     // top 7 of the probabilities, descending: insertion into a register list
     float top[kTopK];
 #pragma unroll
     for (int k = 0; k < kTopK; ++k) top[k] = -INFINITY;
     for (int d = 0; d < D; ++d) {
-        float x = v[d] / se;
+        float x = expf(-(c[d * plane] / nrm) * 100.f - mx) / se;
 #pragma unroll
         for (int k = 0; k < kTopK; ++k) {
             const float hi = fmaxf(top[k], x), lo = fminf(top[k], x);
@@ -184,7 +178,7 @@ int launch_conf(const esm_conf_desc* d, hipStream_t s) {
     const long long px = static_cast<long long>(a.B) * a.H * a.W;
     switch (a.op) {
         case ESM_CONF_COST_FEATURES:
-            if (a.D < kTopK || a.D > kMaxD) return arg_error("conf: cost features need 7 <= D <= 64");
+            if (a.D < kTopK) return arg_error("conf: cost features need D >= 7 (torch.topk(7))");
             hipLaunchKernelGGL(cost_features_kernel, dim3(ceil_div(px, kThreads)), dim3(kThreads), 0, s, a.x[0], a.out,
                                a.B, a.D, a.H, a.W);
             break;

@@ -208,23 +208,43 @@ class Ctx:
         except Exception:
             pass
 
-    ARENA_CHUNK = 256 << 20  # bytes: one chunk holds every buffer of an S / M plan at KITTI size
+    ARENA_CHUNK = 256 << 20  # bytes: the largest arena chunk (every buffer of an S / M plan at KITTI size)
+    ARENA_FIRST = 16 << 20   # the first chunk; each further chunk doubles, up to ARENA_CHUNK
 
     def empty(self, *shape: int) -> torch.Tensor:
-        """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of large arena chunks, so
-        the buffers of one launch list sit close together: kernels that address several sources through
-        one buffer descriptor (the wide form over a channel concat) need them inside one window."""
+        """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of arena chunks, so the
+        buffers of one launch list sit close together: kernels that address several sources through
+        one buffer descriptor (the wide form over a channel concat) need them inside one 1 GiB window
+        (``_check_window``).  Chunks start at 16 MiB and double, so small plans stay small."""
         if not self.plan:
             return torch.empty(shape, device=self.device, dtype=torch.float32)
         n = math.prod(shape)
         nb = (4 * n + 255) // 256 * 256
         if self._arena is None or self._arena_off + nb > self._arena.numel():
-            self._arena = torch.empty(max(self.ARENA_CHUNK, nb), device=self.device, dtype=torch.uint8)
+            size = self.ARENA_FIRST if self._arena is None else min(self.ARENA_CHUNK, 2 * self._arena.numel())
+            self._arena = torch.empty(max(size, nb), device=self.device, dtype=torch.uint8)
             self._arena_off = 0
             self.keep.append(self._arena)
         t = self._arena[self._arena_off:self._arena_off + 4 * n].view(torch.float32).view(shape)
         self._arena_off += nb
         return t
+
+    WINDOW = 1 << 30  # conv_direct.h kOOB: a concat's sources must span less than this
+    _window_warned = False
+
+    def check_window(self, srcs: Sequence[torch.Tensor], tag: str) -> None:
+        """Warn (once per process) when a channel concat's sources span >= 1 GiB: the register-weight
+        forms then cannot address them through one descriptor and the launch silently takes a slower
+        form (conv_direct.h source_window)."""
+        if len(srcs) < 2 or Ctx._window_warned:
+            return
+        lo = min(t.data_ptr() for t in srcs)
+        hi = max(t.data_ptr() + 4 * (1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()))) for t in srcs)
+        if hi - lo >= self.WINDOW:
+            Ctx._window_warned = True
+            import warnings
+            warnings.warn(f"{tag}: concat sources span {(hi - lo) >> 20} MiB (>= 1 GiB); the wide conv forms fall "
+                          "back to slower ones for this launch", RuntimeWarning, stacklevel=3)
 
     def hold(self, *objs) -> None:
         if self.plan:
@@ -488,6 +508,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.out2 = out2.data_ptr()
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
+    ctx.check_window(srcs, tag)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
     if not ROWS3_ENABLED and d.hint == 0 and nd == 3 and not pc.transposed and (pc.k, pc.stride, pc.pad) == (3, 1, 1) \
             and pc.cout <= 8 and pc.cin % 4 == 0 and 4 <= pc.cin <= 32 and len(srcs) == 1:

@@ -16,8 +16,16 @@ publishes it.  :class:`StereoNode` does the same work with the device doing all 
 * only the uint16 disparity comes back to the host.
 
 ``elapsed_ms`` is measured as the node measures it (``:357-376``): from the input copy to the end
-of inference.  Publishing (ROS topics) and the OpenCV visualisation window are outside this
-package; :meth:`StereoNode.run` yields the per-frame results to whatever publishes them.
+of inference.  The first frame also builds the hot path's launch plan and hipGraph, so
+:meth:`StereoNode.warmup` runs one frame untimed (:meth:`run` calls it first).  Publishing (ROS
+topics) and the OpenCV visualisation window are outside this package; :meth:`StereoNode.run` yields
+the per-frame results to whatever publishes them.
+
+Parity: the post-filter is bit-exact against ``oracle/io_oracle.py``, whose median restatement
+matches ``scipy.ndimage.median_filter(mode="nearest")``.  Parity with OpenCV itself is UNPINNED: cv2
+is not importable here and the reference holds no node outputs.  That ``cv::medianBlur`` on the
+cropped ROI replicates the ROI's own border (rather than reading the padded image around it) is an
+assumption of this restatement.
 """
 from __future__ import annotations
 
@@ -88,7 +96,15 @@ class StereoNode:
             s.synchronize()
         return self.host_u16.numpy().view(np.uint16).copy(), elapsed_ms
 
+    def warmup(self, left: np.ndarray, right: np.ndarray) -> None:
+        """One untimed frame: builds the plan / hipGraph so later frames' elapsed_ms is steady state."""
+        self.process(left, right)
+        self._warm = True
+
     def run(self, pairs: Iterable[Tuple[np.ndarray, np.ndarray]]) -> Iterator[Tuple[np.ndarray, float]]:
-        """The timer loop's body over a frame source (the node cycles its image list, :325-327)."""
+        """The timer loop's body over a frame source (the node cycles its image list, :325-327); the
+        first pair is also run once untimed (warmup) before its timed frame."""
         for left, right in pairs:
+            if not getattr(self, "_warm", False):
+                self.warmup(left, right)
             yield self.process(left, right)

@@ -258,7 +258,7 @@ int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
  * stages' dm<t> / spx_<t> pairs.) */
 int esm_conv_pair2_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
 /* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
- *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D <= 64) -> out [B,7,H,W]: the 7 largest of
+ *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D >= 7) -> out [B,7,H,W]: the 7 largest of
  *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
  *   ESM_CONF_ATTEND         x[0..2] = cost_x, disp_x, imag_x [B,C,H,W], x[3] = logits [B,3,H,W] ->
  *                           out [B,3C,H,W] = cat(x_k * softmax_k(logits)) (:679-689)
