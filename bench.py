@@ -521,8 +521,9 @@ def main() -> None:
                        for i, m in enumerate(meta)], f, indent=1)
         # the timed region's whole steps, and the launches after them (the dominant op's
         # back-to-back batch), for the position-based trace mapping of scripts/prof_ops.py / pmc_traffic.py
-        with open(args.kernel_table + ".meta.json", "w") as f:
-            json.dump({"timed_steps": args.steps, "trailing_dispatches": 3 + args.steps}, f)
+        has_stem = marg is not None and any(m["name"] == "group_stem" for m in meta)
+        with open(args.kernel_table + ".meta.json", "w") as f:  # dominant-op batch (+ group_stem's batch)
+            json.dump({"timed_steps": args.steps, "trailing_dispatches": 3 + args.steps + (23 if has_stem else 0)}, f)
 
     # the timed region: the plain plan (one hipGraph per step) + the per-step disparity all-gather
     gather = D.DisparityGather(hp.outputs[0]) if world > 1 and not args.no_gather else None

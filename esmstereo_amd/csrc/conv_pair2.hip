@@ -59,7 +59,18 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
     const int yi0 = ya0 * SA - a.ph, xi0 = xa0 * SA - a.pw;   // staged input origin
     const int cin = a.Cin;
 
-    // ---- stage: input window (zero outside the input and past Cin), weights, BN affines
+    // ---- stage: input window (zero outside the input and past Cin), weights, BN affines.  The sources'
+    //      pointers / strides are read once as wave-uniform values and selected per element in
+    //      registers (indexing a.src[] by a per-lane value would re-load them from the kernarg
+    //      segment for every element).
+    const int ns = a.nsrc;
+    const float* sp0 = a.src[0].ptr + b * a.src[0].sb;
+    const float* sp1 = ns > 1 ? a.src[1].ptr + b * a.src[1].sb : sp0;
+    const float* sp2 = ns > 2 ? a.src[2].ptr + b * a.src[2].sb : sp0;
+    const int c0 = a.src[0].C, c01 = c0 + (ns > 1 ? a.src[1].C : 0);
+    const int sc0 = static_cast<int>(a.src[0].sc), sh0 = static_cast<int>(a.src[0].sh);
+    const int sc1 = ns > 1 ? static_cast<int>(a.src[1].sc) : sc0, sh1 = ns > 1 ? static_cast<int>(a.src[1].sh) : sh0;
+    const int sc2 = ns > 2 ? static_cast<int>(a.src[2].sc) : sc0, sh2 = ns > 2 ? static_cast<int>(a.src[2].sh) : sh0;
     constexpr int NIN = CINMAX * IR * IC;
     constexpr int PI = (NIN + kP2Threads - 1) / kP2Threads;
     float vi[PI];
@@ -68,13 +79,12 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         const int e = i * kP2Threads + tid;
         const int q = e % IC, r = (e / IC) % IR, c = e / (IC * IR);
         const int yi = yi0 + r, xi = xi0 + q;
-        int s = 0, cl = c;
-        if (a.nsrc > 1 && cl >= a.src[0].C) { cl -= a.src[0].C; s = 1; }
-        if (a.nsrc > 2 && s == 1 && cl >= a.src[1].C) { cl -= a.src[1].C; s = 2; }
-        const esm_src& sr = a.src[s];
+        const bool s1 = c >= c0, s2 = c >= c01;
+        const float* base = s2 ? sp2 : (s1 ? sp1 : sp0);
+        const int cl = c - (s2 ? c01 : (s1 ? c0 : 0));
+        const int scs = s2 ? sc2 : (s1 ? sc1 : sc0), shs = s2 ? sh2 : (s1 ? sh1 : sh0);
         const bool ok = e < NIN && c < cin && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-        const float* p = sr.ptr + b * sr.sb + (ok ? cl * sr.sc + yi * sr.sh + xi : 0);
-        const float v = *p;
+        const float v = base[ok ? cl * scs + yi * shs + xi : 0];
         vi[i] = ok ? v : 0.f;
     }
     constexpr int NWA = TA * CINMAX * 16;
@@ -100,11 +110,11 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         vwb[i] = ok ? v : 0.f;
     }
     float vep = 0.f;
-    if (tid < 64) {
+    if (tid < 64) {  // scaleA, shiftA, scaleB, shiftB: wave-uniform pointers, selected per lane
         const int k = tid >> 4, c = tid & 15;
-        const esm_conv_desc& d = k < 2 ? a : bd;
-        const float* p = (k & 1) ? d.shift : d.scale;
-        const bool ok = p != nullptr && c < d.Cout;
+        const float* p = k == 0 ? a.scale : (k == 1 ? a.shift : (k == 2 ? bd.scale : bd.shift));
+        const int cn = k < 2 ? a.Cout : bd.Cout;
+        const bool ok = p != nullptr && c < cn;
         const float v = (ok ? p : a.w)[ok ? c : 0];
         vep = ok ? v : ((k & 1) ? 0.f : 1.f);
     }

@@ -8,7 +8,7 @@ tag=${1:-sk}
 shift || true
 OUT=gpurun_out/pmcsq_$tag
 rm -rf $OUT && mkdir -p $OUT
-BENCH=(bench.py --steps 10 --warmup 3 --no-extra --no-cpu-baseline --kernel-table $OUT/ops.json "$@")
+BENCH=(bench.py --steps 10 --warmup 3 --no-extra --no-cpu-baseline --no-marginal --kernel-table $OUT/ops.json "$@")
 pass() {
   local n=$1; shift
   timeout -s KILL 300 rocprofv3 --pmc "$@" -d "$PWD/$OUT/p$n" -o p$n --output-format csv -- \

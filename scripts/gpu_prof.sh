@@ -8,7 +8,7 @@ tag=${1:-run}
 shift || true
 mkdir -p gpurun_out
 rm -rf "gpurun_out/prof_$tag" "gpurun_out/pmcf_$tag" "gpurun_out/pmcw_$tag"
-BENCH=(bench.py --steps 20 --warmup 5 --no-extra --no-cpu-baseline "$@")
+BENCH=(bench.py --steps 20 --warmup 5 --no-extra --no-cpu-baseline --no-marginal "$@")
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_$tag" -o "$tag" -- \
     python3 "${BENCH[@]}" --kernel-table "gpurun_out/ops_$tag.json" > "gpurun_out/prof_bench_$tag.log" 2>&1
 rc=$?
