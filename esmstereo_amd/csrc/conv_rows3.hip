@@ -108,8 +108,10 @@ __global__ void __launch_bounds__(64 * R * KSW) rconv3_kernel(const esm_conv_des
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const int dz = p - hi;                       // this lane's tap plane
-        const bool wok = dz >= 0 && dz <= 2;
-        const float* wp = wb + (wok ? dz : 0) * WDZ;
+        // an out-of-range tap plane multiplies a clamped (valid) weight by 0: an unconditional LDS read,
+        // so the reads are not split by exec-mask branches and can run ahead of the MFMAs
+        const float wm = (dz >= 0 && dz <= 2) ? 1.f : 0.f;
+        const float* wp = wb + (dz < 0 ? 0 : (dz > 2 ? 2 : dz)) * WDZ;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int dy = t / 3, dx = t % 3;
@@ -117,7 +119,7 @@ __global__ void __launch_bounds__(64 * R * KSW) rconv3_kernel(const esm_conv_des
             for (int gi = 0; gi < NG; ++gi) {
                 const int g = kpart + gi * KSW;
                 if (g >= KC) break;
-                const float av = wok ? wp[(t * CIN + 4 * g) * 8] : 0.f;
+                const float av = wp[(t * CIN + 4 * g) * 8] * wm;
                 const float bv = xb[4 * g * CS + p * PLANE + dy * 18 + dx];
                 // two accumulation chains, alternating per MFMA (a single dependent chain stalls)
                 acc[(t * NG + gi) & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[(t * NG + gi) & 1], 0, 0, 0);
