@@ -140,17 +140,24 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         const float* ib = in + kq * ICS + i * SA * ICP + n * SA;
         const float* wp = wa + kq * 16 + n;
         const int kca = (cin + 3) >> 2;
-        // channel groups unrolled at compile time (a runtime loop of 1..9 MFMAs waited on its LDS reads
-        // every iteration); the groups past Cin are skipped by a wave-uniform test
+        // accumulator indices stay compile-time (a runtime index turns every MFMA into a select chain
+        // over the accumulators): two chains alternate by tap, or by channel group for 1x1 convA
+        if constexpr (TA > 1) {
+            for (int kc = 0; kc < kca; ++kc) {
 #pragma unroll
-        for (int kc = 0; kc < CINMAX / 4; ++kc) {
-            if (kc >= kca) break;
-#pragma unroll
-            for (int t = 0; t < TA; ++t) {
-                const int ky = t / KA, kx = t % KA;
-                const float bv = ib[4 * kc * ICS + ky * ICP + kx];
-                const float av = wp[(t * CINMAX + 4 * kc) * 16];
-                acc[(kc * TA + t) & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[(kc * TA + t) & 1], 0, 0, 0);
+                for (int t = 0; t < TA; ++t) {
+                    const int ky = t / KA, kx = t % KA;
+                    const float bv = ib[4 * kc * ICS + ky * ICP + kx];
+                    const float av = wp[(t * CINMAX + 4 * kc) * 16];
+                    acc[t & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t & 1], 0, 0, 0);
+                }
+            }
+        } else {
+            for (int kc = 0; kc < kca; kc += 2) {
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[4 * kc * 16], ib[4 * kc * ICS], acc[0], 0, 0, 0);
+                if (kc + 1 < kca)
+                    acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[4 * (kc + 1) * 16], ib[4 * (kc + 1) * ICS], acc[1],
+                                                                  0, 0, 0);
             }
         }
         const int ya = ya0 + i, xa = xa0 + n;
