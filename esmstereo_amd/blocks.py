@@ -269,7 +269,7 @@ class _ESMUpsampler(nn.Module):
             # hourglass's first conv fused behind it where the kernel has the shape
             ref = getattr(self, f"ref{tag}")
             c10 = None
-            if shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed()):
+            if shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed(), x):
                 c10 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(),
                                        tag=f"{me}.upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1.0")
                 x = None

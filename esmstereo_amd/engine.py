@@ -725,9 +725,14 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
 # tail(upsampling(x)) and the refinement's first conv in one launch (esm_shuffle_conv_f32);
 # ESM_SHUFFLE_CONV=0 runs them as two launches (A/B measurements)
 SHUFFLE_CONV_ENABLED = os.environ.get("ESM_SHUFFLE_CONV", "1") != "0"
+# largest low-resolution input (B * H * W) it is used on: measured faster than the two launches at S-K's 2x
+# stage (24x78 in: 8.4 vs 10.5 us) and slower at the 4x stage (96x312 in: 23.2 vs 20.8 us)
+SHUFFLE_CONV_MAX_PIX = int(os.environ.get("ESM_SHUFFLE_CONV_MAXPIX", "8192"))
 
 
-def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv) -> bool:
+def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[torch.Tensor] = None) -> bool:
+    if x is not None and int(x.shape[0]) * int(x.shape[2]) * int(x.shape[3]) > SHUFFLE_CONV_MAX_PIX:
+        return False
     return SHUFFLE_CONV_ENABLED and (p.nf, p.r, conv.cout) in ((8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)) and \
         conv.nd == 2 and not conv.transposed and (conv.k, conv.stride, conv.pad, conv.cin) == (3, 2, 1, 1) and \
         conv.act == ACT_GELU
@@ -743,7 +748,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     r = p.r
     if nf != p.nf:
         raise RuntimeError(f"shuffle_conv: input has {nf} channels, layer expects {p.nf}")
-    if not shuffle_conv_supported(p, conv):
+    if not shuffle_conv_supported(p, conv):  # (size policy is the caller's: blocks.py)
         raise ValueError("shuffle_conv: unsupported head / conv geometry")
     Ho2, Wo2 = (H * r + 1) // 2, (W * r + 1) // 2
     out = ctx.empty(B, conv.cout, Ho2, Wo2)
