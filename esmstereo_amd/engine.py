@@ -547,10 +547,27 @@ def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]
     return len(srcs) == 1 or all(int(t.shape[1]) % 4 == 0 for t in srcs)
 
 
-def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
-              tags: Tuple[str, str] = ("convA", "convB")) -> torch.Tensor:
-    """``pb(pa(cat(srcs)))`` (two BasicConvs, BN + GELU each) as one launch when supported, else two."""
+def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
+    """Where the hot path takes the fused pair.  Measured in the S-K chain (rocprofv3, round 3): the pair
+    wins where convA is light -- the dm stacks' 5x5 single-channel head (dm.0 + dm.1: 6.1 vs 9.1 us at
+    24x78, 10.6 vs 11.5 at 96x312), a 1x1 convB (dm.2 + dm.3: 6.5 vs 9.2, 7.6 vs 10.4), the 1x1 agg.0 of
+    the small refinement levels (7.6 vs 9.0, 8.7 vs 9.3) -- and loses where convA's recomputed halo is
+    heavy work for one workgroup (spx 48 / 40 -> 16 3x3: 13.7 vs 9.1, 32.9 vs 14.8; the 192x624 agg_1:
+    48.4 vs 20.5; the stride-2 conv pairs at 96x312 and up: 24.2 vs 13.7)."""
     if not pair2_supported(pa, pb, srcs):
+        return False
+    B = int(srcs[0].shape[0])
+    Ho = (int(srcs[0].shape[2]) + 2 * pa.pad - pa.k) // pa.stride + 1
+    Wo = (int(srcs[0].shape[3]) + 2 * pa.pad - pa.k) // pa.stride + 1
+    light = pa.cin * pa.k * pa.k
+    return pb.k == 1 or light <= 25 or (pa.k == 1 and B * Ho * Wo <= 8192)
+
+
+def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
+              tags: Tuple[str, str] = ("convA", "convB"), force: bool = False) -> torch.Tensor:
+    """``pb(pa(cat(srcs)))`` (two BasicConvs, BN + GELU each) as one launch where ``pair2_auto`` takes it
+    (``force``: wherever supported), else two launches."""
+    if not (pair2_supported(pa, pb, srcs) if force else pair2_auto(pa, pb, srcs)):
         return run_conv(ctx, pb, [run_conv(ctx, pa, srcs, tag=tags[0])], tag=tags[1])
     da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
     B = int(srcs[0].shape[0])
