@@ -34,7 +34,6 @@ struct R3Layout {
 template <int KC, int R, int KSW, int ACT, bool PLAIN>
 __global__ void __launch_bounds__(64 * R * KSW) rconv3_kernel(const esm_conv_desc a) {
     constexpr int CIN = 4 * KC;
-    constexpr int NT = 64 * R * KSW;
     constexpr int RR = R + 2;                 // staged rows
     constexpr int PLANE = RR * 18;            // words per staged (channel, plane)
     constexpr int CS0 = 4 * PLANE;            // words per staged channel (4 planes)
@@ -48,6 +47,7 @@ __global__ void __launch_bounds__(64 * R * KSW) rconv3_kernel(const esm_conv_des
 
     const int tid = static_cast<int>(threadIdx.x);
     const int lane = tid & 63;
+    (void)tid;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kpart = wave % KSW, r = wave / KSW;
     const int x0 = static_cast<int>(blockIdx.x) * 16;
@@ -56,52 +56,70 @@ __global__ void __launch_bounds__(64 * R * KSW) rconv3_kernel(const esm_conv_des
     const int b = static_cast<int>(blockIdx.z) / npair;
     const int z0 = (static_cast<int>(blockIdx.z) - b * npair) * 2;
 
-    // ---- stage the input window: channels x planes z0-1..z0+2 x rows y0-1..y0+R x columns x0-1..x0+16
+    // ---- stage the input window (channels x planes z0-1..z0+2 x rows y0-1..y0+R x columns x0-1..x0+16)
+    //      and the weights with the MFMA lane layout, so a load's address is a per-lane voffset fixed for
+    //      the kernel (channel k = lane / 16, column lane % 16) plus a wave-uniform soffset (channel group,
+    //      plane, row): scalar arithmetic per load instead of a per-element index decomposition.
+    constexpr int NW = R * KSW;
+    const int n = lane & 15, kq = lane >> 4;
     const esm_src& s0 = a.src[0];
     const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
         4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
-    constexpr int NIN = CIN * 4 * PLANE;
-    constexpr int PER = (NIN + NT - 1) / NT;
-    float v[PER];
+    const int xin_ = x0 + n;                                       // interior column
+    const int xh = n == 0 ? x0 - 1 : x0 + 16;                      // halo column (lanes n = 0, 1)
+    const unsigned vin = xin_ < a.Wi ? 4u * (kq * sc + xin_) : kOOB;
+    const unsigned vh = (n < 2 && xh >= 0 && xh < a.Wi) ? 4u * (kq * sc + xh) : kOOB;
+    constexpr int NU = KC * 4 * RR;                                // (channel group, plane, row) units
+    constexpr int NUW = (NU + NW - 1) / NW;
+    float vi[NUW], vhv[NUW];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int e = i * NT + tid;
-        const int col = e % 18, row = (e / 18) % RR, p = (e / PLANE) % 4, c = e / (4 * PLANE);
-        const int xi = x0 - 1 + col, yi = y0 - 1 + row, zi = z0 - 1 + p;
-        const bool ok = e < NIN && c < a.Cin && xi >= 0 && xi < a.Wi && yi >= 0 && yi < a.Hi && zi >= 0 && zi < a.Di;
-        v[i] = buf_load_s(rs, ok ? 4u * (c * sc + zi * sd + yi * sh + xi) : kOOB, 0);
+    for (int j = 0; j < NUW; ++j) {
+        const int u = wave + j * NW;                               // wave-uniform
+        const int cg = u / (4 * RR), p = (u / RR) % 4, row = u % RR;
+        const int zi = z0 - 1 + p, yi = y0 - 1 + row;
+        const bool ok = u < NU && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi;
+        const int so = ok ? 4 * (4 * cg * sc + zi * sd + yi * sh) : static_cast<int>(kOOB);
+        vi[j] = buf_load_s(rs, vin, so);
+        vhv[j] = buf_load_s(rs, vh, so);
     }
-    // ---- weights: packed w[tap][cin_pad][cout_pad], tap = (dz*3 + dy)*3 + dx -> wl[dz][(t*CIN + c)*8 + co]
-    constexpr int NWT = 27 * CIN * 8;
-    constexpr int PERW = (NWT + NT - 1) / NT;
-    float wv[PERW];
+    // weights: packed w[tap][cin_pad][cout_pad], tap = (dz*3 + dy)*3 + dx -> wl[dz][(t*CIN + c)*8 + co];
+    // a load covers 8 channels x 8 couts (lane = channel * 8 + cout)
+    constexpr int NG8 = (CIN + 7) / 8;
+    constexpr int NWU = 27 * NG8;
+    constexpr int NWW = (NWU + NW - 1) / NW;
+    const int wcl = lane >> 3, wco = lane & 7;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
+    float wv[NWW];
 #pragma unroll
-    for (int i = 0; i < PERW; ++i) {
-        const int e = i * NT + tid;
-        const int co = e & 7, c = (e >> 3) % CIN, tap = e / (8 * CIN);
-        wv[i] = (e < NWT && co < a.Cout && c < a.Cin)
-                    ? a.w[(static_cast<long long>(tap) * a.cin_pad + c) * a.cout_pad + co]
-                    : 0.f;
+    for (int j = 0; j < NWW; ++j) {
+        const int u = wave + j * NW;
+        const int tap = u / NG8, g8 = u % NG8;
+        const bool ok = u < NWU && g8 * 8 + wcl < a.Cin && wco < a.Cout;
+        wv[j] = buf_load_s(wrs, ok ? 4u * (wcl * a.cout_pad + wco) : kOOB, 4 * (tap * a.cin_pad + g8 * 8) * a.cout_pad);
     }
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int e = i * NT + tid;
-        if (e < NIN) xin[(e / (4 * PLANE)) * CS + e % (4 * PLANE)] = v[i];
-    }
-#pragma unroll
-    for (int i = 0; i < PERW; ++i) {
-        const int e = i * NT + tid;
-        if (e < NWT) {
-            const int tap = e / (8 * CIN);
-            wl[(tap / 9) * WDZ + (tap % 9) * CIN * 8 + (e % (8 * CIN))] = wv[i];
+    for (int j = 0; j < NUW; ++j) {
+        const int u = wave + j * NW;
+        if (u < NU) {
+            const int cg = u / (4 * RR), pr = u % (4 * RR);  // pr = p * RR + row
+            float* dst = xin + (4 * cg + kq) * CS + pr * 18;
+            dst[n + 1] = vi[j];
+            if (n < 2) dst[n == 0 ? 0 : 17] = vhv[j];
         }
+    }
+#pragma unroll
+    for (int j = 0; j < NWW; ++j) {
+        const int u = wave + j * NW;
+        const int tap = u / NG8, g8 = u % NG8;
+        if (u < NWU && g8 * 8 + wcl < CIN) wl[(tap / 9) * WDZ + ((tap % 9) * CIN + g8 * 8 + wcl) * 8 + wco] = wv[j];
     }
     __syncthreads();
 
     // ---- MFMAs: this wave's output row y0 + r, channel groups kpart, kpart + KSW, ...
-    const int n = lane & 15, kq = lane >> 4, co = lane & 7, hi = (lane >> 3) & 1;
+    const int co = lane & 7, hi = (lane >> 3) & 1;
     floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
     const float* xb = xin + kq * CS + r * 18 + n;
     const float* wb = wl + kq * 8 + co;

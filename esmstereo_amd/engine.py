@@ -553,14 +553,15 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     24x78, 10.6 vs 11.5 at 96x312), a 1x1 convB (dm.2 + dm.3: 6.5 vs 9.2, 7.6 vs 10.4), the 1x1 agg.0 of
     the small refinement levels (7.6 vs 9.0, 8.7 vs 9.3) -- and loses where convA's recomputed halo is
     heavy work for one workgroup (spx 48 / 40 -> 16 3x3: 13.7 vs 9.1, 32.9 vs 14.8; the 192x624 agg_1:
-    48.4 vs 20.5; the stride-2 conv pairs at 96x312 and up: 24.2 vs 13.7)."""
+    48.4 vs 20.5; the stride-2 conv pairs at 96x312 and up: 24.2 vs 13.7; the refinement's 1 -> 16
+    stride-2 head + conv1.1 at 192x624: 23.6 vs 19.0)."""
     if not pair2_supported(pa, pb, srcs):
         return False
     B = int(srcs[0].shape[0])
     Ho = (int(srcs[0].shape[2]) + 2 * pa.pad - pa.k) // pa.stride + 1
     Wo = (int(srcs[0].shape[3]) + 2 * pa.pad - pa.k) // pa.stride + 1
     light = pa.cin * pa.k * pa.k
-    return pb.k == 1 or light <= 25 or (pa.k == 1 and B * Ho * Wo <= 8192)
+    return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 
 def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
