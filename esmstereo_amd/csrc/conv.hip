@@ -20,8 +20,6 @@ int launch_wide(const esm_conv_desc& a, hipStream_t s);  // conv_wide.hip
 bool wide3_ok(const esm_conv_desc& a);                    // conv_wide3.hip
 int launch_wide3(const esm_conv_desc& a, hipStream_t s);  // conv_wide3.hip
 bool widet_ok(const esm_conv_desc& a);                    // conv_widet.hip
-bool rows3_ok(const esm_conv_desc& a);                    // conv_rows3.hip
-int launch_rows3(const esm_conv_desc& a, hipStream_t s);  // conv_rows3.hip
 int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
 }  // namespace conv
 
@@ -32,7 +30,6 @@ constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound la
 constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
 constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
 constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 form, all 4 classes per wave (conv_widet.hip)
-constexpr int kHintRows3 = 1 << 30;    // row-block LDS-staged 3x3x3 form, <= 8 couts (conv_rows3.hip)
 
 int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("conv: null descriptor");
@@ -84,10 +81,6 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return launch_conv(&d, s);
     }
     if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
-    if (a.hint & kHintRows3) return conv::launch_rows3(a, s);
-    // 3x3x3 stride-1 stems with <= 8 couts (group_stem, agg): the row-block form stages each input
-    // window once per R rows (conv_rows3.hip)
-    if (a.hint == 0 && conv::rows3_ok(a)) return conv::launch_rows3(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

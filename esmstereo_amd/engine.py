@@ -370,11 +370,6 @@ if os.path.exists(_TUNED_PATH) and not os.environ.get("ESM_NO_TUNED"):
         TUNED_HINTS = {k: int(v) for k, v in json.load(_f).get("hints", {}).items()}
 
 
-# The row-block LDS-staged form is the automatic choice for 3x3x3 stems with <= 8 couts; ESM_ROWS3=0 runs
-# the plane-streaming form instead (A/B measurements)
-ROWS3_ENABLED = os.environ.get("ESM_ROWS3", "1") != "0"
-
-
 def conv_key(d: EsmConvDesc, nd: int) -> str:
     """Shape key of a conv launch: geometry, source channel split, batch, input extent and the
     epilogue features that change the store path."""
@@ -510,9 +505,6 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     key = conv_key(d, nd)
     ctx.check_window(srcs, tag)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
-    if not ROWS3_ENABLED and d.hint == 0 and nd == 3 and not pc.transposed and (pc.k, pc.stride, pc.pad) == (3, 1, 1) \
-            and pc.cout <= 8 and pc.cin % 4 == 0 and 4 <= pc.cin <= 32 and len(srcs) == 1:
-        d.hint = 1 << 24  # the plane-streaming form instead of the row-block form (A/B measurements)
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd
     if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap

@@ -128,9 +128,7 @@ typedef struct {
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
                      sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
                      split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
-                     8 waves per workgroup splitting K (layers with more than 4 channel groups).
-                     ROWS3 << 30: row-block LDS-staged form for 3x3x3 s1 p1 3-D convs with <= 8 couts over
-                     4..32 input channels (conv_rows3.hip; the automatic choice for those layers). */
+                     8 waves per workgroup splitting K (layers with more than 4 channel groups). */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;

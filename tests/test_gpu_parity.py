@@ -402,32 +402,6 @@ def test_conv_small_form_epilogues():
         run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), [x.to(DEV)], mul=att.to(DEV), hint=HINT_SMALL)
 
 
-HINT_ROWS3 = 1 << 30
-
-
-@pytest.mark.parametrize("B,cin,cout,shape", [(1, 32, 8, (12, 24, 78)), (2, 32, 8, (5, 7, 21)), (1, 8, 8, (12, 24, 78)),
-                                              (1, 8, 8, (3, 5, 17)), (2, 4, 8, (4, 9, 33)), (1, 12, 6, (6, 11, 40)),
-                                              (1, 24, 8, (7, 3, 16)), (1, 32, 8, (48, 20, 50)),
-                                              (1, 20, 8, (2, 2, 2))])
-def test_conv_rows3_form(B, cin, cout, shape):
-    """Row-block LDS-staged 3x3x3 form (conv_rows3.hip: group_stem / agg shapes, odd plane counts, ragged rows
-    and strips, both row-block geometries), forced and automatic, plain and general epilogues, vs fp64 torch
-    (1e-5 relative)."""
-    conv, bn = _mk(3, cin, cout, 3, 1, 1, seed=14)
-    x = torch.randn(B, cin, *shape)
-    ref = _ref_conv([x], conv, bn, ACT_GELU)
-    p = pk(conv, bn, ACT_GELU)
-    for h in (HINT_ROWS3, 0):
-        assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
-    res = torch.randn_like(ref)
-    att = torch.rand(B, cout, *shape[1:]) + 0.5
-    out2 = torch.empty(ref.shape, device=DEV)
-    y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), mul=att.to(DEV), post_scale=2.0, out2=out2,
-                 post_scale2=0.5, hint=HINT_ROWS3)
-    want = (ref * att.unsqueeze(2) + res) * 2.0
-    assert rel(y, want) < 1e-5 and rel(out2, want / 4) < 1e-5
-
-
 HINT_STEM, HINT_NO_STEM = 1 << 17, 1 << 18
 STEM_CASES = [(3, 32, 8, (6, 9, 21)), (3, 1, 8, (5, 7, 30)), (3, 8, 8, (7, 5, 29)), (3, 12, 12, (4, 6, 15)),
               (3, 32, 8, (2, 3, 10)), (3, 3, 8, (9, 4, 44)), (2, 16, 8, (23, 37)), (2, 8, 12, (17, 50)),
