@@ -237,21 +237,17 @@ constexpr int kFTW = 16;
 // 512 threads: the t1 region is one pass (448 / 480 pixels), the t2 region one pass, the depthwise
 // phases half the iterations of a 256-thread workgroup
 constexpr int kFThreads = 512;
-#ifndef ESM_FMBLOCK_TH
-#define ESM_FMBLOCK_TH 1
-#endif
-#ifndef ESM_FMBLOCK_TW
-#define ESM_FMBLOCK_TW 16
-#endif
-// output tile of the whole-FMBlock form: 1 x 16 measured 1.2 us faster per S-K step than 2 x 16 (twice
-// the workgroups, the t1 region 450 instead of 480 pixels)
-constexpr int kFConvTH = ESM_FMBLOCK_TH;
-constexpr int kFConvTW = ESM_FMBLOCK_TW;
+// output tile of the whole-FMBlock form: 16 wide, 1 or 3 rows.  1 x 16 measured 1.2 us faster per S-K
+// step than 2 x 16 (twice the workgroups on a map that fills a quarter of the chip); on maps with
+// enough tiles to fill the chip the recompute of the halo dominates (the t1 region of a 1 x 16 tile is
+// 450 pixels, 28x the tile; of a 3 x 16 tile 510 pixels, 10.6x), so those take 3 rows
+constexpr int kFConvTW = 16;
+constexpr int kFConvTallMinTiles = 512;  // 3-row tiles at or above this many (2 per CU)
 
 // CONV: FMBlock.conv fused behind net (shufflemixer.py:124-131): out = conv2(silu(conv0(t3) + b0)) + b2
 // + t3, t3 = net(x) + x.  conv0 is 3x3 zero-padded, so t3 is computed on the tile plus a 1-pixel ring
-// (zero outside the image) and kept in LDS; the tile is kFConvTH x kFConvTW (1 x 16: the t1 region
-// (1 + 2 + 12) x (16 + 2 + 12) = 450 pixels is one pass).  HID = conv0's output channels (dim + 16).
+// (zero outside the image) and kept in LDS; the tile is CTH x kFConvTW (the t1 region
+// (CTH + 2 + 12) x (16 + 2 + 12) <= 512 pixels is one pass).  HID = conv0's output channels (dim + 16).
 // Depthwise K x K (+ bias) of an OH x OW region, reading the [C][SH][SWP] LDS image `src` (row r
 // of the region reads source rows r .. r + K - 1), into dst [C][OH * OW].  A wave owns a channel
 // (wave-uniform: its K*K weights and bias are scalar loads from global memory) and a lane owns SEG
@@ -290,10 +286,10 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
     }
 }
 
-template <int C, int K, bool CONV, int HID>
+template <int C, int K, bool CONV, int HID, int CTH = 1>
 __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
     constexpr int R = K / 2;
-    constexpr int TH = CONV ? kFConvTH : 4, TW = CONV ? kFConvTW : kFTW;                        // output tile
+    constexpr int TH = CONV ? CTH : 4, TW = CONV ? kFConvTW : kFTW;                        // output tile
     constexpr int HC = CONV ? 1 : 0;                                    // t3 ring for conv0
     constexpr int CH = TH + 2 * HC, CW = TW + 2 * HC, CP = CH * CW;    // t3 region
     constexpr int BH = CH + 2 * R, BW = CW + 2 * R, BP = BH * BW;      // t2 region
@@ -522,12 +518,16 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
     const bool conv = a.conv0_w != nullptr;
     if (conv && (!a.conv0_b || !a.conv2_w || !a.conv2_b || a.hid != a.C + 16))
         return arg_error("fmnet: the fused FMBlock.conv needs conv0/conv2 weights and biases, hid = C + 16");
-    const dim3 grid(ceil_div(a.W, conv ? kFConvTW : kFTW), ceil_div(a.H, conv ? kFConvTH : 4), a.B);
+    const bool tall = conv && static_cast<long long>(ceil_div(a.W, kFConvTW)) * ceil_div(a.H, 3) * a.B >= kFConvTallMinTiles;
+    const int th = conv ? (tall ? 3 : 1) : 4;
+    const dim3 grid(ceil_div(a.W, conv ? kFConvTW : kFTW), ceil_div(a.H, th), a.B);
     if (a.C == 8) {
-        if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24>), grid, dim3(kFThreads), 0, s, a);
+        if (tall) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24, 3>), grid, dim3(kFThreads), 0, s, a);
+        else if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24>), grid, dim3(kFThreads), 0, s, a);
         else hipLaunchKernelGGL((fmnet_kernel<8, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
     } else if (a.C == 16) {
-        if (conv) hipLaunchKernelGGL((fmnet_kernel<16, 7, true, 32>), grid, dim3(kFThreads), 0, s, a);
+        if (tall) hipLaunchKernelGGL((fmnet_kernel<16, 7, true, 32, 3>), grid, dim3(kFThreads), 0, s, a);
+        else if (conv) hipLaunchKernelGGL((fmnet_kernel<16, 7, true, 32>), grid, dim3(kFThreads), 0, s, a);
         else hipLaunchKernelGGL((fmnet_kernel<16, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
     } else {
         set_error("fmnet: C must be 8 or 16");

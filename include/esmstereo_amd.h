@@ -312,7 +312,7 @@ int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V
                         int D);
 int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float* V, float* work, int B, int C,
                           int H, int W, int D);
-/* kind 0 = disparity_regression, 1 = regression_topk k=2 */
+/* kind 0 = disparity_regression, 1 = regression_topk k=2, 2 + k = regression_topk with that k */
 int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* out, int B, int D, int H, int W);
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);

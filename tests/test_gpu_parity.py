@@ -894,11 +894,12 @@ def test_expected_raises():
                 model(left, left, False)
 
 
-@pytest.mark.parametrize("C,H,W", [(8, 24, 78), (8, 7, 13), (16, 96, 312), (16, 5, 40), (8, 1, 1)])
+@pytest.mark.parametrize("C,H,W", [(8, 24, 78), (8, 7, 13), (16, 96, 312), (16, 5, 40), (8, 1, 1), (8, 200, 100)])
 def test_fmnet_fused_bitwise(C, H, W):
     """FMBlock.net + x in one launch (esm_fmnet_f32, halo recomputation) vs the three smix launches:
     the same per-pixel operations in the same order, up to the compiler's FMA contraction choices in
-    the two kernels (relative 1e-6)."""
+    the two kernels (relative 1e-6).  96x312 and 200x100 (ragged in 3) take the 3-row tile of the whole
+    block, the others the 1-row tile."""
     from esmstereo_amd.engine import run_fmnet, run_smix
 
     torch.manual_seed(C * 100 + H)
