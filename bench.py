@@ -565,7 +565,9 @@ def main() -> None:
                     "tests/helpers.py fullsize_inputs; seeded random-init weights, tests/helpers.py seeded_state)",
             "config": {"workload": "hot path: cost volume -> 3D stems -> 3D hourglass -> regression -> "
                                    "ESM upsampler (models/ESMStereo.py:700-745), " + workload,
-                       "baseline_config": f"configs[{args.config}]: {cfg['name']}",
+                       "baseline_config": (f"configs[{args.config}]: {cfg['name']}" if all(
+                           getattr(args, k) == cfg[k] for k in ("variant", "cv", "height", "width", "maxdisp"))
+                           else f"none (configs[{args.config}] overridden on the command line)"),
                        "variant": args.variant, "cv": args.cv, "global_batch": total_batch,
                        "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                        "parallelism": f"dp{world}", "graph": hp.graph,

@@ -71,7 +71,7 @@ class EsmShuffleTailDesc(Structure):
                 ("up_w", c_void_p), ("up_b", c_void_p), ("tail_w", c_void_p), ("tail_b", c_void_p),
                 ("out", c_void_p), ("ob", c_int64), ("oh", c_int64),
                 ("B", c_int32), ("nf", c_int32), ("H", c_int32), ("W", c_int32), ("r", c_int32),
-                ("reserved", c_int32)]
+                ("flags", c_int32)]
 
 
 class EsmShuffleConvDesc(Structure):

@@ -70,15 +70,30 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-// Workgroup coordinates in the hardware's dispatch order.  An XCD-slab remap of this order
-// (neighbouring tiles on one XCD so halo rows stay in its L2) cut memory-side bytes to 1.0-2.1x the
-// algorithmic but made the S-K step 13 us and L-K 27 us slower on these latency-bound forms
-// (round 2); halo reuse now happens inside a workgroup instead.
 struct Blk3 {
     int x, y, z;
 };
-__device__ __forceinline__ Blk3 xcd_block() {
-    return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
+// Workgroup coordinates.  The dispatcher deals workgroups (x fastest, then y, z) round-robin over the
+// 8 XCDs, so neighbouring tiles, which read each other's halo rows, sit in different XCDs' L2s and
+// each fetches the shared lines from memory again.  With `slab` (a per-launch flag: conv hint bit 30,
+// esm_shuffle_tail_desc.flags bit 0) the order is remapped bijectively so that XCD k runs a contiguous
+// range of logical tiles (a slab of rows) and the halo stays in its own L2.  Measured (round 3, S-K):
+// memory-side bytes of the full-resolution launches fall from 2.1-2.9x the algorithmic to 1.05-1.13x
+// at no cost in their time, while on the small maps of the hourglasses the slab order costs
+// 0.1-1 us per launch (+10 us on the step with every launch remapped), so the host sets the flag for
+// 2-D maps of >= 64k output pixels only (engine.XCD_SLAB_MIN_PIX).
+constexpr int kHintXcd = 1 << 30;
+__device__ __forceinline__ Blk3 xcd_block(bool slab) {
+    if (!slab) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
+    const unsigned gx = gridDim.x, gy = gridDim.y;
+    const unsigned nwg = gx * gy * gridDim.z;
+    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    unsigned wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    const int x = static_cast<int>(wg % gx);
+    wg /= gx;
+    const int y = static_cast<int>(wg % gy);
+    return {x, y, static_cast<int>(wg / gy)};
 }
 
 // SiLU as nn.SiLU: x / (1 + exp(-x))

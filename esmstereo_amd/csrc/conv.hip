@@ -56,13 +56,14 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (a.shuffle > 1 && (d3 || a.transposed)) return arg_error("conv: pixel shuffle only for 2-D convs");
     if (a.up && (a.Cout != 1 || d3 || a.up_f <= 0)) return arg_error("conv: bilinear add needs 2-D, Cout == 1");
     if (a.Hi <= 0 || a.Wi <= 0 || a.Di <= 0) return arg_error("conv: empty input");
+    const int form = a.hint & ~kHintXcd;  // the form / tile bits (bit 30 only orders the tiles)
     if (a.transposed) {
         if (a.kh != 4 || a.stride != 2 || a.ph != 1 || a.pw != 1 || (d3 && a.pd != 1))
             return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
         if (a.Ho != 2 * a.Hi || a.Wo != 2 * a.Wi || (d3 && a.Do != 2 * a.Di))
             return arg_error("conv: transposed output extent must be 2x the input");
         if (a.hint & kHintWideT) return conv::launch_widet(a, s);
-        if ((a.hint & kHintSmall) || (a.hint == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
+        if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
     }
     const int S = a.stride;
@@ -77,7 +78,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         // a launch list's arena): the automatic rules instead
         if (conv::wide_ok(a)) return conv::launch_wide(a, s);
         esm_conv_desc d = a;
-        d.hint = 0;
+        d.hint &= kHintXcd;
         return launch_conv(&d, s);
     }
     if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
@@ -86,7 +87,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).
     // Measured (scripts/probes/c1in_sweep.py, profiles/r01_c1in_sweep.txt): 1->16 k3s2 at 192x624
     // output 8.6 us; on small maps the MFMA direct form wins (4.8 vs 11.6 us at 24x78)
-    if (a.hint == 0 && conv::c1in_ok(a) && static_cast<long long>(a.B) * a.Ho * a.Wo >= 65536)
+    if (form == 0 && conv::c1in_ok(a) && static_cast<long long>(a.B) * a.Ho * a.Wo >= 65536)
         return conv::launch_c1in(a, s);
     if (a.hint & kHintNoStem) {
         esm_conv_desc d = a;
@@ -94,9 +95,9 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return d3 ? launch_conv3d(d, s) : launch_conv2d(d, s);
     }
     // 8 / 12 / 24 output channels, 3x3(x3) stride 1: the 16-block MFMA form wastes no tile rows
-    if (a.hint == 0 && conv::stem_auto(a)) return conv::launch_stem(a, s);
+    if (form == 0 && conv::stem_auto(a)) return conv::launch_stem(a, s);
     // latency-bound layers (most of the hot path): the lean K-split form (conv_small.hip)
-    if (a.hint == 0 && conv::small_auto(a)) return conv::launch_small(a, s);
+    if (form == 0 && conv::small_auto(a)) return conv::launch_small(a, s);
     return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
 }
 

@@ -48,9 +48,10 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
 
     const int tid = threadIdx.x;
     const int Ho = a.Ho, Wo = a.Wo, Do = D3 ? a.Do : 1;
-    const int Y0 = blockIdx.y * kC1TH, X0 = blockIdx.x * TW;
-    const int b = blockIdx.z / Do;
-    const int oz = blockIdx.z - b * Do;
+    const Blk3 bk = xcd_block((a.hint & kHintXcd) != 0);
+    const int Y0 = bk.y * kC1TH, X0 = bk.x * TW;
+    const int b = bk.z / Do;
+    const int oz = bk.z - b * Do;
     const int qz = D3 ? (oz & 1) : 0;
     const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
@@ -182,9 +183,10 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
 
     const int tid = threadIdx.x;
     const int Ho = a.Ho, Wo = a.Wo, Do = D3 ? a.Do : 1;
-    const int Y0 = blockIdx.y * kC1TH, X0 = blockIdx.x * TW;
-    const int b = blockIdx.z / Do;
-    const int oz = blockIdx.z - b * Do;
+    const Blk3 bk = xcd_block((a.hint & kHintXcd) != 0);
+    const int Y0 = bk.y * kC1TH, X0 = bk.x * TW;
+    const int b = bk.z / Do;
+    const int oz = bk.z - b * Do;
     const int qz = D3 ? (oz & 1) : 0;
     const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0

@@ -362,7 +362,7 @@ int launch_geom(const esm_conv_desc& a, hipStream_t s) {
         }
         return arg_error("conv: c1-transposed hint not applicable");
     }
-    if (a.hint) {  // explicit tile (tuning sweeps, tests of every variant)
+    if (a.hint & ~kHintXcd) {  // explicit tile (tuning sweeps, tests of every variant)
         const int hnt = a.hint & 15, hks = (a.hint >> 4) & 15, hc1 = (a.hint >> 8) & 1, hdir = (a.hint >> 9) & 1;
         const int hrw = (a.hint >> 12) & 15;  // direct form: rows per wave (0 = automatic)
         if ((a.hint >> 10) & 1) {  // row-streaming form

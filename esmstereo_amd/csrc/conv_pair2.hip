@@ -52,8 +52,9 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n = lane & 15, kq = lane >> 4;
     constexpr int VB = 16 - KB + 1;
-    const int b = static_cast<int>(blockIdx.z);
-    const int yb0 = static_cast<int>(blockIdx.y) * TH, xb0 = static_cast<int>(blockIdx.x) * VB;
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
+    const int b = bk_.z;
+    const int yb0 = bk_.y * TH, xb0 = bk_.x * VB;
     const int pb = bd.ph;
     const int ya0 = yb0 - pb, xa0 = xb0 - pb;                 // convA tile origin
     const int yi0 = ya0 * SA - a.ph, xi0 = xa0 * SA - a.pw;   // staged input origin

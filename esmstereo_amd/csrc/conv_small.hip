@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, u
 
     const int Ws = TR ? a.Wi : a.Wo;
     const int Ds = D3 ? (TR ? a.Di : a.Do) : 1;
-    const Blk3 bk_ = xcd_block();
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
     const int x0 = bk_.x * 16;
     const int ys = bk_.y;
     const int zz = bk_.z;

@@ -36,8 +36,12 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 // KS: the 4 waves split the input-channel chunks of ONE 4-row tile (grids far below one
 // workgroup per CU) and add their partial sums in LDS in a fixed order.
-template <bool D3, int CG, int CK, bool KS>
-__global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
+// NW: waves per workgroup, 4 or 8 (3-D only: 8 consecutive planes share one staged weight slab, for
+// slabs so large that the LDS would otherwise hold two 4-wave workgroups per CU).
+template <bool D3, int CG, int CK, bool KS, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) sconv_kernel(const esm_conv_desc a) {
+    static_assert(NW == 4 || (NW == 8 && D3 && !KS), "8-wave workgroups: 3-D, no K split");
+    constexpr int NT = 64 * NW;
     constexpr int K = 3;
     constexpr int KDT = D3 ? 3 : 1;
     constexpr int TAPS = KDT * 9;
@@ -55,7 +59,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
     const int tiles_w = (Wo + VALID - 1) / VALID;
     // 3-D: a workgroup = 4 planes x 4 rows; 2-D: 16 rows (4 groups of 4)
     const int tiles_h = (D3 || KS) ? (Ho + 3) / 4 : (Ho + 15) / 16;
-    const int tiles_z = D3 ? (KS ? Do : (Do + 3) / 4) : 1;
+    const int tiles_z = D3 ? (KS ? Do : (Do + NW - 1) / NW) : 1;
     // XCD-aware order (conv_direct.h): each XCD takes a contiguous range of tiles
     const unsigned nwg = gridDim.x, orig = blockIdx.x;
     const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
@@ -67,7 +71,7 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
     const int tz = static_cast<int>(wg % tiles_z);
     const int b = static_cast<int>(wg / tiles_z);
     if (b >= a.B) return;  // whole workgroup, before any barrier: a grid larger than the tile count stays in bounds
-    const int oz = D3 ? (KS ? tz : tz * 4 + wave) : 0;
+    const int oz = D3 ? (KS ? tz : tz * NW + wave) : 0;
     const int oy = (D3 || KS) ? ty * 4 + r : ty * 16 + wave * 4 + r;  // this lane's output row
     const int o0 = tx * VALID;
     const int xi = o0 - 1 + n;  // input column held by this lane (pad 1)
@@ -108,11 +112,11 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
     const int cst = (a.Cin + CK - 1) / CK * CK;  // staged channels (whole chunks; past Cin: zeros)
     {
         const int total = cst * TAPS * 4 * CGP;
-        for (int e0 = 0; e0 < total; e0 += 256 * 8) {
+        for (int e0 = 0; e0 < total; e0 += NT * 8) {
             float v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * 256 + static_cast<int>(threadIdx.x);
+                const int e = e0 + u * NT + static_cast<int>(threadIdx.x);
                 const int g = e % CGP, i = (e / CGP) & 3, rest = e / (4 * CGP);
                 const int tap = rest % TAPS, ci = rest / TAPS;
                 const int co = 4 * g + i;
@@ -122,21 +126,11 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * 256 + static_cast<int>(threadIdx.x);
+                const int e = e0 + u * NT + static_cast<int>(threadIdx.x);
                 if (e < total) wl[e] = v[u];
             }
         }
     }
-    // BN scale / shift of this lane's couts (VGPR i of group g = cout 4g + i)
-    float scl[CG][4], shf[CG][4];
-#pragma unroll
-    for (int g = 0; g < CG; ++g)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int co = min(4 * g + i, a.Cout - 1);
-            scl[g][i] = a.scale ? a.scale[co] : 1.f;
-            shf[g][i] = a.shift ? a.shift[co] : 0.f;
-        }
     __syncthreads();
 
     // independent accumulation chains: a 4x4x1 MFMA issues every 8 cycles but its result is ready
@@ -235,7 +229,10 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
             if (co >= a.Cout) continue;
             const float s = sum[g][i];
             if (plain) {
-                const float v = a.scale ? s * scl[g][i] + shf[g][i] : s + shf[g][i];
+                // BN scale / shift loaded here, not before the K loop: 2 * CG * 4 registers less
+                // through the loop (wave-uniform: scalar loads)
+                const float shf = a.shift ? a.shift[co] : 0.f;
+                const float v = a.scale ? s * a.scale[co] + shf : s + shf;
                 a.out[rowb + co * a.oc] = apply_act(v, a.act) * a.post_scale;
             } else {
                 conv_put(a, conv_finish(a, s, b, co, oz, oy, ox), b, co, oz, oy, ox);
@@ -243,7 +240,13 @@ __global__ void __launch_bounds__(256) sconv_kernel(const esm_conv_desc a) {
         }
 }
 
-template <bool D3, int CG, bool KS>
+#ifdef ESM_STEM_NW4
+constexpr bool kStemNW8 = false;  // A/B builds
+#else
+constexpr bool kStemNW8 = true;
+#endif
+
+template <bool D3, int CG, bool KS, int NW = 4>
 int launch_sconv_ks(const esm_conv_desc& a, hipStream_t s, int ck, long long nwg) {
     constexpr int TAPS = D3 ? 27 : 9;
     constexpr int CGP = CG == 3 ? 4 : CG;
@@ -252,11 +255,11 @@ int launch_sconv_ks(const esm_conv_desc& a, hipStream_t s, int ck, long long nwg
     if (nwg > 0x7fffffffLL) return arg_error("conv: grid too large");
     const dim3 grid(static_cast<unsigned>(nwg));
     if (ck == 1)
-        hipLaunchKernelGGL((sconv_kernel<D3, CG, 1, KS>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((sconv_kernel<D3, CG, 1, KS, NW>), grid, dim3(64 * NW), lds, s, a);
     else if (ck == 2)
-        hipLaunchKernelGGL((sconv_kernel<D3, CG, 2, KS>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((sconv_kernel<D3, CG, 2, KS, NW>), grid, dim3(64 * NW), lds, s, a);
     else
-        hipLaunchKernelGGL((sconv_kernel<D3, CG, 4, KS>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((sconv_kernel<D3, CG, 4, KS, NW>), grid, dim3(64 * NW), lds, s, a);
     return check_launch("conv(stem)");
 }
 
@@ -272,6 +275,14 @@ int launch_sconv(const esm_conv_desc& a, hipStream_t s) {
         return launch_sconv_ks<D3, CG, true>(a, s, ck_ks, nwg);
     }
     const int ck = a.Cin <= 1 ? 1 : (a.Cin <= 2 ? 2 : 4);  // the chunk size does not change the order
+    if constexpr (D3 && CG >= 6) {
+        // a weight slab over 40 KB leaves room for two 4-wave workgroups per CU (2 waves per SIMD):
+        // 8 planes per workgroup share it instead (4 waves per SIMD; 2-channel chunks keep the
+        // double-buffered operands within the 128 registers that allows)
+        const long long slab = static_cast<long long>((a.Cin + 1) / 2 * 2) * 27 * 4 * CG * 4;
+        const long long nwg8 = tiles_w * ((a.Ho + 3) / 4) * ((a.Do + 7) / 8) * a.B;
+        if (kStemNW8 && slab > 40 * 1024 && nwg8 >= 256) return launch_sconv_ks<D3, CG, false, 8>(a, s, 2, nwg8);
+    }
     return launch_sconv_ks<D3, CG, false>(a, s, ck, plain);
 }
 

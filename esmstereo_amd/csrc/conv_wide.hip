@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
     const int n16 = lane & 15, kq = lane >> 4;
     const int kh = KS == 2 ? (wave & 1) : 0;  // which half of the channel groups
     const int gb = kh * NGW;                  // first channel group of this wave
-    const Blk3 bk_ = xcd_block();
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
     const int x0 = (bk_.x * (4 / KS) + wave / KS) * 16;
     const int y0 = bk_.y * R;
     const int b = bk_.z;

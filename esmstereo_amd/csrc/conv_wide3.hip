@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
     const int kpart = wave % KSW, zpart = wave / KSW;
-    const Blk3 bk_ = xcd_block();
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
     const int x0 = bk_.x * 16;
     const int y = bk_.y;
     const int nzb = (a.Do + ZB - 1) / ZB;

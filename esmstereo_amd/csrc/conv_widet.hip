@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(kWtThreads) wtconv_kernel(const esm_conv_desc 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
-    const Blk3 bk_ = xcd_block();
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
     const int x0 = (bk_.x * 4 + wave) * 16;  // input-grid column of lane 0
     const int y0 = bk_.y * R;
     const int b = bk_.z;

@@ -329,8 +329,9 @@ int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint) {
         return esm::arg_error("plan: op is not a conv");
     const int prev = plan->ops[index].conv.hint;
     plan->clear_graph();
-    plan->ops[index].conv.hint = hint;
-    return prev;
+    // the tile-order bit (30) is the host's per-launch choice, not a form: kept across tuning hints
+    plan->ops[index].conv.hint = (hint & ~esm::kHintXcd) | (prev & esm::kHintXcd);
+    return prev & ~esm::kHintXcd;
 }
 
 int esm_plan_set_repeat(esm_plan* plan, int index, int repeat) {

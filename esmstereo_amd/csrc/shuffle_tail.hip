@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
 
     const int tid = threadIdx.x;
     const int H = a.H, W = a.W, HO = H * R, WO = W * R;
-    const Blk3 bk_ = xcd_block();
+    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
     const int b = bk_.z;
     const int Y0 = bk_.y * TH, X0 = bk_.x * kTW;
     const int ly0 = Y0 / R - 1, lx0 = X0 / R - 1;  // low-res pixel of lr[.][0][0]
@@ -166,41 +166,54 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
     }
     __syncthreads();
 
-    // ---- 3x3 tail: thread (row, column quad)
-    constexpr int QPR = kTW / 4;  // quads per row
+    // ---- 3x3 tail: thread (row, QW consecutive columns), QW chosen so the tile's items fill the
+    //      workgroup (16 x 32: 2 columns per thread on all 4 waves, not 4 on two of them)
+    constexpr int QW = TH * kTW >= 4 * kThreads ? 4 : (TH * kTW >= 2 * kThreads ? 2 : 1);
+    constexpr int QPR = kTW / QW;  // items per row
+    const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(a.out + b * a.ob, static_cast<short>(0),
+                                                                         0x7fffffff, 0x00020000);
     for (int q = tid; q < TH * QPR; q += kThreads) {
         const int r = q / QPR, g = q - (q / QPR) * QPR;
-        const int oy = Y0 + r, ox = X0 + 4 * g;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const int oy = Y0 + r, ox = X0 + QW * g;
+        float acc[QW];
+#pragma unroll
+        for (int j = 0; j < QW; ++j) acc[j] = 0.f;
 #pragma unroll 2
         for (int c = 0; c < NF; ++c) {
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky) {
-                float v[6];
+                float v[QW + 2];
 #pragma unroll
-                for (int j = 0; j < 6; ++j) v[j] = mid[c][r + ky][4 * g + j + MX0 - 1];
+                for (int j = 0; j < QW + 2; ++j) v[j] = mid[c][r + ky][QW * g + j + MX0 - 1];
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
                     const float w = tw[(c * 3 + ky) * 3 + kx];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                    for (int j = 0; j < QW; ++j) acc[j] += w * v[j + kx];
                 }
             }
         }
         if (oy >= HO) continue;
-        float* o = a.out + b * a.ob + static_cast<long long>(oy) * a.oh + ox;
-        if (ox + 3 < WO && ((reinterpret_cast<uintptr_t>(o)) & 15) == 0) {
-            // write-through (sc1) 16-B store (conv_direct.h kStoreAux)
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out + b * a.ob, static_cast<short>(0),
-                                                                                0x7fffffff, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{__float_as_uint(acc[0] + tb), __float_as_uint(acc[1] + tb), __float_as_uint(acc[2] + tb),
-                      __float_as_uint(acc[3] + tb)},
-                rs, static_cast<int>(4 * (static_cast<long long>(oy) * a.oh + ox)), 0, 16);
+        const int vo = static_cast<int>(4 * (static_cast<long long>(oy) * a.oh + ox));
+        if (ox + QW - 1 < WO && ((reinterpret_cast<uintptr_t>(a.out + b * a.ob) + vo) & (4 * QW - 1)) == 0) {
+            // write-through (sc1) vector store (conv_direct.h kStoreAux)
+            if constexpr (QW == 4) {
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{__float_as_uint(acc[0] + tb), __float_as_uint(acc[1] + tb), __float_as_uint(acc[2] + tb),
+                          __float_as_uint(acc[3] + tb)},
+                    rso, vo, 0, conv::kStoreAux);
+            } else if constexpr (QW == 2) {
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(acc[0] + tb), __float_as_uint(acc[1] + tb)},
+                                                      rso, vo, 0, conv::kStoreAux);
+            } else {
+                conv::store_b32(__float_as_uint(acc[0] + tb), rso, vo, 0);
+            }
         } else {
+            float* o = a.out + b * a.ob + static_cast<long long>(oy) * a.oh + ox;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < QW; ++j)
                 if (ox + j < WO) o[j] = acc[j] + tb;
         }
     }

@@ -362,6 +362,14 @@ class Ctx:
 
 
 # Measured tile choices (scripts/autotune.py on MI355X, in the hot path's own launch sequence):
+# XCD-slab tile order (esm_conv_desc.hint bit 30, esm_shuffle_tail_desc.flags bit 0; common.h xcd_block)
+# for launches whose input or output map (B x D x H x W) has at least this many pixels: there it takes
+# the memory-side bytes of the full-resolution convs from 2.1-2.9x the algorithmic to 1.05-1.13x at no
+# cost in step time, while on the hourglasses' small maps it measured 0.1-1 us slower per launch
+# (round 3, S-K, rocprofv3 op maps; every launch remapped: +10 us on the S-K step).
+HINT_XCD_SLAB = 1 << 30
+XCD_SLAB_MIN_PIX = int(os.environ.get("ESM_XCD_SLAB_MIN_PIX", "65536"))
+
 # shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
 _TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
 TUNED_HINTS: Dict[str, int] = {}
@@ -505,6 +513,8 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
     key = conv_key(d, nd)
     ctx.check_window(srcs, tag)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
+    if B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX:
+        d.hint |= HINT_XCD_SLAB
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd
     if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap
@@ -723,8 +733,9 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
     d.out = out.data_ptr()
     d.ob, d.oh = out.stride(0), out.stride(2)
     d.B, d.nf, d.H, d.W, d.r = B, nf, H, W, r
-    ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b)
     npix = B * H * W * r * r
+    d.flags = 1 if npix >= XCD_SLAB_MIN_PIX else 0
+    ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b)
     ctx.meta.append(dict(name=tag, kind="shuffle_tail", flops=2 * npix * nf * (1 + 9),
                          bytes=4 * (B * nf * H * W + npix), shape=f"nf{nf} r{r} in {H}x{W} out {H * r}x{W * r}",
                          reads=_spans(x), writes=_spans(out)))

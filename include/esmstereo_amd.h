@@ -128,7 +128,11 @@ typedef struct {
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
                      sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
                      split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
-                     8 waves per workgroup splitting K (layers with more than 4 channel groups). */
+                     8 waves per workgroup splitting K (layers with more than 4 channel groups).
+                     Bit 30 (any value of the other bits, including 0 = automatic): XCD-slab tile order for
+                     the small / wide / wide3 / wideT / pair / single-output ConvT forms: each XCD runs a
+                     contiguous band of tiles, so halo rows are fetched once per band instead of once per
+                     XCD (memory-side bytes ~1.1x the algorithmic instead of 2-3x on full-size maps). */
     int64_t ub, uh;
     float post_scale;
     float post_scale2;
@@ -200,7 +204,8 @@ typedef struct {
     float* out;
     int64_t ob, oh;
     int32_t B, nf, H, W, r;
-    int32_t reserved;
+    int32_t flags; /* bit 0: XCD-slab tile order (each XCD runs a contiguous band of output rows; see
+                      esm_conv_desc.hint bit 30) */
 } esm_shuffle_tail_desc;
 
 /* `tail(upsampling(x))` (as esm_shuffle_tail_desc, st.out unused) followed by the refinement
@@ -321,7 +326,8 @@ int esm_plan_num_ops(const esm_plan* plan);
  * fused forms) */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
- * (>= 0) or an error.  Drops a built graph (rebuild with esm_plan_graph_build). */
+ * (>= 0) or an error.  Bit 30 (tile order) is kept as the op was added, and is not part of the
+ * returned value.  Drops a built graph (rebuild with esm_plan_graph_build). */
 int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint);
 /* Diagnostics: launch op `index` `repeat` times per replay (0..8; 0 drops it, so the step time
  * minus the dropped step time is the op's marginal cost in the chain, gaps included).  Returns the

@@ -406,7 +406,8 @@ HINT_STEM, HINT_NO_STEM = 1 << 17, 1 << 18
 STEM_CASES = [(3, 32, 8, (6, 9, 21)), (3, 1, 8, (5, 7, 30)), (3, 8, 8, (7, 5, 29)), (3, 12, 12, (4, 6, 15)),
               (3, 32, 8, (2, 3, 10)), (3, 3, 8, (9, 4, 44)), (2, 16, 8, (23, 37)), (2, 8, 12, (17, 50)),
               (2, 64, 8, (33, 15)), (3, 24, 24, (5, 9, 31)), (3, 16, 16, (3, 6, 20)), (2, 32, 32, (19, 47)),
-              (2, 16, 16, (12, 39)), (3, 12, 24, (2, 3, 10)), (2, 40, 16, (9, 30))]
+              (2, 16, 16, (12, 39)), (3, 12, 24, (2, 3, 10)), (2, 40, 16, (9, 30)),
+              (3, 24, 24, (13, 32, 100))]  # the last: 8-wave workgroups (62 KB weight slab), ragged in 8 planes
 
 
 @pytest.mark.parametrize("nd,cin,cout,shape", STEM_CASES)
@@ -513,10 +514,12 @@ def test_convt_c1_form(nd, cin):
 
 
 @pytest.mark.parametrize("nf,r,H,W", [(8, 4, 24, 78), (8, 4, 7, 21), (8, 2, 13, 29), (16, 2, 24, 78), (16, 2, 5, 9),
-                                      (16, 4, 6, 17)])
+                                      (16, 4, 6, 17), (8, 4, 96, 312), (8, 2, 130, 301)])
 def test_shuffle_tail(nf, r, H, W):
     """upsampling (1x1 + PixelShuffle + SiLU) fused with tail (3x3 -> 1) vs fp64 torch of the
-    reference's two modules (models/ESMStereo.py:264-271,301-302); rel <= 1e-5."""
+    reference's two modules (models/ESMStereo.py:264-271,301-302); rel <= 1e-5.  Tiles: 8 x 32 (one
+    output per thread), 16 x 32 at 96 x 312 (S-K's 4x head: two per thread, XCD-slab order), 16 x 64
+    at 130 x 301 (four per thread, ragged)."""
     from esmstereo_amd.engine import pack_shuffle_tail, run_shuffle_tail
     torch.manual_seed(nf * 100 + r)
     up = torch.nn.Conv2d(nf, nf * r * r, 1, 1, 0)
