@@ -21,6 +21,7 @@
 // row tap, column tap.
 #pragma once
 
+#include "conv_direct.h"
 #include "conv_epilogue.h"
 
 namespace esm {
@@ -28,6 +29,52 @@ namespace conv {
 
 constexpr int kC1Threads = 256;
 constexpr int kC1TH = 16;  // output rows per tile
+
+// Per-thread staging plan of an input tile [NP planes][CC channels][IR rows][IC columns] (element i of
+// the tile = thread tid + 256 k): the buffer offset of its element at channel c0 = 0 (kOOB outside the
+// input or past the tile), its channel within the chunk and its LDS index, computed once; a chunk of
+// channels c0.. is then one buffer_load per element with the channel in the wave-uniform soffset and
+// one LDS store (no per-element index arithmetic per chunk: the index math was ~4x the FMAs).
+template <int XR, int XN, int NP, int CC, int IR, int IC, int ICP>
+struct C1Stage {
+    unsigned voff[XR];
+    int crel[XR];
+    int sidx[XR];
+    __device__ __forceinline__ C1Stage(const esm_conv_desc& a, int tid, int iz0, int iy0, int ix0) {
+        const esm_src& sr = a.src[0];
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int i = tid + k * kC1Threads;
+            const int col = i % IC;
+            const int row = (i / IC) % IR;
+            const int c = (i / (IC * IR)) % CC;
+            const int p = i / (IC * IR * CC);
+            const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
+            const bool ok = i < XN && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi && (NP == 1 || (iz >= 0 && iz < a.Di));
+            voff[k] = ok ? 4u * static_cast<unsigned>(c * sr.sc + (NP > 1 ? iz * sr.sd : 0) + iy * sr.sh + ix) : kOOB;
+            crel[k] = i < XN ? c : 1 << 30;
+            sidx[k] = ((p * CC + c) * IR + row) * ICP + col;
+        }
+    }
+    // channel chunk c0 of the tile into registers (every load in flight together)
+    __device__ __forceinline__ void load(float (&rx)[XR], __amdgpu_buffer_rsrc_t rs, int sc, int c0, int cin) const {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) rx[k] = buf_load_s(rs, crel[k] < cin - c0 ? voff[k] : kOOB, 4 * c0 * sc);
+    }
+    __device__ __forceinline__ void store(float* xs, const float (&rx)[XR]) const {
+#pragma unroll
+        for (int k = 0; k < XR; ++k)
+            if (k * kC1Threads + static_cast<int>(threadIdx.x) < XN) xs[sidx[k]] = rx[k];
+    }
+};
+
+// buffer descriptor over one batch item of the single source (range = its last element + 1)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t c1_src_rsrc(const esm_conv_desc& a, int b, bool d3) {
+    const esm_src& sr = a.src[0];
+    const long long span = (a.Cin - 1) * sr.sc + (d3 ? (a.Di - 1) * sr.sd : 0) + (a.Hi - 1) * sr.sh + a.Wi;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sr.ptr + b * sr.sb), static_cast<short>(0),
+                                             static_cast<int>(4 * span), 0x00020000);
+}
 
 // 2-D: the input tile of all channels (<= 32) and the weights staged with one batch of loads.
 template <bool D3, int CP, int QW>
@@ -55,24 +102,10 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
     const int qz = D3 ? (oz & 1) : 0;
     const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
-    const esm_src& sr = a.src[0];
-    const float* xb = sr.ptr + b * sr.sb;
-
     // ---- stage: every load of the thread in flight together, then the LDS stores
+    const C1Stage<XR, XN, NP, CP, IR, IC, ICP> stg(a, tid, iz0, iy0, ix0);
     float rx[XR], rw[WR];
-#pragma unroll
-    for (int k = 0; k < XR; ++k) {
-        const int i = tid + k * kC1Threads;
-        const int col = i % IC;
-        const int row = (i / IC) % IR;
-        const int c = (i / (IC * IR)) % CP;
-        const int p = i / (IC * IR * CP);
-        const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
-        const bool ok = i < XN && c < a.Cin && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi &&
-                        (!D3 || (iz >= 0 && iz < a.Di));
-        const float v = xb[ok ? c * sr.sc + (D3 ? iz * sr.sd : 0) + iy * sr.sh + ix : 0];
-        rx[k] = ok ? v : 0.f;
-    }
+    stg.load(rx, c1_src_rsrc(a, b, D3), static_cast<int>(a.src[0].sc), 0, a.Cin);
 #pragma unroll
     for (int k = 0; k < WR; ++k) {
         // LDS index (qz, qy, c, qx, tz, ty, tx) <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
@@ -90,17 +123,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
         rw[k] = ok ? v : 0.f;
     }
     __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
-#pragma unroll
-    for (int k = 0; k < XR; ++k) {
-        const int i = tid + k * kC1Threads;
-        if (i < XN) {
-            const int col = i % IC;
-            const int row = (i / IC) % IR;
-            const int c = (i / (IC * IR)) % CP;
-            const int p = i / (IC * IR * CP);
-            xs[p][c][row][col] = rx[k];
-        }
-    }
+    stg.store(&xs[0][0][0][0], rx);
 #pragma unroll
     for (int k = 0; k < WR; ++k) {
         const int i = tid + k * kC1Threads;
@@ -190,28 +213,12 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     const int qz = D3 ? (oz & 1) : 0;
     const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
-    const esm_src& sr = a.src[0];
-    const float* xb = sr.ptr + b * sr.sb;
     const int nch = (a.Cin + CC - 1) / CC;
-
-    // one channel chunk of the input tile: every load of the thread in flight together
-    auto load_chunk = [&](float (&rx)[XR], int c0) {
-#pragma unroll
-        for (int k = 0; k < XR; ++k) {
-            const int i = tid + k * kC1Threads;
-            const int col = i % IC;
-            const int row = (i / IC) % IR;
-            const int c = c0 + (i / (IC * IR)) % CC;
-            const int p = i / (IC * IR * CC);
-            const int iy = iy0 + row, ix = ix0 + col, iz = iz0 + p;
-            const bool ok = i < XN && c < a.Cin && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi &&
-                            (!D3 || (iz >= 0 && iz < a.Di));
-            const float v = xb[ok ? c * sr.sc + (D3 ? iz * sr.sd : 0) + iy * sr.sh + ix : 0];
-            rx[k] = ok ? v : 0.f;
-        }
-    };
+    const int sc = static_cast<int>(a.src[0].sc);
+    const __amdgpu_buffer_rsrc_t rs = c1_src_rsrc(a, b, D3);
+    const C1Stage<XR, XN, NP, CC, IR, IC, ICP> stg(a, tid, iz0, iy0, ix0);
     float rx[XR];
-    load_chunk(rx, 0);
+    stg.load(rx, rs, sc, 0, a.Cin);
     {
         float rw[WR];
 #pragma unroll
@@ -253,19 +260,9 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     for (int j = 0; j < QW; ++j) acc[j] = 0.f;
     for (int ch = 0; ch < nch; ++ch) {
         if (ch) __syncthreads();  // the previous chunk's reads of xs are done
-#pragma unroll
-        for (int k = 0; k < XR; ++k) {
-            const int i = tid + k * kC1Threads;
-            if (i < XN) {
-                const int col = i % IC;
-                const int row = (i / IC) % IR;
-                const int c = (i / (IC * IR)) % CC;
-                const int p = i / (IC * IR * CC);
-                xs[p][c][row][col] = rx[k];
-            }
-        }
+        stg.store(&xs[0][0][0][0], rx);
         __syncthreads();
-        if (ch + 1 < nch) load_chunk(rx, (ch + 1) * CC);  // next chunk in flight during this one's FMAs
+        if (ch + 1 < nch) stg.load(rx, rs, sc, (ch + 1) * CC, a.Cin);  // next chunk in flight during this one's FMAs
 #pragma unroll
         for (int tz = 0; tz < NP; ++tz) {
             const int p = D3 ? 1 - tz : 0;  // plane tap t = tz sits at tile plane 1 - t

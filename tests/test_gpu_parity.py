@@ -502,6 +502,12 @@ def test_convt_c1_form(nd, cin):
     p = pk(conv, None, ACT_NONE)
     for h in (0, 1 << 16):
         assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
+    # a channel slice of a wider tensor (batch stride > C * plane): channels past Cin in a staged chunk
+    # must read as zero, not as the wider tensor's next channels
+    wide = torch.randn(shape[0], cin + 7, *shape[2:], device=DEV)
+    wide[:, 3:3 + cin] = x.to(DEV)
+    wide[:, 3 + cin:] = float("nan")
+    assert rel(run_conv(Ctx(DEV), p, [wide[:, 3:3 + cin]]), ref) < 1e-5
     if nd == 2:  # the up_refinement epilogue: + bilinear(prev, x2), x4 store, unscaled copy
         prev = torch.randn(2, 1, 13, 45)
         cp = torch.empty(2, 1, 26, 90, device=DEV)
