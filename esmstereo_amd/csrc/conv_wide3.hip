@@ -20,11 +20,10 @@ namespace esm {
 namespace conv {
 namespace {
 
-constexpr int kW3Threads = 256;
-
-template <int KSW, int NGW, int ZW, int ACT, bool PLAIN, bool PZ>
-__global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc a) {
-    constexpr int ZS = 4 / KSW;        // plane sub-blocks per workgroup
+// KSW x ZS waves per workgroup: KSW ways over channel groups, ZS plane sub-blocks
+template <int KSW, int NGW, int ZW, int ACT, bool PLAIN, bool PZ, int ZS = 4 / KSW>
+__global__ void __launch_bounds__(64 * KSW * ZS) wconv3_kernel(const esm_conv_desc a) {
+    constexpr int kW3Threads = 64 * KSW * ZS;
     constexpr int NZ = ZW + 2;         // input planes a wave streams
     constexpr int ZB = ZW * ZS;        // output planes per workgroup
     // PZ (<= 8 couts): the 16 MFMA rows hold 8 couts x 2 output planes (a plane pair 2q, 2q + 1), so
@@ -32,7 +31,7 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
     // 0..3: rows 0-7 use tap plane dz = r (if <= 2), rows 8-15 dz = r - 1 (if >= 0); 4 weight sets
     constexpr int NA = PZ ? ZW / 2 : ZW;  // accumulators (pairs or planes)
     static_assert(!PZ || ZW % 2 == 0, "plane pairs need an even plane block");
-    __shared__ __attribute__((aligned(16))) float red[4][NA][4][64];
+    __shared__ __attribute__((aligned(16))) float red[KSW * ZS][NA][4][64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
@@ -134,7 +133,8 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
         for (int j = 0; j < 4; ++j) red[wave][z][j][lane] = acc[z][j];
     __syncthreads();
     // elements (plane sub-block zp, accumulator z, j, lane) over the 256 threads, lane fastest
-    constexpr int NE = ZS * NA * 4 * 64 / kW3Threads;  // elements per thread
+    constexpr int NEL = ZS * NA * 4 * 64;                      // elements (zp, z, j, lane)
+    constexpr int NE = (NEL + kW3Threads - 1) / kW3Threads;  // elements per thread
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
         4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
@@ -143,6 +143,7 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         const int idx = e * kW3Threads + static_cast<int>(threadIdx.x);  // over (zp, z, j, lane)
+        if (NEL % kW3Threads != 0 && idx >= NEL) break;
         const int l = idx & 63, j = (idx >> 6) & 3, zz = idx >> 8;       // zz = zp * NA + z (= e)
         const int zp = zz / NA, z = zz - zp * NA;
         float v = red[zp * KSW][z][j][l];
@@ -172,9 +173,10 @@ __global__ void __launch_bounds__(kW3Threads) wconv3_kernel(const esm_conv_desc 
     }
 }
 
-template <int KSW, int NGW, int ZW>
+template <int KSW, int NGW, int ZW, int ZS = 4 / KSW>
 int launch_w3(const esm_conv_desc& a, hipStream_t s) {
-    constexpr int ZB = ZW * (4 / KSW);
+    constexpr int ZB = ZW * ZS;
+    constexpr int kW3Threads = 64 * KSW * ZS;
     const long long z = static_cast<long long>(a.B) * ((a.Do + ZB - 1) / ZB);
     if (a.Ho > 65535 || z > 65535) return arg_error("conv(wide3): grid too large");
     const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(a.Ho), static_cast<unsigned>(z));
@@ -183,14 +185,14 @@ int launch_w3(const esm_conv_desc& a, hipStream_t s) {
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (a.Cout <= 8) {  // plane pairs: no padding MFMA rows
         if (plain)
-            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, true>), grid, dim3(kW3Threads), 0, s, a);
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, true, ZS>), grid, dim3(kW3Threads), 0, s, a);
         else
-            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, true>), grid, dim3(kW3Threads), 0, s, a);
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, true, ZS>), grid, dim3(kW3Threads), 0, s, a);
     } else {
         if (plain)
-            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, false>), grid, dim3(kW3Threads), 0, s, a);
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, ESM_ACT_GELU, true, false, ZS>), grid, dim3(kW3Threads), 0, s, a);
         else
-            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, false>), grid, dim3(kW3Threads), 0, s, a);
+            hipLaunchKernelGGL((wconv3_kernel<KSW, NGW, ZW, -1, false, false, ZS>), grid, dim3(kW3Threads), 0, s, a);
     }
     return check_launch("conv(wide3)");
 }
@@ -207,6 +209,12 @@ bool wide3_ok(const esm_conv_desc& a) {
     return direct_ok(a);
 }
 
+#ifdef ESM_W3_NOSPLIT8
+constexpr bool kW3Split8 = false;  // A/B builds
+#else
+constexpr bool kW3Split8 = true;
+#endif
+
 int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
     if (!wide3_ok(a)) return arg_error("conv: wide3-form hint not applicable");
     const int ng = (a.Cin + 3) / 4;
@@ -215,7 +223,9 @@ int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
     const long long vox = rows * a.Do;
     if (ng > 4) {  // 5..8 groups: 4 waves split K, 2 groups each; more planes per wave on big volumes
         if (vox >= 16LL * 65536) return launch_w3<4, 2, 8>(a, s);
-        return vox >= 4LL * 16384 ? launch_w3<4, 2, 4>(a, s) : launch_w3<4, 2, 2>(a, s);
+        if (vox >= 4LL * 16384) return launch_w3<4, 2, 4>(a, s);
+        // small volumes (S-K group_stem): 8 waves, one group each, halving each wave's load -> MFMA chain
+        return kW3Split8 ? launch_w3<8, 1, 2, 1>(a, s) : launch_w3<4, 2, 2>(a, s);
     }
     if (ng > 2) return launch_w3<4, 1, 2>(a, s);  // 3..4 groups: one each
     if (ng == 2) return rows * a.Do >= 4LL * 16384 ? launch_w3<2, 1, 4>(a, s) : launch_w3<2, 1, 2>(a, s);

@@ -182,6 +182,8 @@ class Ctx:
         self.stream = None if plan else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         self._arena: Optional[torch.Tensor] = None
         self._arena_off = 0
+        self.arena_bytes = 0   # bytes carved out of the arena (256-B granules)
+        self.arena_chunks = 0
 
     def launch(self, graph: bool = True, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Run a plan context's launch list (as a hipGraph by default) on the current stream."""
@@ -220,14 +222,33 @@ class Ctx:
             return torch.empty(shape, device=self.device, dtype=torch.float32)
         n = math.prod(shape)
         nb = (4 * n + 255) // 256 * 256
-        if self._arena is None or self._arena_off + nb > self._arena.numel():
+        if self._arena is None or self._arena_off + nb > self._tail_lo():
             size = self.ARENA_FIRST if self._arena is None else min(self.ARENA_CHUNK, 2 * self._arena.numel())
             self._arena = torch.empty(max(size, nb), device=self.device, dtype=torch.uint8)
             self._arena_off = 0
+            self._tail = None
+            self.arena_chunks += 1
             self.keep.append(self._arena)
         t = self._arena[self._arena_off:self._arena_off + 4 * n].view(torch.float32).view(shape)
         self._arena_off += nb
+        self.arena_bytes += nb
         return t
+
+    def empty_tail(self, *shape: int) -> torch.Tensor:
+        """A float32 buffer carved from the END of the current arena chunk (which must have room):
+        the hot path's backbone-feature inputs go there, next to the upsampler's buffers (the last
+        ones the plan allocates from the front) that they are concatenated with."""
+        n = math.prod(shape)
+        nb = (4 * n + 255) // 256 * 256
+        if not self.plan or self._arena is None or self._arena_off + nb > self._tail_lo():
+            return self.empty(*shape)
+        self._tail = self._tail_lo() - nb
+        self.arena_bytes += nb
+        return self._arena[self._tail:self._tail + 4 * n].view(torch.float32).view(shape)
+
+    def _tail_lo(self) -> int:
+        t = getattr(self, "_tail", None)
+        return self._arena.numel() if t is None or t > self._arena.numel() else t
 
     WINDOW = 1 << 30  # conv_direct.h kOOB: a concat's sources must span less than this
     _window_warned = False
@@ -236,7 +257,7 @@ class Ctx:
         """Warn (once per process) when a channel concat's sources span >= 1 GiB: the register-weight
         forms then cannot address them through one descriptor and the launch silently takes a slower
         form (conv_direct.h source_window)."""
-        if len(srcs) < 2 or Ctx._window_warned:
+        if len(srcs) < 2 or Ctx._window_warned or getattr(self, "sizing", False):
             return
         lo = min(t.data_ptr() for t in srcs)
         hi = max(t.data_ptr() + 4 * (1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()))) for t in srcs)

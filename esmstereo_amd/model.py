@@ -111,17 +111,36 @@ class HotPath:
 
     def __init__(self, model: "ESMStereo", B: int, h: int, w: int, att_ch: int, up_shapes: Sequence[Tuple[int, ...]],
                  device: torch.device, train_status: bool = False, graph: bool = True, channels: int = 64):
-        self.ctx = Ctx(device, plan=True)
         self.device = torch.device(device)
+        args = (model, B, h, w, att_ch, up_shapes, train_status, channels)
+        self._emit(*args, first=Ctx.ARENA_FIRST, sizing=True)
+        if self.ctx.arena_chunks > 1:
+            # every buffer of the plan in ONE arena chunk: chunks allocated one by one can land more
+            # than 1 GiB apart in the address space, and a channel concat whose sources straddle two
+            # such chunks cannot be addressed through one buffer descriptor by the register-weight
+            # forms (conv_direct.h source_window), which then fall back to slower ones (measured: the
+            # S-K step 346.6 vs 363-366 us, depending on where the allocator placed the chunks)
+            need = self.ctx.arena_bytes + (1 << 20)
+            self.ctx.close()
+            self._emit(*args, first=need)
+        self.num_ops = lib.esm_plan_num_ops(self.ctx.plan)
+        self.graph = bool(graph)
+        self._graph_ready = False
+
+    def _emit(self, model, B, h, w, att_ch, up_shapes, train_status, channels, first: int,
+              sizing: bool = False) -> None:
+        self.ctx = Ctx(self.device, plan=True)
+        self.ctx.ARENA_FIRST = first
+        self.ctx.sizing = sizing  # a sizing pass: its buffer placement is discarded, so no window warning
         e = self.ctx.empty
         self.ml = e(B, channels, h, w)
         self.mr = e(B, channels, h, w)
         self.att = e(B, att_ch, h, w) if att_ch else None
-        self.up = [e(*s) for s in up_shapes]
+        # the upsampler's feature inputs at the arena's far end, next to the buffers allocated last
+        # (the upsampler's own, which they are concatenated with): a concat's sources stay within one
+        # 1 GiB window even when the cost volume between them is larger (configs[2]: B = 8)
+        self.up = [self.ctx.empty_tail(*s) for s in up_shapes]
         self.outputs = model._emit_hot(self.ctx, self.ml, self.mr, self.att, self.up, train_status)
-        self.num_ops = lib.esm_plan_num_ops(self.ctx.plan)
-        self.graph = bool(graph)
-        self._graph_ready = False
 
     def op_kinds(self) -> List[int]:
         return [lib.esm_plan_op_kind(self.ctx.plan, i) for i in range(self.num_ops)]

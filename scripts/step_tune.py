@@ -116,7 +116,7 @@ def step_only(variant: str, dev, rounds: int) -> dict:
     return {"variant": variant, "step_us": round(med, 2), "windows": [round(t, 2) for t in ts]}
 
 
-def tune(variant: str, dev, rounds: int, margin_us: float) -> dict:
+def tune(variant: str, dev, rounds: int, margin_us: float, only=()) -> dict:
     hp = build(variant, dev)
     plan, meta = hp.ctx.plan, hp.ctx.meta
     reps = reps_for(hp)
@@ -124,7 +124,7 @@ def tune(variant: str, dev, rounds: int, margin_us: float) -> dict:
     step0 = statistics.median(window(hp, reps) for _ in range(5))
     chosen, rows = {}, []
     for i, m in enumerate(meta):
-        if m["kind"] != "conv":
+        if m["kind"] != "conv" or (only and not any(o in m["name"] for o in only)):
             continue
         cur = lib.esm_plan_set_conv_hint(plan, i, 0)
         lib.esm_plan_set_conv_hint(plan, i, cur)
@@ -164,6 +164,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--margin-us", type=float, default=0.3)
     ap.add_argument("--out", default="")
+    ap.add_argument("--only", default="", help="tune: comma-separated substrings of the op names to tune")
     ap.add_argument("--report", default=os.path.join(ROOT, "gpurun_out", "step_tune_report.json"))
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -174,7 +175,8 @@ def main():
     elif args.mode == "step":
         reports = [step_only(v, dev, args.rounds) for v in variants]
     else:
-        reports = [tune(v, dev, args.rounds, args.margin_us) for v in variants]
+        only = tuple(o for o in args.only.split(",") if o)
+        reports = [tune(v, dev, args.rounds, args.margin_us, only) for v in variants]
     os.makedirs(os.path.dirname(args.report), exist_ok=True)
     with open(args.report, "w") as f:
         json.dump(reports, f, indent=1)
