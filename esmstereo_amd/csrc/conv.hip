@@ -31,9 +31,9 @@ constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-
 constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
 constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 form, all 4 classes per wave (conv_widet.hip)
 
-int launch_conv(const esm_conv_desc* d, hipStream_t s) {
-    if (!d) return arg_error("conv: null descriptor");
-    const esm_conv_desc& a = *d;
+// Descriptor validation shared by every entry point that takes an esm_conv_desc (launch_conv, the
+// chain of chain.hip); ESM_OK or ESM_ERR_ARG with the message set.
+int conv_check(const esm_conv_desc& a) {
     if (!a.w || !a.out) return arg_error("conv: null weights/output");
     if (a.nsrc < 1 || a.nsrc > ESM_MAX_SRC) return arg_error("conv: nsrc must be 1..3");
     int cin = 0;
@@ -56,15 +56,12 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (a.shuffle > 1 && (d3 || a.transposed)) return arg_error("conv: pixel shuffle only for 2-D convs");
     if (a.up && (a.Cout != 1 || d3 || a.up_f <= 0)) return arg_error("conv: bilinear add needs 2-D, Cout == 1");
     if (a.Hi <= 0 || a.Wi <= 0 || a.Di <= 0) return arg_error("conv: empty input");
-    const int form = a.hint & ~kHintXcd;  // the form / tile bits (bit 30 only orders the tiles)
     if (a.transposed) {
         if (a.kh != 4 || a.stride != 2 || a.ph != 1 || a.pw != 1 || (d3 && a.pd != 1))
             return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
         if (a.Ho != 2 * a.Hi || a.Wo != 2 * a.Wi || (d3 && a.Do != 2 * a.Di))
             return arg_error("conv: transposed output extent must be 2x the input");
-        if (a.hint & kHintWideT) return conv::launch_widet(a, s);
-        if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
-        return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
+        return ESM_OK;
     }
     const int S = a.stride;
     if (S != 1 && S != 2) return arg_error("conv: stride must be 1 or 2");
@@ -72,6 +69,21 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         (d3 && a.Do != (a.Di + 2 * a.pd - a.kd) / S + 1))
         return arg_error("conv: output extent inconsistent with kernel/stride/padding");
     if (a.Ho <= 0 || a.Wo <= 0 || a.Do <= 0) return arg_error("conv: empty output");
+    return ESM_OK;
+}
+
+int launch_conv(const esm_conv_desc* d, hipStream_t s) {
+    if (!d) return arg_error("conv: null descriptor");
+    const esm_conv_desc& a = *d;
+    const int rc = conv_check(a);
+    if (rc != ESM_OK) return rc;
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    const int form = a.hint & ~kHintXcd;  // the form / tile bits (bit 30 only orders the tiles)
+    if (a.transposed) {
+        if (a.hint & kHintWideT) return conv::launch_widet(a, s);
+        if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
+        return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
+    }
     if (a.hint & kHintSmall) return conv::launch_small(a, s);
     if (a.hint & kHintWide) {
         // a tuned choice for a concat whose sources lie outside one buffer window (eager use, outside

@@ -233,6 +233,18 @@ int launch_c(const esm_smix_desc& a, hipStream_t s) {
 // halo and t2 on the tile plus an R halo (each zero outside the image: the depthwise convs' zero
 // padding), then the output.  Per pixel and channel the operations and their order are those of
 // smix_kernel (equal to the three-launch chain up to the compiler's FMA contraction choices).
+#ifdef ESM_CONV_STAMPS
+// Diagnostic build only: s_memrealtime (100 MHz) of workgroup-thread 0 at each phase boundary of the
+// whole-FMBlock kernel, [workgroup][8] (esm_diag_fmnet_stamps); never in the product library.
+__device__ unsigned long long fm_stamps[4096 * 8];
+#define FM_STAMP(k)                                                                                   \
+    do {                                                                                              \
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);          \
+        if (threadIdx.x == 0 && wg_ < 4096) fm_stamps[wg_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define FM_STAMP(k) (void)0
+#endif
 constexpr int kFTW = 16;
 // 512 threads: the t1 region is one pass (448 / 480 pixels), the t2 region one pass, the depthwise
 // phases half the iterations of a 256-thread workgroup
@@ -255,14 +267,17 @@ constexpr int kFConvTallMinTiles = 512;  // 3-row tiles at or above this many (2
 // the products are summed over ky, then kx, as in smix_kernel.  Lanes of the last segment of a row
 // compute (and drop) up to SEG - 1 outputs past OW: src needs SEG + K - 2 floats of slack at its end.
 template <int C, int K, int OH, int OW, int SH, int SWP, int SEG>
-__device__ __forceinline__ void dw_region(const float* src, float* dst, const float* __restrict__ gw,
-                                          const float* __restrict__ gb, int wave, int lane) {
+__device__ __forceinline__ void dw_region(const float* src, float* dst, const float* lw, const float* lb, int wave,
+                                          int lane) {
     constexpr int NSEG = (OW + SEG - 1) / SEG;
     constexpr int ITEMS = OH * NSEG;
     constexpr int NWAVES = kFThreads / 64;
     for (int c = wave; c < C; c += NWAVES) {
-        const float* w = gw + c * K * K;
-        const float bias = gb[c];
+        // the channel's K*K weights from the workgroup's LDS copy into registers (broadcast reads)
+        float w[K * K];
+#pragma unroll
+        for (int i = 0; i < K * K; ++i) w[i] = lw[c * K * K + i];
+        const float bias = lb[c];
         for (int it = lane; it < ITEMS; it += 64) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
             float acc[SEG];
@@ -314,6 +329,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
     const long long plane = static_cast<long long>(H) * W;
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
+    FM_STAMP(0);
 
     // Cache warm-up: every weight is touched by one vector load here, all in flight together with the
     // t1 pixel loads, so that the scalar loads of the phases below hit L2 instead of each paying a
@@ -325,6 +341,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int CV2 = CV0 + (CONV ? HID * C * 9 + HID : 0);
     constexpr int NW = CV2 + (CONV ? C * HID + C : 0);
     constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
+    // the depthwise, conv0 and conv2 weights (everything past the four mlp stages) go to LDS: their phases
+    // read them as LDS broadcasts (as scalar loads they were a chain of L2 round trips per phase:
+    // dw0 1.6, dw1 1.5, conv0 3.5 us of the 12.4-us block at S-K, profiles/r03_fmnet_phases.txt)
+    constexpr int NLW = NW - DW0;
+    __shared__ float sw[NLW];
     __shared__ float wsink[kFThreads];
     float rw[NWR];
 #pragma unroll
@@ -370,9 +391,17 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     {
         float sink = 0.f;
 #pragma unroll
-        for (int k = 0; k < NWR; ++k) sink += rw[k];
+        for (int k = 0; k < NWR; ++k) {
+            const int i = tid + k * kFThreads;
+            if (i >= DW0 && i < NW) sw[i - DW0] = rw[k];
+            else sink += rw[k];
+        }
         wsink[tid] = sink;
     }
+    const float* lw_dw0 = sw;                          // [C][K][K], then bias [C]
+    const float* lw_dw1 = sw + (DW1 - DW0);
+    const float* lw_cv0 = sw + (CV0 - DW0);            // conv0_w [HID][C][9], then conv0_b [HID]
+    const float* lw_cv2 = sw + (CV2 - DW0);            // conv2_w [C][HID], then conv2_b [C]
     // t1 = SMLayer0.mlp1 (x) on region A
     if (q < AP) {
         if (ain) mix_stage_g<C>(t1, a.stage[0]);
@@ -380,9 +409,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
     __syncthreads();
+    FM_STAMP(1);
     // dw0 (t1) on region B
-    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, a.dw_w[0], a.dw_b[0], wave, lane);
+    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, lw_dw0, lw_dw0 + C * K * K, wave, lane);
     __syncthreads();
+    FM_STAMP(2);
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
     for (int p = tid; p < BP; p += kFThreads) {
         const int py = p / BW, px = p - (p / BW) * BW;
@@ -399,9 +430,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
     }
     __syncthreads();
+    FM_STAMP(3);
     // dw1 (t2) on region C
-    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, a.dw_w[1], a.dw_b[1], wave, lane);
+    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, lw_dw1, lw_dw1 + C * K * K, wave, lane);
     __syncthreads();
+    FM_STAMP(4);
     // t3 = SMLayer1.mlp2 (dw1) + x on region C
     if constexpr (!CONV) {
         if (tid >= CP) return;
@@ -436,6 +469,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             for (int c = 0; c < C; ++c) s3[c * CP + tid] = in ? t[c] : 0.f;
         }
         __syncthreads();
+        FM_STAMP(5);
         // h = silu(conv0(t3) + b0) on the tile: a wave owns HID / 8 hidden channels (scalar weight
         // loads), a lane one pixel; each t3 value read from LDS feeds all of the wave's channels
         constexpr int HPW = HID / NWAVES;
@@ -444,7 +478,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             float acc[HPW];
 #pragma unroll
             for (int j = 0; j < HPW; ++j) acc[j] = 0.f;
-            const float* w0 = a.conv0_w + wave * HPW * C * 9;
+            const float* w0 = lw_cv0 + wave * HPW * C * 9;
 #pragma unroll
             for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -458,10 +492,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
             for (int j = 0; j < HPW; ++j) {
                 const int hc = wave * HPW + j;
-                sh[hc * NPX + lane] = silu(acc[j] + a.conv0_b[hc]);
+                sh[hc * NPX + lane] = silu(acc[j] + lw_cv0[HID * C * 9 + hc]);
             }
         }
         __syncthreads();
+        FM_STAMP(6);
         // out = conv2(h) + b2 + t3 on the tile: a wave owns C / 8 output channels, a lane one pixel
         if (lane < NPX) {
             const int py = lane / TW, px = lane - (lane / TW) * TW;
@@ -469,15 +504,17 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             if (y < H && x < W) {
 #pragma unroll
                 for (int c = wave; c < C; c += NWAVES) {
-                    const float* w = a.conv2_w + c * HID;
+                    const float* w = lw_cv2 + c * HID;
                     float sacc = 0.f;
 #pragma unroll
                     for (int hc = 0; hc < HID; ++hc) sacc += w[hc] * sh[hc * NPX + lane];
-                    const float v = sacc + a.conv2_b[c] + s3[(c * CH + py + HC) * CW + px + HC];
+                    const float v = sacc + lw_cv2[C * HID + c] + s3[(c * CH + py + HC) * CW + px + HC];
                     a.out[static_cast<long long>(b) * C * plane + c * plane + static_cast<long long>(y) * W + x] = v;
                 }
             }
         }
+        __syncthreads();
+        FM_STAMP(7);
     }
 }
 
@@ -541,6 +578,14 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
 extern "C" int esm_fmnet_f32(const esm_fmnet_desc* desc, void* stream) {
     return esm::launch_fmnet(desc, esm::as_stream(stream));
 }
+
+#ifdef ESM_CONV_STAMPS
+// Diagnostic build only: copy n <= 4096 * 8 fmnet phase stamps to the host.
+extern "C" int esm_diag_fmnet_stamps(unsigned long long* host, int n) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(esm::fm_stamps), 8ull * n) == hipSuccess ? n : -1;
+}
+#endif
 
 extern "C" int esm_smix_f32(const esm_smix_desc* desc, void* stream) {
     return esm::launch_smix(desc, esm::as_stream(stream));
