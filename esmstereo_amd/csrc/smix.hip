@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int NWAVES = kFThreads / 64;
     constexpr int NPX = TH * TW;
     static_assert(AP <= kFThreads, "one t1 pixel per thread");
-    static_assert(!CONV || (HID % NWAVES == 0 && NPX <= 64), "conv0: HID / 8 hidden channels per wave, one pixel per lane");
+    static_assert(!CONV || NPX <= 64, "conv2: one pixel per lane");
     // Weights are never staged: every weight index below is wave-uniform, so they are scalar loads
     // (the LDS then only carries activations: one read per operand of the depthwise / 3x3 convs)
     __shared__ float s1[C * AH * AWP + SLACK];  // t1 image, then t2 image ([C][BH][BWP])
@@ -388,16 +388,6 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         const float v = xb[ain ? c * plane + agy * W + agx : 0];
         t1[c] = ain ? v : 0.f;
     }
-    {
-        float sink = 0.f;
-#pragma unroll
-        for (int k = 0; k < NWR; ++k) {
-            const int i = tid + k * kFThreads;
-            if (i >= DW0 && i < NW) sw[i - DW0] = rw[k];
-            else sink += rw[k];
-        }
-        wsink[tid] = sink;
-    }
     const float* lw_dw0 = sw;                          // [C][K][K], then bias [C]
     const float* lw_dw1 = sw + (DW1 - DW0);
     const float* lw_cv0 = sw + (CV0 - DW0);            // conv0_w [HID][C][9], then conv0_b [HID]
@@ -407,6 +397,16 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         if (ain) mix_stage_g<C>(t1, a.stage[0]);
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
+    }
+    {  // the warm-up values: LDS weights (after the t1 chain, which does not wait for them)
+        float sink = 0.f;
+#pragma unroll
+        for (int k = 0; k < NWR; ++k) {
+            const int i = tid + k * kFThreads;
+            if (i >= DW0 && i < NW) sw[i - DW0] = rw[k];
+            else sink += rw[k];
+        }
+        wsink[tid] = sink;
     }
     __syncthreads();
     FM_STAMP(1);
@@ -472,28 +472,22 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         FM_STAMP(5);
         // h = silu(conv0(t3) + b0) on the tile: a wave owns HID / 8 hidden channels (scalar weight
         // loads), a lane one pixel; each t3 value read from LDS feeds all of the wave's channels
-        constexpr int HPW = HID / NWAVES;
-        if (lane < NPX) {
-            const int py = lane / TW, px = lane - (lane / TW) * TW;
-            float acc[HPW];
-#pragma unroll
-            for (int j = 0; j < HPW; ++j) acc[j] = 0.f;
-            const float* w0 = lw_cv0 + wave * HPW * C * 9;
+        // h = silu(conv0(t3) + b0) on the tile: one (hidden channel, pixel) output per thread and pass, so
+        // every lane works (a wave owning HID / 8 channels of the tile's 16 pixels left 3/4 of its lanes
+        // idle: 1.6 us of the S-K block); weights as LDS reads, per output the products summed over c, ky,
+        // kx as before
+        for (int e = tid; e < HID * NPX; e += kFThreads) {
+            const int hc = e / NPX, pp = e - (e / NPX) * NPX;
+            const int py = pp / TW, px = pp - (pp / TW) * TW;
+            const float* w0 = lw_cv0 + hc * C * 9;
+            float acc = 0.f;
 #pragma unroll
             for (int c = 0; c < C; ++c)
 #pragma unroll
                 for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) {
-                        const float v = s3[(c * CH + py + ky) * CW + px + kx];
-#pragma unroll
-                        for (int j = 0; j < HPW; ++j) acc[j] += w0[(j * C + c) * 9 + ky * 3 + kx] * v;
-                    }
-#pragma unroll
-            for (int j = 0; j < HPW; ++j) {
-                const int hc = wave * HPW + j;
-                sh[hc * NPX + lane] = silu(acc[j] + lw_cv0[HID * C * 9 + hc]);
-            }
+                    for (int kx = 0; kx < 3; ++kx) acc += w0[c * 9 + ky * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
+            sh[hc * NPX + pp] = silu(acc + lw_cv0[HID * C * 9 + hc]);
         }
         __syncthreads();
         FM_STAMP(6);
