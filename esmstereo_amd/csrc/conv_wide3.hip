@@ -14,6 +14,8 @@
 // multiplied.  With <= 8 couts the 16 MFMA rows carry two output planes (a plane pair), so no row
 // is padding.  The waves' partial tiles meet in LDS at the end and are added in a fixed order
 // (deterministic); every thread then finishes its (plane, cout, pixel) elements.
+#include <cstdlib>
+
 #include "conv_direct.h"
 
 namespace esm {
@@ -173,6 +175,170 @@ __global__ void __launch_bounds__(64 * KSW * ZS) wconv3_kernel(const esm_conv_de
     }
 }
 
+// Row-streaming variant for the small volumes (S-K group_stem: 32 -> 8 on 12x24x78), where the plane-pair
+// form above with one output row per workgroup re-fetched every weight once per workgroup and every input
+// row three times from L2: 720 workgroups x 8 waves x (36 weight + 36 input loads) ~ 106 MB of L2 -> CU
+// traffic for 3.7 MB of algorithmic bytes.  Here a workgroup owns RB consecutive output rows of its
+// 16-column strip and plane pair: each wave (one 4-channel group) loads its 36 weight operands once and
+// streams input rows through a 4-row register ring (load row y + 2 while the MFMAs of row y run), so per
+// output row it loads 12 input operands instead of 36.  Per wave and output row the MFMAs run in the
+// same order as wconv3_kernel<8, 1, 2, ..> (input plane, then tap), and the 8 waves' partial tiles are
+// added in the same fixed order: results are bit-identical to that form.
+template <int RB, int ACT, bool PLAIN, int NACC>
+__global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
+    constexpr int KSW = 8;
+    __shared__ __attribute__((aligned(16))) float red[KSW][RB][4][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int n16 = lane & 15, kq = lane >> 4;
+    const int x0 = blockIdx.x * 16;
+    const int y0 = blockIdx.y * RB;
+    const int nzb = (a.Do + 1) / 2;
+    const int b = blockIdx.z / nzb;
+    const int z0 = (blockIdx.z - b * nzb) * 2;  // the plane pair z0, z0 + 1
+
+    // weights of group `wave` for the 4 pair-relative input planes (rows 8-15 of the MFMA lag one plane)
+    float wv[4][9];
+    {
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
+        const unsigned wl = 4u * (kq * a.cout_pad + (n16 & 7));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int dz = n16 < 8 ? r : r - 1;
+                const bool ok = dz >= 0 && dz <= 2;
+                wv[r][t] = buf_load_s(wrs, ok ? wl : kOOB, 4 * (((ok ? dz : 0) * 9 + t) * a.cin_pad + 4 * wave) * a.cout_pad);
+            }
+    }
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
+        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const int xo = x0 + n16;
+    const int c = 4 * wave + kq;
+    unsigned vo[3];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+        const int xi = xo - 1 + dx;
+        vo[dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
+    }
+    int poff[4];  // input planes z0 - 1 .. z0 + 2 (kOOB outside)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int zi = z0 - 1 + p;
+        poff[p] = (zi >= 0 && zi < a.Di) ? 4 * zi * sd : static_cast<int>(kOOB);
+    }
+    // ring of input rows: row yi = y0 - 1 + k lives in slot k % 4
+    float ring[4][4][3];  // [slot][plane][dx]
+    auto load_row = [&](float (&d)[4][3], int k) {
+        const int yi = y0 - 1 + k;
+        const int ro = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) d[p][dx] = buf_load_s(rs, vo[dx], poff[p] + ro);
+    };
+    load_row(ring[0], 0);
+    load_row(ring[1], 1);
+    // NACC = 2: the row's 36 MFMAs alternate between two accumulators (two dependency chains for the
+    // matrix pipe), added at the end; NACC = 1 is the plane-pair form's exact summation order
+    floatx4 acc[RB][NACC];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) acc[r][k] = floatx4{0.f, 0.f, 0.f, 0.f};
+        load_row(ring[(r + 2) & 3], r + 2);  // output row y0 + r needs input rows r .. r + 2 (ring index)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int t = (p * 3 + dy) * 3 + dx;
+                    acc[r][t % NACC] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[p][dy * 3 + dx], ring[(r + dy) & 3][p][dx],
+                                                                           acc[r][t % NACC], 0, 0, 0);
+                }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[wave][r][j][lane] = NACC == 1 ? acc[r][0][j] : acc[r][0][j] + acc[r][NACC - 1][j];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0),
+        4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) + (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+    constexpr int NEL = RB * 4 * 64;  // elements (r, j, lane)
+#pragma unroll
+    for (int e = 0; e < (NEL + 511) / 512; ++e) {
+        const int idx = e * 512 + static_cast<int>(threadIdx.x);
+        if (NEL % 512 != 0 && idx >= NEL) break;
+        const int l = idx & 63, j = (idx >> 6) & 3, r = idx >> 8;
+        float v = red[0][r][j][l];
+#pragma unroll
+        for (int k = 1; k < KSW; ++k) v += red[k][r][j][l];
+        const int row = 4 * (l >> 4) + j;
+        const int co = row & 7;
+        const int zo = z0 + (row >> 3);
+        const int y = y0 + r;
+        const int px = x0 + (l & 15);
+        const float sc_ = a.scale ? a.scale[min(co, a.Cout - 1)] : 1.f;
+        const float sh_ = a.shift ? a.shift[min(co, a.Cout - 1)] : 0.f;
+        v = a.scale ? v * sc_ + sh_ : v + sh_;
+        v = act_t<ACT>(v, a.act);
+        if constexpr (PLAIN) {
+            const unsigned o = (co < a.Cout && px < a.Wo && zo < a.Do && y < a.Ho)
+                                   ? 4u * (co * static_cast<int>(a.oc) + zo * static_cast<int>(a.od) + y * static_cast<int>(a.oh) + px)
+                                   : kOOB;
+            store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0);
+        } else {
+            if (co >= a.Cout || px >= a.Wo || zo >= a.Do || y >= a.Ho) continue;
+            if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + static_cast<long long>(y) * a.mh + px];
+            if (a.res) v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(zo) * a.rd + static_cast<long long>(y) * a.rh + px];
+            const long long o = b * a.ob + co * a.oc + static_cast<long long>(zo) * a.od + static_cast<long long>(y) * a.oh + px;
+            a.out[o] = v * a.post_scale;
+            if (a.out2) a.out2[o] = v * a.post_scale2;
+        }
+    }
+}
+
+// output rows per workgroup of the row-streaming variant (A/B: ESM_W3_ROWS=1 disables it) and its
+// accumulators per row (ESM_W3_NACC)
+static const int kW3Rows = [] {
+    const char* e = getenv("ESM_W3_ROWS");
+    return e ? atoi(e) : 3;
+}();
+static const int kW3Nacc = [] {
+    const char* e = getenv("ESM_W3_NACC");
+    return e ? atoi(e) : 1;
+}();
+
+template <int RB>
+int launch_w3r(const esm_conv_desc& a, hipStream_t s) {
+    const long long z = static_cast<long long>(a.B) * ((a.Do + 1) / 2);
+    if (z > 65535) return arg_error("conv(wide3r): grid too large");
+    const dim3 grid(ceil_div(a.Wo, 16), ceil_div(a.Ho, RB), static_cast<unsigned>(z));
+    const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
+                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
+                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (kW3Nacc == 2) {
+        if (plain)
+            hipLaunchKernelGGL((wconv3r_kernel<RB, ESM_ACT_GELU, true, 2>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((wconv3r_kernel<RB, -1, false, 2>), grid, dim3(512), 0, s, a);
+    } else {
+        if (plain)
+            hipLaunchKernelGGL((wconv3r_kernel<RB, ESM_ACT_GELU, true, 1>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((wconv3r_kernel<RB, -1, false, 1>), grid, dim3(512), 0, s, a);
+    }
+    return check_launch("conv(wide3r)");
+}
+
 template <int KSW, int NGW, int ZW, int ZS = 4 / KSW>
 int launch_w3(const esm_conv_desc& a, hipStream_t s) {
     constexpr int ZB = ZW * ZS;
@@ -224,7 +390,13 @@ int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
     if (ng > 4) {  // 5..8 groups: 4 waves split K, 2 groups each; more planes per wave on big volumes
         if (vox >= 16LL * 65536) return launch_w3<4, 2, 8>(a, s);
         if (vox >= 4LL * 16384) return launch_w3<4, 2, 4>(a, s);
-        // small volumes (S-K group_stem): 8 waves, one group each, halving each wave's load -> MFMA chain
+        // small volumes (S-K group_stem): 8 waves, one group each, halving each wave's load -> MFMA chain;
+        // <= 8 couts: RB output rows per workgroup streamed through a register ring (ESM_W3_ROWS, 1 = off)
+        if (a.Cout <= 8 && ng <= 8 && kW3Rows > 1) {
+            if (kW3Rows == 2) return launch_w3r<2>(a, s);
+            if (kW3Rows == 3) return launch_w3r<3>(a, s);
+            return launch_w3r<4>(a, s);
+        }
         return kW3Split8 ? launch_w3<8, 1, 2, 1>(a, s) : launch_w3<4, 2, 2>(a, s);
     }
     if (ng > 2) return launch_w3<4, 1, 2>(a, s);  // 3..4 groups: one each
