@@ -184,9 +184,9 @@ __global__ void __launch_bounds__(64 * KSW * ZS) wconv3_kernel(const esm_conv_de
 // output row it loads 12 input operands instead of 36.  Per wave and output row the MFMAs run in the
 // same order as wconv3_kernel<8, 1, 2, ..> (input plane, then tap), and the 8 waves' partial tiles are
 // added in the same fixed order: results are bit-identical to that form.
-template <int RB, int ACT, bool PLAIN, int NACC>
-__global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
-    constexpr int KSW = 8;
+template <int KSW, int RB, int ACT, bool PLAIN>
+__global__ void __launch_bounds__(64 * KSW) wconv3r_kernel(const esm_conv_desc a) {
+    constexpr int NT = 64 * KSW;
     __shared__ __attribute__((aligned(16))) float red[KSW][RB][4][64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -243,13 +243,10 @@ __global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
     };
     load_row(ring[0], 0);
     load_row(ring[1], 1);
-    // NACC = 2: the row's 36 MFMAs alternate between two accumulators (two dependency chains for the
-    // matrix pipe), added at the end; NACC = 1 is the plane-pair form's exact summation order
-    floatx4 acc[RB][NACC];
+    floatx4 acc[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-#pragma unroll
-        for (int k = 0; k < NACC; ++k) acc[r][k] = floatx4{0.f, 0.f, 0.f, 0.f};
+        acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
         load_row(ring[(r + 2) & 3], r + 2);  // output row y0 + r needs input rows r .. r + 2 (ring index)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -257,16 +254,13 @@ __global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    const int t = (p * 3 + dy) * 3 + dx;
-                    acc[r][t % NACC] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[p][dy * 3 + dx], ring[(r + dy) & 3][p][dx],
-                                                                           acc[r][t % NACC], 0, 0, 0);
-                }
+                for (int dx = 0; dx < 3; ++dx)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[p][dy * 3 + dx], ring[(r + dy) & 3][p][dx], acc[r], 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < RB; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[wave][r][j][lane] = NACC == 1 ? acc[r][0][j] : acc[r][0][j] + acc[r][NACC - 1][j];
+        for (int j = 0; j < 4; ++j) red[wave][r][j][lane] = acc[r][j];
     __syncthreads();
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
@@ -274,9 +268,9 @@ __global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
         0x00020000);
     constexpr int NEL = RB * 4 * 64;  // elements (r, j, lane)
 #pragma unroll
-    for (int e = 0; e < (NEL + 511) / 512; ++e) {
-        const int idx = e * 512 + static_cast<int>(threadIdx.x);
-        if (NEL % 512 != 0 && idx >= NEL) break;
+    for (int e = 0; e < (NEL + NT - 1) / NT; ++e) {
+        const int idx = e * NT + static_cast<int>(threadIdx.x);
+        if (NEL % NT != 0 && idx >= NEL) break;
         const int l = idx & 63, j = (idx >> 6) & 3, r = idx >> 8;
         float v = red[0][r][j][l];
 #pragma unroll
@@ -306,18 +300,15 @@ __global__ void __launch_bounds__(512) wconv3r_kernel(const esm_conv_desc a) {
     }
 }
 
-// output rows per workgroup of the row-streaming variant (A/B: ESM_W3_ROWS=1 disables it) and its
-// accumulators per row (ESM_W3_NACC)
+// output rows per workgroup of the row-streaming variant (A/B: ESM_W3_ROWS=1 disables it).  Measured at S-K
+// (scripts/gpu_r03_w3rows.sh, two rotations): RB 1 / 2 / 3 / 4 -> group_stem in the replayed step 13.6 /
+// 13.4 / 10.1 / 11.5-12.2 us.  Neither two accumulators per row nor the same form for the 8 -> 8 `agg`
+// (2 waves) measured faster; both were removed.
 static const int kW3Rows = [] {
     const char* e = getenv("ESM_W3_ROWS");
     return e ? atoi(e) : 3;
 }();
-static const int kW3Nacc = [] {
-    const char* e = getenv("ESM_W3_NACC");
-    return e ? atoi(e) : 1;
-}();
-
-template <int RB>
+template <int KSW, int RB>
 int launch_w3r(const esm_conv_desc& a, hipStream_t s) {
     const long long z = static_cast<long long>(a.B) * ((a.Do + 1) / 2);
     if (z > 65535) return arg_error("conv(wide3r): grid too large");
@@ -325,17 +316,10 @@ int launch_w3r(const esm_conv_desc& a, hipStream_t s) {
     const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
-    if (kW3Nacc == 2) {
-        if (plain)
-            hipLaunchKernelGGL((wconv3r_kernel<RB, ESM_ACT_GELU, true, 2>), grid, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((wconv3r_kernel<RB, -1, false, 2>), grid, dim3(512), 0, s, a);
-    } else {
-        if (plain)
-            hipLaunchKernelGGL((wconv3r_kernel<RB, ESM_ACT_GELU, true, 1>), grid, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((wconv3r_kernel<RB, -1, false, 1>), grid, dim3(512), 0, s, a);
-    }
+    if (plain)
+        hipLaunchKernelGGL((wconv3r_kernel<KSW, RB, ESM_ACT_GELU, true>), grid, dim3(64 * KSW), 0, s, a);
+    else
+        hipLaunchKernelGGL((wconv3r_kernel<KSW, RB, -1, false>), grid, dim3(64 * KSW), 0, s, a);
     return check_launch("conv(wide3r)");
 }
 
@@ -393,9 +377,9 @@ int launch_wide3(const esm_conv_desc& a, hipStream_t s) {
         // small volumes (S-K group_stem): 8 waves, one group each, halving each wave's load -> MFMA chain;
         // <= 8 couts: RB output rows per workgroup streamed through a register ring (ESM_W3_ROWS, 1 = off)
         if (a.Cout <= 8 && ng <= 8 && kW3Rows > 1) {
-            if (kW3Rows == 2) return launch_w3r<2>(a, s);
-            if (kW3Rows == 3) return launch_w3r<3>(a, s);
-            return launch_w3r<4>(a, s);
+            if (kW3Rows == 2) return launch_w3r<8, 2>(a, s);
+            if (kW3Rows == 3) return launch_w3r<8, 3>(a, s);
+            return launch_w3r<8, 4>(a, s);
         }
         return kW3Split8 ? launch_w3<8, 1, 2, 1>(a, s) : launch_w3<4, 2, 2>(a, s);
     }
