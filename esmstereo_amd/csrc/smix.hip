@@ -316,8 +316,8 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int NPX = TH * TW;
     static_assert(AP <= kFThreads, "one t1 pixel per thread");
     static_assert(!CONV || NPX <= 64, "conv2: one pixel per lane");
-    // Weights are never staged: every weight index below is wave-uniform, so they are scalar loads
-    // (the LDS then only carries activations: one read per operand of the depthwise / 3x3 convs)
+    // Every weight is staged in LDS once (below) and read there as a wave-uniform broadcast; the LDS
+    // otherwise carries the activations of the three regions
     __shared__ float s1[C * AH * AWP + SLACK];  // t1 image, then t2 image ([C][BH][BWP])
     __shared__ float s2[C * BP];                // depthwise results: region B, then region C
     __shared__ float s3[CONV ? C * CP : 1];           // t3 on region C
@@ -331,22 +331,18 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     const float* xb = a.x + static_cast<long long>(b) * C * plane;
     FM_STAMP(0);
 
-    // Cache warm-up: every weight is touched by one vector load here, all in flight together with the
-    // t1 pixel loads, so that the scalar loads of the phases below hit L2 instead of each paying a
-    // memory round trip in series (between two graph replays the weights leave L2).  The values land
-    // in an LDS scratch that nothing reads.
+    // Weights: one vector load per weight and thread slot, all in flight together with the t1 pixel loads.
     using Lyt = SmixLayout<C>;
     constexpr int DW0 = 4 * Lyt::STAGE, DW1 = DW0 + C * K * K + C;
     constexpr int CV0 = DW1 + C * K * K + C;
     constexpr int CV2 = CV0 + (CONV ? HID * C * 9 + HID : 0);
     constexpr int NW = CV2 + (CONV ? C * HID + C : 0);
     constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
-    // the depthwise, conv0 and conv2 weights (everything past the four mlp stages) go to LDS: their phases
-    // read them as LDS broadcasts (as scalar loads they were a chain of L2 round trips per phase:
-    // dw0 1.6, dw1 1.5, conv0 3.5 us of the 12.4-us block at S-K, profiles/r03_fmnet_phases.txt)
-    constexpr int NLW = NW - DW0;
-    __shared__ float sw[NLW];
-    __shared__ float wsink[kFThreads];
+    // every weight goes to LDS (the warm-up loads below fetch each one once, all in flight together with
+    // the t1 pixel loads) and every phase reads its weights there as LDS broadcasts: as scalar loads they
+    // were a chain of L2 (or, in the replayed step, memory) round trips per phase -- dw0 1.6, dw1 1.5,
+    // conv0 3.5 us of the 12.4-us block at S-K (profiles/r03_fmnet_phases.txt)
+    __shared__ float sw[NW];
     float rw[NWR];
 #pragma unroll
     for (int k = 0; k < NWR; ++k) {
@@ -372,11 +368,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             p = j < C * HID ? a.conv2_w : a.conv2_b;
             off = j < C * HID ? j : j - C * HID;
         }
-#ifndef ESM_FMNET_NOWARM
         rw[k] = (p ? p : a.x)[p ? off : 0];
-#else
-        rw[k] = 0.f;
-#endif
     }
     const int q = tid;  // this thread's t1 pixel (region A)
     const int aly = q / AW, alx = q - (q / AW) * AW;
@@ -388,25 +380,22 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         const float v = xb[ain ? c * plane + agy * W + agx : 0];
         t1[c] = ain ? v : 0.f;
     }
-    const float* lw_dw0 = sw;                          // [C][K][K], then bias [C]
-    const float* lw_dw1 = sw + (DW1 - DW0);
-    const float* lw_cv0 = sw + (CV0 - DW0);            // conv0_w [HID][C][9], then conv0_b [HID]
-    const float* lw_cv2 = sw + (CV2 - DW0);            // conv2_w [C][HID], then conv2_b [C]
+    const float* lw_dw0 = sw + DW0;                    // [C][K][K], then bias [C]
+    const float* lw_dw1 = sw + DW1;
+    const float* lw_cv0 = sw + CV0;                    // conv0_w [HID][C][9], then conv0_b [HID]
+    const float* lw_cv2 = sw + CV2;                    // conv2_w [C][HID], then conv2_b [C]
+    // the mlp stages: SmixLayout<C> blocks 0..3 at the start of sw (the warm-up's index order)
+#pragma unroll
+    for (int k = 0; k < NWR; ++k) {  // the warm-up values -> LDS weights
+        const int i = tid + k * kFThreads;
+        if (i < NW) sw[i] = rw[k];
+    }
+    __syncthreads();
     // t1 = SMLayer0.mlp1 (x) on region A
     if (q < AP) {
-        if (ain) mix_stage_g<C>(t1, a.stage[0]);
+        if (ain) mix_stage<C>(t1, sw);
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
-    }
-    {  // the warm-up values: LDS weights (after the t1 chain, which does not wait for them)
-        float sink = 0.f;
-#pragma unroll
-        for (int k = 0; k < NWR; ++k) {
-            const int i = tid + k * kFThreads;
-            if (i >= DW0 && i < NW) sw[i - DW0] = rw[k];
-            else sink += rw[k];
-        }
-        wsink[tid] = sink;
     }
     __syncthreads();
     FM_STAMP(1);
@@ -423,8 +412,8 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * BP + p];
         if (in) {
-            mix_stage_g<C>(t, a.stage[1]);
-            mix_stage_g<C>(t, a.stage[2]);
+            mix_stage<C>(t, sw + Lyt::STAGE);
+            mix_stage<C>(t, sw + 2 * Lyt::STAGE);
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
@@ -444,7 +433,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         float t[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
-        mix_stage_g<C>(t, a.stage[3]);
+        mix_stage<C>(t, sw + 3 * Lyt::STAGE);
         const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
@@ -459,7 +448,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
             for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
             if (in) {
-                mix_stage_g<C>(t, a.stage[3]);
+                mix_stage<C>(t, sw + 3 * Lyt::STAGE);
                 const long long pix = static_cast<long long>(y) * W + x;
 #pragma unroll
                 for (int c = 0; c < C; ++c) t[c] += xb[pix + c * plane];
