@@ -159,6 +159,8 @@ def marginal_costs(hp: E.HotPath, rounds: int = 3, window_ms: float = 6.0) -> tu
             lib.esm_plan_set_repeat(plan, i, 1)
         out.append(statistics.median(base) - statistics.median(drop))
         base_all += base
+        if (i + 1) % 8 == 0:  # progress for long steps (configs 3 / 4): a silent minute reads as a hang
+            print(f"marginal costs: {i + 1}/{hp.num_ops} ops", file=sys.stderr, flush=True)
     hp._graph_ready = False
     return out, statistics.median(base_all)
 

@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int NWAVES = kFThreads / 64;
     constexpr int NPX = TH * TW;
     static_assert(AP <= kFThreads, "one t1 pixel per thread");
-    static_assert(!CONV || NPX <= 64, "conv2: one pixel per lane");
+    static_assert(!CONV || (NPX <= 64 && HID % NWAVES == 0), "conv0 / conv2: one pixel per lane");
     // Every weight is staged in LDS once (below) and read there as a wave-uniform broadcast; the LDS
     // otherwise carries the activations of the three regions
     __shared__ float s1[C * AH * AWP + SLACK];  // t1 image, then t2 image ([C][BH][BWP])
@@ -342,7 +342,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     // the t1 pixel loads) and every phase reads its weights there as LDS broadcasts: as scalar loads they
     // were a chain of L2 (or, in the replayed step, memory) round trips per phase -- dw0 1.6, dw1 1.5,
     // conv0 3.5 us of the 12.4-us block at S-K (profiles/r03_fmnet_phases.txt)
-    __shared__ float sw[NW];
+    // LDS weights for C = 8 (S / M): at C = 16 (L) their 32 KB would halve the residency of the 3-row-tile
+    // form (two workgroups per CU on L-K's 96 x 312 maps), so there the weights stay scalar loads
+    constexpr bool LW = C == 8;
+    __shared__ float sw[LW ? NW : 1];
+    __shared__ float wsink[LW ? 1 : kFThreads];
     float rw[NWR];
 #pragma unroll
     for (int k = 0; k < NWR; ++k) {
@@ -384,23 +388,38 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     const float* lw_dw1 = sw + DW1;
     const float* lw_cv0 = sw + CV0;                    // conv0_w [HID][C][9], then conv0_b [HID]
     const float* lw_cv2 = sw + CV2;                    // conv2_w [C][HID], then conv2_b [C]
+    const float* w_dw0 = LW ? lw_dw0 : a.dw_w[0];
+    const float* b_dw0 = LW ? lw_dw0 + C * K * K : a.dw_b[0];
+    const float* w_dw1 = LW ? lw_dw1 : a.dw_w[1];
+    const float* b_dw1 = LW ? lw_dw1 + C * K * K : a.dw_b[1];
+    const float* w_cv2 = LW ? lw_cv2 : a.conv2_w;
+    const float* b_cv2 = LW ? lw_cv2 + C * HID : a.conv2_b;
     // the mlp stages: SmixLayout<C> blocks 0..3 at the start of sw (the warm-up's index order)
 #pragma unroll
     for (int k = 0; k < NWR; ++k) {  // the warm-up values -> LDS weights
         const int i = tid + k * kFThreads;
-        if (i < NW) sw[i] = rw[k];
+        if (LW && i < NW) sw[i] = rw[k];
+    }
+    if constexpr (!LW) {  // scalar weights: the vector loads above only warm L2 for them
+        float sink = 0.f;
+#pragma unroll
+        for (int k = 0; k < NWR; ++k) sink += rw[k];
+        wsink[tid] = sink;
     }
     __syncthreads();
     // t1 = SMLayer0.mlp1 (x) on region A
     if (q < AP) {
-        if (ain) mix_stage<C>(t1, sw);
+        if (ain) {
+            if constexpr (LW) mix_stage<C>(t1, sw);
+            else mix_stage_g<C>(t1, a.stage[0]);
+        }
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
     __syncthreads();
     FM_STAMP(1);
     // dw0 (t1) on region B
-    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, lw_dw0, lw_dw0 + C * K * K, wave, lane);
+    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, w_dw0, b_dw0, wave, lane);
     __syncthreads();
     FM_STAMP(2);
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
@@ -412,8 +431,13 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * BP + p];
         if (in) {
-            mix_stage<C>(t, sw + Lyt::STAGE);
-            mix_stage<C>(t, sw + 2 * Lyt::STAGE);
+            if constexpr (LW) {
+                mix_stage<C>(t, sw + Lyt::STAGE);
+                mix_stage<C>(t, sw + 2 * Lyt::STAGE);
+            } else {
+                mix_stage_g<C>(t, a.stage[1]);
+                mix_stage_g<C>(t, a.stage[2]);
+            }
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) s1[(c * BH + py) * BWP + px] = in ? t[c] : 0.f;
@@ -421,7 +445,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     __syncthreads();
     FM_STAMP(3);
     // dw1 (t2) on region C
-    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, lw_dw1, lw_dw1 + C * K * K, wave, lane);
+    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, w_dw1, b_dw1, wave, lane);
     __syncthreads();
     FM_STAMP(4);
     // t3 = SMLayer1.mlp2 (dw1) + x on region C
@@ -433,7 +457,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         float t[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
-        mix_stage<C>(t, sw + 3 * Lyt::STAGE);
+        if constexpr (LW) mix_stage<C>(t, sw + 3 * Lyt::STAGE); else mix_stage_g<C>(t, a.stage[3]);
         const long long pix = static_cast<long long>(b) * C * plane + static_cast<long long>(y) * W + x;
 #pragma unroll
         for (int c = 0; c < C; ++c) t[c] += a.x[pix + c * plane];
@@ -448,7 +472,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
 #pragma unroll
             for (int c = 0; c < C; ++c) t[c] = s2[c * CP + tid];
             if (in) {
-                mix_stage<C>(t, sw + 3 * Lyt::STAGE);
+                if constexpr (LW) mix_stage<C>(t, sw + 3 * Lyt::STAGE); else mix_stage_g<C>(t, a.stage[3]);
                 const long long pix = static_cast<long long>(y) * W + x;
 #pragma unroll
                 for (int c = 0; c < C; ++c) t[c] += xb[pix + c * plane];
@@ -459,24 +483,48 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
         }
         __syncthreads();
         FM_STAMP(5);
-        // h = silu(conv0(t3) + b0) on the tile: a wave owns HID / 8 hidden channels (scalar weight
-        // loads), a lane one pixel; each t3 value read from LDS feeds all of the wave's channels
-        // h = silu(conv0(t3) + b0) on the tile: one (hidden channel, pixel) output per thread and pass, so
-        // every lane works (a wave owning HID / 8 channels of the tile's 16 pixels left 3/4 of its lanes
-        // idle: 1.6 us of the S-K block); weights as LDS reads, per output the products summed over c, ky,
-        // kx as before
-        for (int e = tid; e < HID * NPX; e += kFThreads) {
-            const int hc = e / NPX, pp = e - (e / NPX) * NPX;
-            const int py = pp / TW, px = pp - (pp / TW) * TW;
-            const float* w0 = lw_cv0 + hc * C * 9;
-            float acc = 0.f;
+        if constexpr (LW) {
+            // h = silu(conv0(t3) + b0) on the tile: one (hidden channel, pixel) output per thread and pass, so
+            // every lane works (a wave owning HID / 8 channels of the tile's 16 pixels left 3/4 of its lanes
+            // idle: 1.6 us of the S-K block); weights as LDS reads, per output the products summed over c, ky,
+            // kx as before
+            for (int e = tid; e < HID * NPX; e += kFThreads) {
+                const int hc = e / NPX, pp = e - (e / NPX) * NPX;
+                const int py = pp / TW, px = pp - (pp / TW) * TW;
+                const float* w0 = lw_cv0 + hc * C * 9;
+                float acc = 0.f;
 #pragma unroll
-            for (int c = 0; c < C; ++c)
+                for (int c = 0; c < C; ++c)
 #pragma unroll
-                for (int ky = 0; ky < 3; ++ky)
+                    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) acc += w0[c * 9 + ky * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
-            sh[hc * NPX + pp] = silu(acc + lw_cv0[HID * C * 9 + hc]);
+                        for (int kx = 0; kx < 3; ++kx) acc += w0[c * 9 + ky * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
+                sh[hc * NPX + pp] = silu(acc + lw_cv0[HID * C * 9 + hc]);
+            }
+        } else {  // C = 16: a wave owns HID / 8 hidden channels (scalar weight loads), a lane one pixel
+            constexpr int HPW = HID / NWAVES;
+            if (lane < NPX) {
+                const int py = lane / TW, px = lane - (lane / TW) * TW;
+                float acc[HPW];
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[j] = 0.f;
+                const float* w0 = a.conv0_w + wave * HPW * C * 9;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                        for (int kx = 0; kx < 3; ++kx) {
+                            const float v = s3[(c * CH + py + ky) * CW + px + kx];
+#pragma unroll
+                            for (int j = 0; j < HPW; ++j) acc[j] += w0[(j * C + c) * 9 + ky * 3 + kx] * v;
+                        }
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) {
+                    const int hc = wave * HPW + j;
+                    sh[hc * NPX + lane] = silu(acc[j] + a.conv0_b[hc]);
+                }
+            }
         }
         __syncthreads();
         FM_STAMP(6);
@@ -487,11 +535,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             if (y < H && x < W) {
 #pragma unroll
                 for (int c = wave; c < C; c += NWAVES) {
-                    const float* w = lw_cv2 + c * HID;
+                    const float* w = w_cv2 + c * HID;
                     float sacc = 0.f;
 #pragma unroll
                     for (int hc = 0; hc < HID; ++hc) sacc += w[hc] * sh[hc * NPX + lane];
-                    const float v = sacc + lw_cv2[C * HID + c] + s3[(c * CH + py + HC) * CW + px + HC];
+                    const float v = sacc + b_cv2[c] + s3[(c * CH + py + HC) * CW + px + HC];
                     a.out[static_cast<long long>(b) * C * plane + c * plane + static_cast<long long>(y) * W + x] = v;
                 }
             }

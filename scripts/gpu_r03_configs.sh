@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for c in 2 3 4; do
+for c in ${CFGS:-2 3 4}; do
   timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c$c.log 2>&1 \
       || { tail -20 gpurun_out/bench_c$c.log; exit 1; }
   python -c "import json;d=json.loads([l for l in open('gpurun_out/bench_c$c.log') if l.startswith('{\"metric')][-1]);r=d['roofline'];print('config $c', d['value'], d['ms_per_step'], r['kernel'], r['avg_us'], r['frac'])"
