@@ -395,26 +395,24 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     const float* w_cv2 = LW ? lw_cv2 : a.conv2_w;
     const float* b_cv2 = LW ? lw_cv2 + C * HID : a.conv2_b;
     // the mlp stages: SmixLayout<C> blocks 0..3 at the start of sw (the warm-up's index order)
+    // t1 = SMLayer0.mlp1 (x) on region A, its weights as scalar loads: the phase then waits for the pixel
+    // loads only, not for the whole weight batch (staging stage 0 in LDS first cost the S-K block 1 us)
+    if (q < AP) {
+        if (ain) mix_stage_g<C>(t1, a.stage[0]);
 #pragma unroll
-    for (int k = 0; k < NWR; ++k) {  // the warm-up values -> LDS weights
-        const int i = tid + k * kFThreads;
-        if (LW && i < NW) sw[i] = rw[k];
+        for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
-    if constexpr (!LW) {  // scalar weights: the vector loads above only warm L2 for them
+    if constexpr (LW) {  // the warm-up values -> LDS weights, read from the next phase on
+#pragma unroll
+        for (int k = 0; k < NWR; ++k) {
+            const int i = tid + k * kFThreads;
+            if (i < NW) sw[i] = rw[k];
+        }
+    } else {  // scalar weights: the vector loads above only warm L2 for them
         float sink = 0.f;
 #pragma unroll
         for (int k = 0; k < NWR; ++k) sink += rw[k];
         wsink[tid] = sink;
-    }
-    __syncthreads();
-    // t1 = SMLayer0.mlp1 (x) on region A
-    if (q < AP) {
-        if (ain) {
-            if constexpr (LW) mix_stage<C>(t1, sw);
-            else mix_stage_g<C>(t1, a.stage[0]);
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) s1[(c * AH + aly) * AWP + alx] = ain ? t1[c] : 0.f;
     }
     __syncthreads();
     FM_STAMP(1);
