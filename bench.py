@@ -4,6 +4,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher (WORLD_SIZE unset) and --gpus N > 1, this process starts the N ranks itself: N
+fresh child processes, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (before any HIP
+call here, and never by re-exec), waits for them and exits non-zero if any rank fails.  Under a
+launcher, --gpus must equal WORLD_SIZE.
+
 A "step" is one pass of the hot path (models/ESMStereo.py:700-745: cost volume -> 3-D stems ->
 3-D hourglass -> regression -> ESM/ShuffleMixer upsampler -> x4) over one batch of synthetic
 matching features already resident in HBM: by default BASELINE.json configs[1], ESMStereo-S
@@ -35,7 +40,9 @@ import argparse
 import json
 import math
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -44,9 +51,18 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import esmstereo_amd as E  # noqa: E402
-from esmstereo_amd import dist as D  # noqa: E402
-from esmstereo_amd._lib import lib  # noqa: E402
+# the package (and its HIP library) is loaded by the rank processes only (_load_package): a parent that
+# launches the ranks itself never touches the GPU
+E = D = lib = None
+
+
+def _load_package() -> None:
+    global E, D, lib
+    import esmstereo_amd
+    from esmstereo_amd import dist
+    from esmstereo_amd._lib import lib as _native
+
+    E, D, lib = esmstereo_amd, dist, _native
 
 VARIANTS = {"S": ("mobilenetv2_100", 16), "M": ("efficientnet_b2", 8), "L": ("efficientnet_b2", 4)}
 METRIC = "stereo pairs/sec at 384×1248 maxdisp=192; EPE vs reference"
@@ -385,7 +401,7 @@ def epe_vs_reference(model, args, dev):
         init = E.regression_topk(cost, None, 2) if m["cv_scale"] == 4 else \
             E.disparity_regression(cost, D).unsqueeze(1)
         disp0 = model.hot_path(ml, mr, att, up)[0]
-        d_ref_init = model.upsample_module.emit(E.engine.Ctx(dev), up, T(g["init_pred"]), final_scale=4.0)[0]
+        d_ref_init = E.engine.eager_emit(dev, model.upsample_module.emit, up, T(g["init_pred"]), final_scale=4.0)[0]
     rep = check_fullsize(name, m, g, cost, init, disp0, disp0_from_ref_init=d_ref_init[:, 0])
     d = rep.get("disp0")
     epe = d["epe_outside_mask"] if d else rep["disp0_sub_epe"]
@@ -439,6 +455,67 @@ def forward_e2e(model, args, dev, iters: int = 10) -> dict:
                     "model.hot_path() call on resident features, host work included"}
 
 
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(argv: list, n: int) -> int:
+    """Start ``n`` rank processes of this script (one per GPU, as torch.distributed.run would) and wait
+    for them.  If one fails the others are stopped (a rank blocked in a collective would never return);
+    returns 0 or the first failing rank's exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    failed = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad and not failed:
+            failed = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        if p.returncode != 0 and not failed:
+            failed = p.returncode
+    return 0 if not failed else (failed if failed > 0 else 1)
+
+
+def standin_cpu(args, world: int, rank: int) -> None:
+    """The multi-rank bench loop (shards, per-step gather, barrier + max-over-ranks time) over gloo on
+    the CPU with a per-pair stand-in for the HIP hot path: the launcher path is exercised without a GPU
+    (tests/test_dist.py).  Rank 0 prints the contract line with the gathered buffer's shape."""
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+    world, rank = D.world_info()
+    if args.global_batch is not None:
+        b, scaling, total = D.local_batch(world, rank, global_batch=args.global_batch)
+    else:
+        b, scaling, total = D.local_batch(world, rank, batch=args.batch)
+    g = torch.Generator().manual_seed(100 + rank)
+    left, right = torch.randn(b, 3, 8, 16, generator=g), torch.randn(b, 3, 8, 16, generator=g)
+    out = torch.empty(b, 8, 16)
+    gather = D.DisparityGather(out)
+
+    def step():
+        out.copy_((left - right).abs().sum(1) * 4)
+        gather(out)
+
+    elapsed = D.timed_steps(step, args.steps, args.warmup, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(total * args.steps / elapsed, 2), "unit": "pairs/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "scaling": scaling,
+                          "standin": "cpu gloo (no GPU work)", "global_batch": total,
+                          "gathered_shape": list(gather.buf.shape)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -464,7 +541,16 @@ def main() -> None:
     ap.add_argument("--kernel-table", default="", help="write the per-op table (json) here")
     ap.add_argument("--streams", type=int, default=2,
                     help="side measurement: independent B-pair instances on this many concurrent streams")
+    ap.add_argument("--cpu-standin", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        if not args.cpu_standin and args.gpus > torch.cuda.device_count():  # device_count: no HIP init here
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if int(env_world or 1) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE {env_world} from the launcher")
+    _load_package()
     cfg = CONFIGS[args.config]
     for k in ("variant", "cv", "height", "width", "maxdisp"):
         if getattr(args, k) is None:
@@ -475,6 +561,9 @@ def main() -> None:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_standin:
+        standin_cpu(args, world, local)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -23,8 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, pack_conv, pack_shuffle_tail, param_token, run_conv, run_pair2,
-                     run_shuffle_conv, run_shuffle_tail, shuffle_conv_supported)
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail, param_token, run_conv,
+                     run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_supported)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -172,7 +172,7 @@ class aggregation(_Hourglass):
         return self._emit(ctx, x, crop1=True, **last)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.emit(Ctx(x.device), x)
+        return eager_emit(x.device, self.emit, x)
 
 
 class up_refinement(_Hourglass):
@@ -189,7 +189,7 @@ class up_refinement(_Hourglass):
         return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, c10=c10, **last)
 
     def forward(self, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor) -> torch.Tensor:
-        return self.emit(Ctx(disp.device), disp, left_f1x, left_f2x)
+        return eager_emit(disp.device, self.emit, disp, left_f1x, left_f2x)
 
 
 # ----------------------------------------------------------------------------- ESM upsampler
@@ -291,7 +291,7 @@ class _ESMUpsampler(nn.Module):
 
     def forward(self, *args: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         *feats, init = args
-        return tuple(self.emit(Ctx(init.device), feats, init))
+        return tuple(eager_emit(init.device, self.emit, feats, init))
 
 
 class upsample4(_ESMUpsampler):

@@ -84,20 +84,23 @@ __global__ void __launch_bounds__(64 * KSW * ZS) wconv3_kernel(const esm_conv_de
             vo[i][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
         }
     }
-    int roff[3];  // rows y - 1 .. y + 1 (kOOB outside)
+    // plane / row offsets are unsigned: two kOOB marks add to 2^31 without signed overflow, and the
+    // sum is cast once at the soffset operand (past the end of the buffer either way)
+    unsigned roff[3];  // rows y - 1 .. y + 1 (kOOB outside)
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
         const int yi = y - 1 + dy;
-        roff[dy] = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
+        roff[dy] = (yi >= 0 && yi < a.Hi) ? 4u * yi * sh : kOOB;
     }
     auto load_plane = [&](float (&d)[NGW][9], int zi) {
-        const int poff = (zi >= 0 && zi < a.Di) ? 4 * zi * sd : static_cast<int>(kOOB);
+        const unsigned poff = (zi >= 0 && zi < a.Di) ? 4u * zi * sd : kOOB;
 #pragma unroll
         for (int i = 0; i < NGW; ++i)
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx) d[i][dy * 3 + dx] = buf_load_s(rs, vo[i][dx], poff + roff[dy]);
+                for (int dx = 0; dx < 3; ++dx)
+                    d[i][dy * 3 + dx] = buf_load_s(rs, vo[i][dx], static_cast<int>(poff + roff[dy]));
     };
 
     floatx4 acc[NA];
@@ -225,21 +228,21 @@ __global__ void __launch_bounds__(64 * KSW) wconv3r_kernel(const esm_conv_desc a
         const int xi = xo - 1 + dx;
         vo[dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * (c * sc + xi) : kOOB;
     }
-    int poff[4];  // input planes z0 - 1 .. z0 + 2 (kOOB outside)
+    unsigned poff[4];  // input planes z0 - 1 .. z0 + 2 (kOOB outside; unsigned as in wconv3_kernel)
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const int zi = z0 - 1 + p;
-        poff[p] = (zi >= 0 && zi < a.Di) ? 4 * zi * sd : static_cast<int>(kOOB);
+        poff[p] = (zi >= 0 && zi < a.Di) ? 4u * zi * sd : kOOB;
     }
     // ring of input rows: row yi = y0 - 1 + k lives in slot k % 4
     float ring[4][4][3];  // [slot][plane][dx]
     auto load_row = [&](float (&d)[4][3], int k) {
         const int yi = y0 - 1 + k;
-        const int ro = (yi >= 0 && yi < a.Hi) ? 4 * yi * sh : static_cast<int>(kOOB);
+        const unsigned ro = (yi >= 0 && yi < a.Hi) ? 4u * yi * sh : kOOB;
 #pragma unroll
         for (int p = 0; p < 4; ++p)
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) d[p][dx] = buf_load_s(rs, vo[dx], poff[p] + ro);
+            for (int dx = 0; dx < 3; ++dx) d[p][dx] = buf_load_s(rs, vo[dx], static_cast<int>(poff[p] + ro));
     };
     load_row(ring[0], 0);
     load_row(ring[1], 1);

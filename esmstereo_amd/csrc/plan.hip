@@ -127,6 +127,60 @@ std::vector<hipGraphNode_t> graph_roots(hipGraph_t g) {
     return v;
 }
 
+// The kernel nodes captured for one op, in launch order: walk back from the capture frontier after
+// the op to the frontier before it (the plan captures on one stream, so the graph is a chain).
+std::vector<hipGraphNode_t> chain_between(const std::vector<hipGraphNode_t>& before,
+                                          const std::vector<hipGraphNode_t>& after) {
+    std::vector<hipGraphNode_t> out;
+    if (after.size() != 1) return out;
+    hipGraphNode_t nd = after[0];
+    for (;;) {
+        bool stop = false;
+        for (auto b : before) stop = stop || (b == nd);
+        if (stop) break;
+        out.push_back(nd);
+        size_t n = 0;
+        if (hipGraphNodeGetDependencies(nd, nullptr, &n) != hipSuccess || n != 1) break;
+        hipGraphNodeGetDependencies(nd, &nd, &n);
+    }
+    return std::vector<hipGraphNode_t>(out.rbegin(), out.rend());
+}
+
+// Every pointer field of an op that lies in one of the ranges [lo, hi) moves by that range's delta
+// (the first range holding the ORIGINAL value: each field is looked at once, so swapped or chained
+// bindings never move a pointer twice); returns how many moved.
+struct Rebase {
+    struct Range {
+        uintptr_t lo, hi;
+        intptr_t delta;
+    };
+    std::vector<Range> r;
+    template <class T>
+    int operator()(T*& p) const {
+        const uintptr_t v = reinterpret_cast<uintptr_t>(p);
+        if (!p) return 0;
+        for (const Range& g : r) {
+            if (v >= g.lo && v < g.hi) {
+                p = reinterpret_cast<T*>(v + g.delta);
+                return 1;
+            }
+        }
+        return 0;
+    }
+    int conv(esm_conv_desc& d) const {
+        int n = 0;
+        for (int i = 0; i < d.nsrc && i < ESM_MAX_SRC; ++i) n += (*this)(d.src[i].ptr);
+        n += (*this)(d.w) + (*this)(d.scale) + (*this)(d.shift) + (*this)(d.mul) + (*this)(d.res);
+        return n + (*this)(d.out) + (*this)(d.up) + (*this)(d.out2);
+    }
+    int stage(esm_smix_stage& t) const {
+        return (*this)(t.ln_w) + (*this)(t.fc0_w) + (*this)(t.fc0_b) + (*this)(t.fc2_w) + (*this)(t.fc2_b);
+    }
+    int tail(esm_shuffle_tail_desc& t) const {
+        return (*this)(t.x) + (*this)(t.up_w) + (*this)(t.up_b) + (*this)(t.tail_w) + (*this)(t.tail_b) + (*this)(t.out);
+    }
+};
+
 }  // namespace
 
 struct esm_plan {
@@ -140,6 +194,11 @@ struct esm_plan {
     std::vector<hipEvent_t> ev0, ev1;
     long long issued = 0, consumed = 0;
     hipGraphNode_t node0 = nullptr, node1 = nullptr;
+    // per op: its kernel nodes in the captured graph (esm_plan_rebind updates them in place)
+    std::vector<std::vector<hipGraphNode_t>> op_nodes;
+    // recorded after every graph launch: a rebind waits on it before touching the instantiated graph
+    hipEvent_t last_launch = nullptr;
+    bool launched = false;
 
     void clear_graph() {
         if (exec) hipGraphExecDestroy(exec);
@@ -147,6 +206,7 @@ struct esm_plan {
         exec = nullptr;
         graph = nullptr;
         node0 = node1 = nullptr;
+        op_nodes.clear();
     }
     void clear_probe() {
         for (auto e : ev0) hipEventDestroy(e);
@@ -160,7 +220,75 @@ struct esm_plan {
     ~esm_plan() {
         clear_graph();
         clear_probe();
+        if (last_launch) hipEventDestroy(last_launch);
         if (cap_stream) hipStreamDestroy(cap_stream);
+    }
+    int patch(int i, const Rebase& rb) {
+        Op& op = ops[i];
+        switch (op.kind) {
+            case kConv: return rb.conv(op.conv);
+            case kPair2: return rb.conv(op.conv) + rb.conv(op.conv2);
+            case kSmix: {
+                int n = rb(op.smix.x) + rb(op.smix.out) + rb(op.smix.res) + rb(op.smix.dw_w) + rb(op.smix.dw_b);
+                for (int k = 0; k < op.smix.nstages && k < ESM_SMIX_MAX_STAGES; ++k) n += rb.stage(op.smix.stage[k]);
+                return n;
+            }
+            case kFmnet: {
+                int n = rb(op.fm.x) + rb(op.fm.out);
+                for (int k = 0; k < 2; ++k) n += rb(op.fm.dw_w[k]) + rb(op.fm.dw_b[k]);
+                for (int k = 0; k < 4; ++k) n += rb.stage(op.fm.stage[k]);
+                return n + rb(op.fm.conv0_w) + rb(op.fm.conv0_b) + rb(op.fm.conv2_w) + rb(op.fm.conv2_b);
+            }
+            case kShuffleTail: return rb.tail(op.st);
+            case kShuffleConv:
+                return rb.tail(op.sc.st) + rb(op.sc.w) + rb(op.sc.scale) + rb(op.sc.shift) + rb(op.sc.out);
+            case kConf: {
+                int n = rb(op.cf.out);
+                for (int k = 0; k < 4; ++k) n += rb(op.cf.x[k]);
+                return n;
+            }
+            case kGwc:
+            case kConcat:
+            case kNormcorr:
+                return rb(op.vol.L) + rb(op.vol.R) + rb(op.vol.att) + rb(op.vol.V) + rb(op.vol.work);
+            case kRegression: return rb(op.reg.cost) + rb(op.reg.out);
+            default: return 0;
+        }
+    }
+    // Re-capture op i alone and copy its kernel parameters into the instantiated graph's nodes of
+    // that op.  False when the op's node structure changed (e.g. a source moved out of the window the
+    // register-weight forms need, so the launcher picks another kernel): the caller rebuilds.
+    bool refresh_op_nodes(int i) {
+        if (i >= static_cast<int>(op_nodes.size())) return false;
+        const std::vector<hipGraphNode_t>& nodes = op_nodes[i];
+        if (nodes.empty()) return ops[i].repeat == 0;
+        if (hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+        int rc = ESM_OK;
+        for (int r = 0; r < ops[i].repeat && rc == ESM_OK; ++r) rc = run_op(ops[i], cap_stream);
+        hipGraph_t tg = nullptr;
+        const hipError_t ec = hipStreamEndCapture(cap_stream, &tg);
+        bool ok = rc == ESM_OK && ec == hipSuccess && tg;
+        std::vector<hipGraphNode_t> tn;
+        if (ok) {  // the temporary graph is a chain: roots, then successors
+            std::vector<hipGraphNode_t> cur = graph_roots(tg);
+            while (cur.size() == 1) {
+                tn.push_back(cur[0]);
+                cur = successors(cur);
+            }
+            ok = cur.empty() && tn.size() == nodes.size();
+        }
+        for (size_t k = 0; ok && k < tn.size(); ++k) {
+            hipGraphNodeType ta, tb;
+            ok = hipGraphNodeGetType(tn[k], &ta) == hipSuccess && hipGraphNodeGetType(nodes[k], &tb) == hipSuccess &&
+                 ta == hipGraphNodeTypeKernel && tb == hipGraphNodeTypeKernel;
+            hipKernelNodeParams p{}, q{};
+            ok = ok && hipGraphKernelNodeGetParams(tn[k], &p) == hipSuccess &&
+                 hipGraphKernelNodeGetParams(nodes[k], &q) == hipSuccess && p.func == q.func;
+            ok = ok && hipGraphExecKernelNodeSetParams(exec, nodes[k], &p) == hipSuccess;
+        }
+        if (tg) hipGraphDestroy(tg);
+        (void)hipGetLastError();
+        return ok;
     }
     // Launch every op on s; when `slot` >= 0 record the probe pair `slot` around the probed op.
     // Under stream capture the records become event-record graph nodes (hipEventRecordExternal).
@@ -377,11 +505,13 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
     // Capture the launch list; around the probed op remember the capture frontier so the
     // event-record nodes can be spliced in after capture (records inside capture are refused).
     std::vector<hipGraphNode_t> before, after;
+    std::vector<std::vector<hipGraphNode_t>> frontiers;  // capture frontier after each op
     int rc = ESM_OK;
     for (int i = 0; i < static_cast<int>(plan->ops.size()) && rc == ESM_OK; ++i) {
         if (i == plan->probe_index) before = capture_frontier(plan->cap_stream);
         for (int r = 0; r < plan->ops[i].repeat && rc == ESM_OK; ++r) rc = run_op(plan->ops[i], plan->cap_stream);
-        if (i == plan->probe_index) after = capture_frontier(plan->cap_stream);
+        frontiers.push_back(capture_frontier(plan->cap_stream));
+        if (i == plan->probe_index) after = frontiers.back();
     }
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(plan->cap_stream, &g);
@@ -394,6 +524,9 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
         return ESM_ERR_RUNTIME;
     }
     plan->graph = g;
+    plan->op_nodes.resize(frontiers.size());
+    for (size_t i = 0; i < frontiers.size(); ++i)
+        plan->op_nodes[i] = chain_between(i ? frontiers[i - 1] : std::vector<hipGraphNode_t>{}, frontiers[i]);
     if (plan->probe_index >= 0) {
         if (after.empty()) {
             plan->clear_graph();
@@ -422,7 +555,11 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
 }
 
 int esm_plan_graph_launch(esm_plan* plan, void* stream) {
-    if (!plan || !plan->exec) return esm::arg_error("plan: graph not built");
+    if (!plan) return esm::arg_error("plan: null");
+    if (!plan->exec) {  // never built, or dropped by a hint / repeat / probe change or a rebind
+        const int rc = esm_plan_graph_build(plan, stream);
+        if (rc != ESM_OK) return rc;
+    }
     const int slot = next_slot(plan);
     if (slot >= 0) {
         if (hipGraphExecEventRecordNodeSetEvent(plan->exec, plan->node0, plan->ev0[slot]) != hipSuccess ||
@@ -436,7 +573,49 @@ int esm_plan_graph_launch(esm_plan* plan, void* stream) {
         esm::set_error(std::string("plan: hipGraphLaunch failed: ") + hipGetErrorString(e));
         return ESM_ERR_LAUNCH;
     }
+    if (!plan->last_launch && hipEventCreateWithFlags(&plan->last_launch, hipEventDisableTiming) != hipSuccess) {
+        esm::set_error("plan: hipEventCreate failed");
+        return ESM_ERR_RUNTIME;
+    }
+    if (hipEventRecord(plan->last_launch, esm::as_stream(stream)) != hipSuccess) {
+        esm::set_error("plan: hipEventRecord failed");
+        return ESM_ERR_RUNTIME;
+    }
+    plan->launched = true;
     return ESM_OK;
+}
+
+int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const uint64_t* bytes,
+                    const void* const* new_base) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (n < 0 || (n > 0 && (!old_base || !bytes || !new_base))) return esm::arg_error("plan: bad rebind arrays");
+    Rebase rb;
+    for (int k = 0; k < n; ++k) {
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(old_base[k]);
+        if (!old_base[k] || !new_base[k]) return esm::arg_error("plan: rebind of a null buffer");
+        rb.r.push_back({lo, lo + bytes[k], reinterpret_cast<intptr_t>(new_base[k]) - static_cast<intptr_t>(lo)});
+    }
+    std::vector<char> dirty(plan->ops.size(), 0);
+    int moved = 0;
+    for (size_t i = 0; i < plan->ops.size(); ++i) {
+        const int m = plan->patch(static_cast<int>(i), rb);
+        moved += m;
+        dirty[i] = m > 0;
+    }
+    if (!plan->exec || !moved) return moved;
+    // the instantiated graph's kernel arguments are about to change: the previous replay must have
+    // finished reading them
+    if (plan->launched && hipEventSynchronize(plan->last_launch) != hipSuccess) {
+        esm::set_error("plan: hipEventSynchronize failed");
+        return ESM_ERR_RUNTIME;
+    }
+    for (size_t i = 0; i < dirty.size(); ++i) {
+        if (dirty[i] && !plan->refresh_op_nodes(static_cast<int>(i))) {
+            plan->clear_graph();  // rebuilt by the next esm_plan_graph_launch
+            break;
+        }
+    }
+    return moved;
 }
 
 int esm_plan_set_probe(esm_plan* plan, int index, int ring) {

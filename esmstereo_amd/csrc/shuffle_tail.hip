@@ -219,6 +219,177 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// nf = 8, r = 4 (ESMStereo-S, both heads; the 4x head is the S-K step's largest launch): a workgroup of
+// L waves owns L low-resolution rows x 16 low-resolution pixels = a (4L) x 64 output tile.  Wave w
+// builds the shuffled map of low-res row w with MFMA (M = the 16 sub-pixels (sy, sx) of one channel,
+// N = the 16 low-res pixels, K = the 8 input channels): lane (g, n) receives sub-row g, sub-columns
+// 0..3 of pixel n, SiLU'd and stored to LDS as one 16-byte write.  Only the one-pixel ring the 3x3 tail
+// needs around the tile (the sub-row above / below, the sub-column left / right) is computed on top,
+// on the VALU: 2 (4L + 2) + 2 * 64 values per channel, against the (L + 2) x 18 low-res window's 1.6-1.9x
+// of the previous form.  The tail then runs with lane (g, n) of wave w producing the 4 outputs it built
+// (row 4w + g, columns 4n .. 4n + 3), reading each (channel, tap row) as one 16-byte + two 4-byte LDS
+// reads, and stores them with one 16-byte write-through store.
+template <int L>
+struct St4Geo {
+    static constexpr int NF = 8, R = 4;
+    static constexpr int TR = 4 * L, TC = 64;           // output tile
+    static constexpr int SR = TR + 2, SC = 72;          // shuffled tile: row 0 = Y0 - 1, col 4 = X0 (cols 3..68 used)
+    static constexpr int LH = L + 2, LW = 18;           // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
+    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, WN = OW_TB + 1;
+    static constexpr int XN = NF * LH * LW;
+    static constexpr int HALO = 2 * SC - 2 * 3 /* cols 3..68 on the two ring rows */ + 2 * TR;
+};
+
+template <int L>
+__global__ void __launch_bounds__(64 * L) shuffle_tail4_kernel(const esm_shuffle_tail_desc a) {
+    using G = St4Geo<L>;
+    constexpr int NF = G::NF, SR = G::SR, SC = G::SC, LH = G::LH, LW = G::LW, WN = G::WN, XN = G::XN, NT = 64 * L;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ float lr[NF][LH][LW];
+    __shared__ __attribute__((aligned(16))) float sh[NF][SR][SC];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, HO = 4 * H, WO = 4 * W;
+    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
+    const int b = bk_.z;
+    const int ly0 = bk_.y * L, lx0 = bk_.x * 16;  // first low-res row / pixel of the tile
+    const int Y0 = 4 * ly0, X0 = 4 * lx0;
+    const float* xb = a.x + b * a.xb;
+
+    // ---- stage (one round trip): every weight and the low-res window
+    constexpr int WRN = (WN + NT - 1) / NT, XRN = (XN + NT - 1) / NT;
+    float rw[WRN], rx[XRN];
+#pragma unroll
+    for (int k = 0; k < WRN; ++k) {
+        const int i = tid + k * NT;
+        const float* p = i < G::OW_UB ? a.up_w : i < G::OW_TW ? a.up_b : i < G::OW_TB ? a.tail_w : a.tail_b;
+        const int off = i < G::OW_UB ? i : i < G::OW_TW ? i - G::OW_UB : i < G::OW_TB ? i - G::OW_TW : 0;
+        const bool ok = i < WN && p != nullptr;
+        const float v = (ok ? p : a.up_w)[ok ? off : 0];
+        rw[k] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < XRN; ++k) {
+        const int i = tid + k * NT;
+        const int c = i / (LH * LW), rem = i - c * (LH * LW);
+        const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
+        const bool ok = i < XN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+        rx[k] = ok ? v : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
+#pragma unroll
+    for (int k = 0; k < WRN; ++k)
+        if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
+#pragma unroll
+    for (int k = 0; k < XRN; ++k)
+        if (tid + k * NT < XN) (&lr[0][0][0])[tid + k * NT] = rx[k];
+    __syncthreads();
+
+    // ---- interior: wave w = low-res row ly0 + w, 8 channels x 2 MFMA k-steps
+    {
+        const int Y = Y0 + 4 * wave + g;  // lane's output row
+        const int Xl = X0 + 4 * n;        // lane's first output column
+        float bk[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) bk[kk] = lr[4 * kk + g][wave + 1][n + 1];
+#pragma unroll
+        for (int c = 0; c < NF; ++c) {
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wsh[(c * 16 + n) * NF + 4 * kk + g], bk[kk], acc, 0, 0, 0);
+            conv::floatx4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
+                o[j] = (Y < HO && Xl + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+            }
+            *reinterpret_cast<conv::floatx4*>(&sh[c][1 + 4 * wave + g][4 + 4 * n]) = o;
+        }
+    }
+    // ---- the ring (VALU): ring rows 0 and SR - 1 over cols 3..68, ring cols 3 and 68 over rows 1..TR
+    constexpr int RROW = SC - 6;  // 66 columns per ring row
+    constexpr int NRING = 2 * RROW + 2 * G::TR;
+    for (int i = tid; i < NF * NRING; i += NT) {
+        const int c = i / NRING, q = i - c * NRING;
+        int tr, tc;
+        if (q < 2 * RROW) {
+            tr = q < RROW ? 0 : SR - 1;
+            tc = 3 + (q < RROW ? q : q - RROW);
+        } else {
+            const int e = q - 2 * RROW;
+            tr = 1 + (e < G::TR ? e : e - G::TR);
+            tc = e < G::TR ? 3 : 68;
+        }
+        const int Y = Y0 - 1 + tr, X = X0 - 4 + tc;
+        float v = 0.f;
+        if (Y >= 0 && Y < HO && X >= 0 && X < WO) {
+            const int py = (Y >> 2) - (ly0 - 1), px = (X >> 2) - (lx0 - 1);  // in the low-res window
+            const int m = c * 16 + (Y & 3) * 4 + (X & 3);
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < NF; ++k) acc += wsh[m * NF + k] * lr[k][py][px];
+            v = silu_fast(acc + wsh[G::OW_UB + m]);
+        }
+        sh[c][tr][tc] = v;
+    }
+    __syncthreads();
+
+    // ---- 3x3 tail: lane (g, n) of wave w -> output row 4w + g, columns 4n .. 4n + 3
+    const int oy = Y0 + 4 * wave + g, ox = X0 + 4 * n;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int c = 0; c < NF; ++c) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const float* row = &sh[c][4 * wave + g + ky][0];
+            float v[6];
+            v[0] = row[3 + 4 * n];
+            const conv::floatx4 mid4 = *reinterpret_cast<const conv::floatx4*>(row + 4 + 4 * n);
+            v[1] = mid4[0];
+            v[2] = mid4[1];
+            v[3] = mid4[2];
+            v[4] = mid4[3];
+            v[5] = row[8 + 4 * n];
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+            }
+        }
+    }
+    const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
+    if (oy >= HO) return;
+    const int vo = static_cast<int>(4 * (static_cast<long long>(oy) * a.oh + ox));
+    const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(a.out + b * a.ob, static_cast<short>(0),
+                                                                         0x7fffffff, 0x00020000);
+    if (ox + 3 < WO && ((reinterpret_cast<uintptr_t>(a.out + b * a.ob) + vo) & 15) == 0) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(acc[0] + tb), __float_as_uint(acc[1] + tb), __float_as_uint(acc[2] + tb),
+                  __float_as_uint(acc[3] + tb)},
+            rso, vo, 0, conv::kStoreAux);
+    } else {
+        float* o = a.out + b * a.ob + static_cast<long long>(oy) * a.oh + ox;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (ox + j < WO) o[j] = acc[j] + tb;
+    }
+}
+
+template <int L>
+int launch_tile4(const esm_shuffle_tail_desc& a, hipStream_t s) {
+    const dim3 grid(ceil_div(a.W, 16), ceil_div(a.H, L), a.B);
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_tail: grid too large");
+    hipLaunchKernelGGL((shuffle_tail4_kernel<L>), grid, dim3(64 * L), 0, s, a);
+    return check_launch("shuffle_tail");
+}
+
 template <int NF, int R, int TH, int TW>
 int launch_tile(const esm_shuffle_tail_desc& a, hipStream_t s) {
     dim3 grid(ceil_div(static_cast<long long>(a.W) * R, TW), ceil_div(static_cast<long long>(a.H) * R, TH), a.B);
@@ -237,6 +408,11 @@ int launch_nr(const esm_shuffle_tail_desc& a, hipStream_t s) {
     // nf = 8, r = 4 (ESMStereo-S 4x head): 16 x 32 tiles measured faster than 16 x 64 (15.1 vs 16.5 us
     // at 384x1248, 8 x 64: 16.8, 8 x 32: 18.1; in the S-K launch sequence)
     if constexpr (NF == 8 && R == 4) {
+        // flags bits 1-2 (esm_shuffle_tail_desc): 0 automatic (the 4-row form), 1 the window form below,
+        // 2 / 3 the row form with 4 / 8 low-res rows per workgroup
+        const int form = (a.flags >> 1) & 3;
+        if (form == 3) return launch_tile4<8>(a, s);
+        if (form != 1) return launch_tile4<4>(a, s);
         if (big >= 256) return launch_tile<NF, R, 16, 32>(a, s);
     }
     // nf = 16 (ESMStereo-L heads): 8 x 32 tiles (4x head at 384x1248: 38.9 vs 48.2 us for 8 x 64;

@@ -33,9 +33,18 @@ def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+# Dry emission (Ctx(dry=True)): the launch list is walked with shape-only ``meta`` tensors, nothing is
+# submitted and no device memory is touched.  It sizes a plan's arena before the real emission and
+# lets CPU tests read every op's algorithmic cost (ctx.meta).  While one is active, meta tensors pass
+# the device checks below; they can never reach a kernel, because a dry Ctx submits nothing.
+_DRY_DEPTH = 0
+
+
 def require_device(t: torch.Tensor, what: str) -> None:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{what}: expected a torch.Tensor")
+    if _DRY_DEPTH and t.device.type == "meta":
+        return
     if t.device.type != "cuda":
         raise RuntimeError(f"{what}: esmstereo_amd runs on ROCm devices only (got a {t.device.type} tensor); "
                            "there is no CPU path")
@@ -48,6 +57,8 @@ def require_device(t: torch.Tensor, what: str) -> None:
 def require_on(dev: torch.device, what: str, *ts: Optional[torch.Tensor]) -> None:
     """Every pointer a kernel dereferences must live on the launch device (a host or
     other-device pointer would fault the GPU, so this is checked on the host first)."""
+    if _DRY_DEPTH:  # a dry emission submits nothing (its buffers are shape-only)
+        return
     for t in ts:
         if t is None:
             continue
@@ -169,21 +180,48 @@ def _spans(*ts) -> List[Tuple[int, int]]:
 
 
 class Ctx:
-    """Where ops go: launched now (``plan=False``) or appended to a native plan."""
+    """Where ops go: launched now (``plan=False``), appended to a native plan (``plan=True``), or
+    only recorded (``dry=True``: shape-only ``meta`` buffers, nothing submitted; use as a context
+    manager, ``with Ctx(dev, dry=True) as ctx: ...``)."""
 
-    def __init__(self, device: torch.device, plan: bool = False):
+    def __init__(self, device: torch.device, plan: bool = False, dry: bool = False, arena: int = 0):
+        """``arena`` (eager contexts): carve every buffer out of one chunk of that many bytes (the
+        ``arena_bytes`` of a dry emission of the same calls: ``eager_emit``)."""
         self.device = torch.device(device)
-        self.plan = lib.esm_plan_create() if plan else None
-        if plan and not self.plan:
+        self.dry = bool(dry)
+        self.plan = lib.esm_plan_create() if plan and not dry else None
+        if plan and not dry and not self.plan:
             raise RuntimeError("esm_plan_create failed")
         self.keep: List[object] = []  # tensors (and ctypes descs) that must outlive the plan
         # one entry per launch-list op: name, kernel family, algorithmic flops / HBM bytes
         self.meta: List[dict] = []
-        self.stream = None if plan else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self.stream = None if (plan or dry) else ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         self._arena: Optional[torch.Tensor] = None
         self._arena_off = 0
         self.arena_bytes = 0   # bytes carved out of the arena (256-B granules)
         self.arena_chunks = 0
+        self.num_ops = 0       # ops submitted (or, dry, recorded)
+        if arena and not plan and not dry:
+            self.ARENA_FIRST = int(arena)
+            self._eager_arena = True
+
+    def __enter__(self) -> "Ctx":
+        global _DRY_DEPTH
+        if self.dry:
+            _DRY_DEPTH += 1
+        return self
+
+    def __exit__(self, *exc) -> None:
+        global _DRY_DEPTH
+        if self.dry:
+            _DRY_DEPTH -= 1
+
+    def _submit(self) -> bool:
+        """Count one op; True when it is to be handed to the library (not a dry emission)."""
+        self.num_ops += 1
+        if self.dry and not _DRY_DEPTH:
+            raise RuntimeError("a dry Ctx must be used as a context manager")
+        return not self.dry
 
     def launch(self, graph: bool = True, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Run a plan context's launch list (as a hipGraph by default) on the current stream."""
@@ -218,7 +256,11 @@ class Ctx:
         buffers of one launch list sit close together: kernels that address several sources through
         one buffer descriptor (the wide form over a channel concat) need them inside one 1 GiB window
         (``_check_window``).  Chunks start at 16 MiB and double, so small plans stay small."""
-        if not self.plan:
+        if self.dry:  # the plan's arena accounting, with shape-only buffers
+            n = math.prod(shape)
+            self.arena_bytes += (4 * n + 255) // 256 * 256
+            return torch.empty(shape, device="meta", dtype=torch.float32)
+        if not self.plan and not getattr(self, "_eager_arena", False):
             return torch.empty(shape, device=self.device, dtype=torch.float32)
         n = math.prod(shape)
         nb = (4 * n + 255) // 256 * 256
@@ -240,7 +282,7 @@ class Ctx:
         ones the plan allocates from the front) that they are concatenated with."""
         n = math.prod(shape)
         nb = (4 * n + 255) // 256 * 256
-        if not self.plan or self._arena is None or self._arena_off + nb > self._tail_lo():
+        if self.dry or not self.plan or self._arena is None or self._arena_off + nb > self._tail_lo():
             return self.empty(*shape)
         self._tail = self._tail_lo() - nb
         self.arena_bytes += nb
@@ -257,7 +299,7 @@ class Ctx:
         """Warn (once per process) when a channel concat's sources span >= 1 GiB: the register-weight
         forms then cannot address them through one descriptor and the launch silently takes a slower
         form (conv_direct.h source_window)."""
-        if len(srcs) < 2 or Ctx._window_warned or getattr(self, "sizing", False):
+        if len(srcs) < 2 or Ctx._window_warned or self.dry:
             return
         lo = min(t.data_ptr() for t in srcs)
         hi = max(t.data_ptr() + 4 * (1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()))) for t in srcs)
@@ -267,42 +309,59 @@ class Ctx:
             warnings.warn(f"{tag}: concat sources span {(hi - lo) >> 20} MiB (>= 1 GiB); the wide conv forms fall "
                           "back to slower ones for this launch", RuntimeWarning, stacklevel=3)
 
+    def eager_arena_release(self) -> None:
+        """Forget the eager arena (the buffers handed out stay valid while referenced)."""
+        self._arena = None
+        self.keep.clear()
+
     def hold(self, *objs) -> None:
         if self.plan:
             self.keep.extend(o for o in objs if o is not None)
 
     # --- op submission
     def conv(self, d: EsmConvDesc) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_conv(self.plan, ctypes.byref(d)), "plan_add_conv")
         else:
             check(lib.esm_conv_f32(ctypes.byref(d), self.stream), "conv")
 
     def smix(self, d: EsmSmixDesc) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_smix(self.plan, ctypes.byref(d)), "plan_add_smix")
         else:
             check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
 
     def fmnet(self, d) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_fmnet(self.plan, ctypes.byref(d)), "plan_add_fmnet")
         else:
             check(lib.esm_fmnet_f32(ctypes.byref(d), self.stream), "fmnet")
 
     def shuffle_tail(self, d: EsmShuffleTailDesc) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
         else:
             check(lib.esm_shuffle_tail_f32(ctypes.byref(d), self.stream), "shuffle_tail")
 
     def pair2(self, a: EsmConvDesc, b: EsmConvDesc) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_conv_pair2(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair2")
         else:
             check(lib.esm_conv_pair2_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair2")
 
     def shuffle_conv(self, d: EsmShuffleConvDesc) -> None:
+        if not self._submit():
+            return
         if self.plan:
             check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv")
         else:
@@ -313,6 +372,8 @@ class Ctx:
                               bytes=4 * B * (2 * C * H * W + G * D * H * W + (G * H * W if att is not None else 0)),
                               reads=_spans(L, R, att), writes=_spans(V)))
         a = att.data_ptr() if att is not None else None
+        if not self._submit():
+            return
         if self.plan:
             self.hold(L, R, att, V)
             check(lib.esm_plan_add_gwc(self.plan, L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G), "gwc")
@@ -323,6 +384,8 @@ class Ctx:
     def concat(self, L, R, V, B, C, H, W, D) -> None:
         self.meta.append(dict(name="concat_volume", kind="concat", flops=0,
                               bytes=4 * B * (2 * C * H * W + 2 * C * D * H * W), reads=_spans(L, R), writes=_spans(V)))
+        if not self._submit():
+            return
         if self.plan:
             self.hold(L, R, V)
             check(lib.esm_plan_add_concat(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D), "concat")
@@ -333,6 +396,8 @@ class Ctx:
     def normcorr(self, L, R, V, work, B, C, H, W, D) -> None:
         self.meta.append(dict(name="normcorr_volume", kind="normcorr", flops=2 * B * C * D * H * W,
                               bytes=4 * B * (2 * C * H * W + D * H * W), reads=_spans(L, R), writes=_spans(V, work)))
+        if not self._submit():
+            return
         if self.plan:
             self.hold(L, R, V, work)
             check(lib.esm_plan_add_normcorr(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C,
@@ -354,6 +419,8 @@ class Ctx:
         d.out = out.data_ptr()
         nbytes = 4 * (sum(t.numel() for t in xs if t is not None) + out.numel())
         self.meta.append(dict(name=name, kind="conf", flops=0, bytes=nbytes, reads=_spans(*xs), writes=_spans(out)))
+        if not self._submit():
+            return
         if self.plan:
             self.hold(*xs, out)
             check(lib.esm_plan_add_conf(self.plan, ctypes.byref(d)), name)
@@ -365,6 +432,8 @@ class Ctx:
         name = "disparity_regression" if kind == 0 else f"regression_topk{k}"
         self.meta.append(dict(name=name, kind="regression", flops=2 * B * D * H * W, bytes=4 * B * (D + 1) * H * W,
                               reads=_spans(cost, samples), writes=_spans(out)))
+        if not self._submit():
+            return
         if self.plan:
             if samples is not None or (kind and k != 2):
                 raise ValueError("plan regression: disparity_regression or regression_topk(k=2) over arange(D)")
@@ -377,6 +446,24 @@ class Ctx:
             s = samples.data_ptr() if samples is not None else None
             check(lib.esm_topk_regression_f32(cost.data_ptr(), s, out.data_ptr(), B, D, H, W, int(k), self.stream),
                   "regression_topk")
+
+
+def eager_emit(device: torch.device, fn, *args, **kw):
+    """Run ``fn(ctx, *args, **kw)`` (a module's ``emit``) eagerly, with every buffer it allocates carved
+    out of ONE arena chunk sized by a dry emission of the same call: the channel-concat sources of the
+    multi-launch modules (the hourglasses, the upsamplers) then sit inside one buffer window and every
+    launch keeps its register-weight form, as in the compiled plan (conv_direct.h source_window).  The
+    returned tensors are copied out of the arena, which is released with the intermediates."""
+    with Ctx(device, dry=True) as dry:
+        fn(dry, *args, **kw)
+    ctx = Ctx(device, arena=dry.arena_bytes + 256)
+    out = fn(ctx, *args, **kw)
+    if isinstance(out, (list, tuple)):
+        out = type(out)(o.clone() for o in out)
+    else:
+        out = out.clone()
+    ctx.eager_arena_release()
+    return out
 
 
 # ----------------------------------------------------------------------------- ops
@@ -544,8 +631,9 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         macs = B * Do * Ho * Wo * pc.cin * pc.cout * taps
     in_bytes = 4 * B * cin * Di * Hi * Wi
     out_bytes = 4 * B * pc.cout * Do * Ho * Wo * (2 if out2 is not None else 1)
-    extra = 4 * (res.numel() if res is not None else 0) + 4 * (mul.numel() if mul is not None else 0)
-    meta = dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + 4 * pc.w.numel(),
+    extra = 4 * sum(t.numel() for t in (res, mul, up) if t is not None)
+    w_bytes = 4 * pc.cin * pc.cout * taps  # the layer's weights (the packed slab's padding is not algorithmic)
+    meta = dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + w_bytes,
                 shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
                       f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
                 reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint)
@@ -732,9 +820,10 @@ def pack_shuffle_tail(up: torch.nn.Conv2d, tail: torch.nn.Conv2d, r: int) -> Pac
 
 
 def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optional[torch.Tensor] = None,
-                     tag: str = "shuffle_tail") -> torch.Tensor:
+                     tag: str = "shuffle_tail", form: int = 0) -> torch.Tensor:
     """``tail(SiLU(PixelShuffle(r)(up(x))))`` as one launch (``esm_shuffle_tail_f32``): the
-    ``upsampling`` + ``tail`` pair of the ESM upsamplers (models/ESMStereo.py:264-271,301-302)."""
+    ``upsampling`` + ``tail`` pair of the ESM upsamplers (models/ESMStereo.py:264-271,301-302).
+    ``form`` (nf 8, r 4): 0 automatic, 1 window form, 2 / 3 the row form with 4 / 8 rows per workgroup."""
     require_device(x, "shuffle_tail input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
@@ -755,9 +844,10 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
     d.ob, d.oh = out.stride(0), out.stride(2)
     d.B, d.nf, d.H, d.W, d.r = B, nf, H, W, r
     npix = B * H * W * r * r
-    d.flags = 1 if npix >= XCD_SLAB_MIN_PIX else 0
+    d.flags = (1 if npix >= XCD_SLAB_MIN_PIX else 0) | (int(form) & 3) << 1
     ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b)
-    ctx.meta.append(dict(name=tag, kind="shuffle_tail", flops=2 * npix * nf * (1 + 9),
+    # upsampling: the 1x1 nf -> nf*r^2 on H x W = nf^2 MACs per full-resolution pixel; tail: 3x3 nf -> 1
+    ctx.meta.append(dict(name=tag, kind="shuffle_tail", flops=2 * npix * nf * (nf + 9),
                          bytes=4 * (B * nf * H * W + npix), shape=f"nf{nf} r{r} in {H}x{W} out {H * r}x{W * r}",
                          reads=_spans(x), writes=_spans(out)))
     ctx.shuffle_tail(d)
@@ -811,7 +901,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     d.C, d.cin_pad, d.cout_pad = conv.cout, conv.cin_pad, conv.cout_pad
     ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
     npix = B * H * W * r * r
-    flops = 2 * npix * nf * (1 + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9
+    flops = 2 * npix * nf * (nf + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9  # head as shuffle_tail + the 1 -> C 3x3
     ctx.meta.append(dict(name=tag, kind="shuffle_conv", flops=flops,
                          bytes=4 * (B * nf * H * W + B * conv.cout * Ho2 * Wo2),
                          shape=f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}",

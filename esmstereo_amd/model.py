@@ -23,6 +23,8 @@ Split of the forward:
 from __future__ import annotations
 
 import collections
+import ctypes
+import itertools
 import math
 import operator
 import os
@@ -38,7 +40,7 @@ from .backbone import Feature
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
 from .engine import Ctx, require_device
 
-__all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath"]
+__all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath", "plan_ops"]
 
 _VERSION = operator.attrgetter("_version")
 
@@ -104,43 +106,48 @@ _UPSAMPLERS = {4: upsample4, 8: upsample8, 16: upsample16}
 class HotPath:
     """The hot path (ESMStereo.py:700-745) compiled for one set of input shapes.
 
-    Inputs live in static device buffers (``ml``, ``mr``, ``att``, ``up``); ``launch()``
-    replays the native plan (a hipGraph by default) on the current stream; ``outputs``
-    are static buffers holding the ``*4``-scaled disparities.
+    The plan owns static device buffers for its inputs (``ml``, ``mr``, ``att``, ``up``) and its
+    outputs; ``launch()`` replays the native plan (a hipGraph by default) on the current stream.
+    :meth:`bind` makes the plan read the caller's own tensors where they lie (zero-copy, as the
+    reference's forward does), :meth:`load_inputs` copies into the plan's buffers; ``outputs`` are
+    static buffers holding the ``*4``-scaled disparities.
     """
 
     def __init__(self, model: "ESMStereo", B: int, h: int, w: int, att_ch: int, up_shapes: Sequence[Tuple[int, ...]],
                  device: torch.device, train_status: bool = False, graph: bool = True, channels: int = 64):
         self.device = torch.device(device)
         args = (model, B, h, w, att_ch, up_shapes, train_status, channels)
-        self._emit(*args, first=Ctx.ARENA_FIRST, sizing=True)
-        if self.ctx.arena_chunks > 1:
-            # every buffer of the plan in ONE arena chunk: chunks allocated one by one can land more
-            # than 1 GiB apart in the address space, and a channel concat whose sources straddle two
-            # such chunks cannot be addressed through one buffer descriptor by the register-weight
-            # forms (conv_direct.h source_window), which then fall back to slower ones (measured: the
-            # S-K step 346.6 vs 363-366 us, depending on where the allocator placed the chunks)
-            need = self.ctx.arena_bytes + (1 << 20)
-            self.ctx.close()
-            self._emit(*args, first=need)
+        # size the arena with a dry emission (shape-only buffers, nothing submitted), then emit once
+        # into ONE arena chunk: chunks allocated one by one can land more than 1 GiB apart, and a
+        # channel concat whose sources straddle two of them cannot be addressed through one buffer
+        # descriptor by the register-weight forms (conv_direct.h source_window), which then fall back
+        # to slower ones (measured: the S-K step 346.6 vs 363-366 us)
+        with Ctx(self.device, dry=True) as dry:
+            self._emit(dry, *args)
+        self.ctx = Ctx(self.device, plan=True)
+        self.ctx.ARENA_FIRST = dry.arena_bytes + (1 << 20)
+        self._emit(self.ctx, *args)
         self.num_ops = lib.esm_plan_num_ops(self.ctx.plan)
+        if self.ctx.arena_chunks != 1 or self.num_ops != dry.num_ops:
+            raise RuntimeError(f"HotPath: dry emission disagrees with the plan ({dry.num_ops} vs {self.num_ops} ops, "
+                               f"{self.ctx.arena_chunks} arena chunks)")
         self.graph = bool(graph)
         self._graph_ready = False
+        arena = self.ctx._arena
+        self._arena_span = (arena.data_ptr(), arena.data_ptr() + arena.numel())
+        self._own = [self.ml, self.mr, self.att] + list(self.up)    # the plan's own input buffers
+        self._bound = [None if t is None else t.data_ptr() for t in self._own]  # what the plan reads now
 
-    def _emit(self, model, B, h, w, att_ch, up_shapes, train_status, channels, first: int,
-              sizing: bool = False) -> None:
-        self.ctx = Ctx(self.device, plan=True)
-        self.ctx.ARENA_FIRST = first
-        self.ctx.sizing = sizing  # a sizing pass: its buffer placement is discarded, so no window warning
-        e = self.ctx.empty
+    def _emit(self, ctx: Ctx, model, B, h, w, att_ch, up_shapes, train_status, channels) -> None:
+        e = ctx.empty
         self.ml = e(B, channels, h, w)
         self.mr = e(B, channels, h, w)
         self.att = e(B, att_ch, h, w) if att_ch else None
         # the upsampler's feature inputs at the arena's far end, next to the buffers allocated last
         # (the upsampler's own, which they are concatenated with): a concat's sources stay within one
         # 1 GiB window even when the cost volume between them is larger (configs[2]: B = 8)
-        self.up = [self.ctx.empty_tail(*s) for s in up_shapes]
-        self.outputs = model._emit_hot(self.ctx, self.ml, self.mr, self.att, self.up, train_status)
+        self.up = [ctx.empty_tail(*s) for s in up_shapes]
+        self.outputs = model._emit_hot(ctx, self.ml, self.mr, self.att, self.up, train_status)
 
     def op_kinds(self) -> List[int]:
         return [lib.esm_plan_op_kind(self.ctx.plan, i) for i in range(self.num_ops)]
@@ -169,13 +176,73 @@ class HotPath:
         else:
             check(lib.esm_plan_run(self.ctx.plan, s), "plan_run")
 
+    # ------------------------------------------------------------------ inputs
+    WINDOW = 1 << 30  # conv_direct.h kOOB: the span a concat's sources must stay inside
+
+    def _slots(self, ml, mr, att, up) -> list:
+        if len(up) != len(self.up):
+            raise ValueError(f"hot path: expected {len(self.up)} upsampler features, got {len(up)}")
+        if (att is None) != (self.att is None):
+            raise ValueError("hot path: att given to a plan built without it, or missing")
+        a = None if att is None else att.reshape(self.att.shape)
+        return [ml, mr, a] + list(up)
+
+    def _in_place_ok(self, i: int, t: torch.Tensor) -> bool:
+        """Whether the plan may read ``t`` where it lies: contiguous fp32 on the plan's device, not
+        overlapping the plan's arena (whose buffers the launches overwrite) unless it IS the slot's own
+        buffer, and for an upsampler feature (a channel-concat source, slots 3+) within one buffer window
+        of the arena, so every launch keeps its register-weight form."""
+        if t.data_ptr() == self._own[i].data_ptr():
+            return True
+        if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+            return False
+        lo, hi = t.data_ptr(), t.data_ptr() + 4 * t.numel()
+        a_lo, a_hi = self._arena_span
+        if lo < a_hi and a_lo < hi:
+            return False
+        return i < 3 or max(hi, a_hi) - min(lo, a_lo) < self.WINDOW
+
+    def _rebind(self, ptrs: Sequence[Optional[int]]) -> None:
+        olds, sizes, news = [], [], []
+        for i, p in enumerate(ptrs):
+            if p is not None and p != self._bound[i]:
+                olds.append(self._bound[i])
+                sizes.append(4 * self._own[i].numel())
+                news.append(p)
+                self._bound[i] = p
+        if olds:
+            n = len(olds)
+            check(lib.esm_plan_rebind(self.ctx.plan, n, (_lib.c_void_p * n)(*olds), (ctypes.c_uint64 * n)(*sizes),
+                                      (_lib.c_void_p * n)(*news)), "plan_rebind")
+
+    def bind(self, ml, mr, att, up) -> None:
+        """Point the plan at the caller's tensors (zero-copy; models/ESMStereo.py:700-745 reads its
+        features where they lie).  A tensor the plan cannot read in place (non-contiguous, another
+        device, aliasing the plan's buffers, or a concat source outside the window) is copied into the
+        plan's own buffer instead.  The plan keeps no reference: the caller keeps the tensors alive
+        until the launch that reads them has run (stream order, as for any PyTorch op).  When the
+        pointers are the ones already bound (a serving loop whose allocator hands back the same
+        blocks), nothing happens; otherwise the graph's affected nodes are updated in place."""
+        ptrs = []
+        for i, (t, own) in enumerate(zip(self._slots(ml, mr, att, up), self._own)):
+            if own is None:
+                ptrs.append(None)
+                continue
+            require_device(t, "hot-path input")
+            if tuple(t.shape) != tuple(own.shape):
+                raise ValueError(f"hot path input {i}: shape {tuple(t.shape)}, plan built for {tuple(own.shape)}")
+            if not self._in_place_ok(i, t):
+                own.copy_(t)
+                t = own
+            ptrs.append(t.data_ptr())
+        self._rebind(ptrs)
+
     def load_inputs(self, ml, mr, att, up) -> None:
-        self.ml.copy_(ml)
-        self.mr.copy_(mr)
-        if self.att is not None:
-            self.att.copy_(att.reshape(self.att.shape))
-        for dst, src in zip(self.up, up):
-            dst.copy_(src)
+        """Copy the inputs into the plan's own buffers (and read those)."""
+        for t, own in zip(self._slots(ml, mr, att, up), self._own):
+            if own is not None:
+                own.copy_(t)
+        self._rebind([None if t is None else t.data_ptr() for t in self._own])
 
     def close(self) -> None:
         # the plan's buffers came from torch's caching allocator on the stream current at build
@@ -184,6 +251,19 @@ class HotPath:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self.ctx.close()
+
+
+def plan_ops(model: "ESMStereo", B: int, h: int, w: int, att_ch: int, up_shapes: Sequence[Tuple[int, ...]],
+             train_status: bool = False, channels: int = 64) -> List[dict]:
+    """The launch list the hot path compiles to for these input shapes, one dict per launch (name,
+    kernel family, shape, algorithmic flops and bytes: ``Ctx.meta``), from a dry emission: nothing runs
+    and no device is needed (the weights may sit on the CPU)."""
+    with Ctx(torch.device("meta"), dry=True) as ctx:
+        e = ctx.empty
+        up = [e(*s) for s in up_shapes]
+        model._emit_hot(ctx, e(B, channels, h, w), e(B, channels, h, w), e(B, att_ch, h, w) if att_ch else None, up,
+                        train_status)
+    return ctx.meta
 
 
 class ESMStereo(nn.Module):
@@ -237,34 +317,38 @@ class ESMStereo(nn.Module):
 
     # ------------------------------------------------------------------ plan cache
     def invalidate_plans(self) -> None:
-        """Drop compiled hot-path plans (call after replacing a hot-path Parameter object; in-place
-        edits, ``load_state_dict`` and ``.to()`` are detected on their own)."""
+        """Drop compiled hot-path plans.  In-place edits, replaced Parameter / buffer objects,
+        ``load_state_dict`` and ``.to()`` are detected on their own; call this after adding or
+        removing a hot-path submodule."""
         for hp in self._plans.values():
             hp.close()
         self._plans.clear()
-        self.__dict__["_hot_list"] = None
+        self.__dict__["_hot_dicts"] = None
 
     def _apply(self, fn, *args, **kwargs):
         self.invalidate_plans()
         return super()._apply(fn, *args, **kwargs)
 
     def _hot_tensors(self) -> list:
-        lst = self.__dict__.get("_hot_list")
-        if lst is None:
+        """Every hot-path Parameter and buffer, read afresh from the modules' own ``_parameters`` /
+        ``_buffers`` dicts: the list of dicts is collected once (``_apply`` / ``load_state_dict``
+        rebuild it), the tensors in them on every call, so a replaced Parameter object
+        (``mod.weight = nn.Parameter(...)``) is seen as well as an in-place edit."""
+        dicts = self.__dict__.get("_hot_dicts")
+        if dicts is None:
             mods = [m for name in self._HOT_MODULES if getattr(self, name, None) is not None
                     for m in getattr(self, name).modules()]
-            lst = [t for m in mods for t in list(m.parameters(recurse=False)) + list(m.buffers(recurse=False))]
-            self.__dict__["_hot_list"] = lst
-        return lst
+            dicts = [d for m in mods for d in (m._parameters, m._buffers)]
+            self.__dict__["_hot_dicts"] = dicts
+        return [t for t in itertools.chain.from_iterable(map(dict.values, dicts)) if t is not None]
 
     def _hot_param_token(self) -> tuple:
-        """Identity (storage, in-place version) of every hot-path tensor: a weight edited in place
-        (``param.copy_``, BN statistics updated elsewhere) changes it, so the plan cache never
-        replays stale packed weights.  The tensor list is collected once (``_apply`` and
-        ``load_state_dict`` rebuild it); the per-call check is two C-level maps (~0.1 ms for the
-        383 tensors of ESMStereo-S, against 2.3 ms for walking the modules)."""
+        """Identity (object, storage, in-place version) of every hot-path tensor: a weight edited in
+        place (``param.copy_``, BN statistics updated elsewhere) or replaced by a new object changes
+        it, so the plan cache never replays stale packed weights.  C-level maps over the tensors
+        (~0.1 ms for the 383 tensors of ESMStereo-S, against 2.3 ms for walking the modules)."""
         ts = self._hot_tensors()
-        return tuple(map(_VERSION, ts)) + tuple(map(torch.Tensor.data_ptr, ts))
+        return tuple(map(_VERSION, ts)) + tuple(map(torch.Tensor.data_ptr, ts)) + tuple(map(id, ts))
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self.invalidate_plans()
@@ -372,7 +456,7 @@ class ESMStereo(nn.Module):
                 self._plans.popitem(last=False)[1].close()
         else:
             self._plans.move_to_end(key)
-        hp.load_inputs(ml, mr, att, up)
+        hp.bind(ml, mr, att, up)
         hp.launch()
         return [o.clone() for o in hp.outputs]
 
@@ -406,6 +490,9 @@ class ESMStereo_confidence(ESMStereo):
     only scale the reference builds it for, ``:915-916``), and ``forward(left, right) -> (disp * 4,
     confidence)`` (``:974``).  The head is emitted into the same compiled plan as the hot path: it
     reads the aggregated cost, ``init_pred`` and ``match_left`` in place (``:972``)."""
+
+    # the head is emitted into the same plan, so its weights key the plan cache too (ADVICE r3)
+    _HOT_MODULES = ESMStereo._HOT_MODULES + ("confidence_net",)
 
     def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
                  backbone: str = "efficientnet_b2", cv_scale: int = 4, device=None, *, feature_cls=None) -> None:

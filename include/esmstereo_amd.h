@@ -205,7 +205,8 @@ typedef struct {
     int64_t ob, oh;
     int32_t B, nf, H, W, r;
     int32_t flags; /* bit 0: XCD-slab tile order (each XCD runs a contiguous band of output rows; see
-                      esm_conv_desc.hint bit 30) */
+                      esm_conv_desc.hint bit 30); bits 1-2, (nf, r) = (8, 4) only: 0 automatic, 1 the
+                      low-res-window form, 2 / 3 the MFMA row form with 4 / 8 low-res rows per workgroup */
 } esm_shuffle_tail_desc;
 
 /* `tail(upsampling(x))` (as esm_shuffle_tail_desc, st.out unused) followed by the refinement
@@ -337,9 +338,19 @@ int esm_plan_run(esm_plan* plan, void* stream);
 /* Launch op `index` alone, `reps` times back to back on `stream` (timing one kernel of the
  * path with a single hipEvent pair around the batch; the op's buffers are the plan's own). */
 int esm_plan_run_op(esm_plan* plan, int index, int reps, void* stream);
-/* Capture the launch list into a hipGraph (instantiated once; replays are cheap). */
+/* Capture the launch list into a hipGraph (instantiated once; replays are cheap).  graph_launch
+ * builds the graph first when there is none (never built, or dropped by a hint / repeat / probe change
+ * or a rebind that changed an op's kernel). */
 int esm_plan_graph_build(esm_plan* plan, void* stream);
 int esm_plan_graph_launch(esm_plan* plan, void* stream);
+/* Zero-copy input binding: every pointer of every op that lies in [old_base[k], old_base[k] + bytes[k])
+ * moves to the same offset in new_base[k], k < n (the caller's tensors are read where they lie, the
+ * reference forward's behaviour, models/ESMStereo.py:700-745).  With a built graph, the nodes of the
+ * ops that changed are updated in place (after the previous replay has finished); when an op's
+ * kernel choice changes with its pointers, the graph is dropped and rebuilt by the next launch.
+ * Returns the number of pointer fields moved, or an error. */
+int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const uint64_t* bytes,
+                    const void* const* new_base);
 /* Probe: record a hipEvent pair around op `index` on every run/replay (ring of `ring`
  * pairs, ring <= 4096).  esm_plan_probe_read returns the elapsed ms of the completed
  * runs since the last read (caller synchronises first); returns the count written. */

@@ -66,7 +66,7 @@ def normcorr_volume(L: torch.Tensor, R: torch.Tensor, D: int) -> torch.Tensor:
 def disparity_regression(cost: torch.Tensor, D: int) -> torch.Tensor:
     """``disparity_regression`` (submodule.py:211-216): sum_d cost[d]*d, no softmax."""
     assert cost.dim() == 4
-    d = torch.arange(0, D, dtype=cost.dtype).view(1, D, 1, 1)
+    d = torch.arange(0, D, dtype=cost.dtype, device=cost.device).view(1, D, 1, 1)
     return torch.sum(cost * d, 1, keepdim=False)
 
 

@@ -4,6 +4,7 @@ Run in the build container only (it imports the reference from /root/reference):
 
     python tests/golden/make_golden.py               # fixture-size vectors (rewrites the manifest)
     python tests/golden/make_golden.py --fullsize    # + full-size summaries (BASELINE KITTI size)
+    python tests/golden/make_golden.py --fullsize --only L_gwc_SF8,M_gwc_K   # just these cases
 
 What it does (SURVEY.md §8(c) recipe):
 * imports ``models/submodule.py``, ``models/shufflemixer.py`` and ``models/ESMStereo.py``
@@ -162,6 +163,11 @@ FULL_CASES = [
     ("S_gwc_K", "S", "gwc", 1, 384, 1248, 192, 11, 101),
     ("L_gwc_K", "L", "gwc", 1, 384, 1248, 192, 15, 102),
     ("L_nc_K", "L", "nc", 1, 384, 1248, 192, 16, 103),
+    # round 4: the other BASELINE configurations (configs[2] SceneFlow B=8 padded to 544x960, configs[4]
+    # Middlebury padded to 1504x1024 md256) and ESMStereo-M at KITTI size
+    ("L_gwc_SF8", "L", "gwc", 8, 544, 960, 192, 15, 201),
+    ("L_gwc_Mid", "L", "gwc", 1, 1024, 1504, 256, 15, 401),
+    ("M_gwc_K", "M", "gwc", 1, 384, 1248, 192, 13, 104),
 ]
 
 
@@ -169,7 +175,10 @@ def make_fullsize(sm, es):
     from helpers import digest, fullsize_inputs
 
     man = {}
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     for tag, var, cv, B, H, W, maxdisp, wseed, iseed in FULL_CASES:
+        if only and tag not in only:
+            continue
         backbone, cv_scale = VARIANTS[var]
         model = es.ESMStereo(maxdisp, cv == "gwc", cv == "nc", backbone, cv_scale).eval()
         spec = module_spec(model)

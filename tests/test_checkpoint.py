@@ -108,3 +108,34 @@ def test_reload_invalidates_packed_weights_and_plan(tmp_path):
         assert float((out - ref).abs().mean()) <= 1e-3, seed
         outs.append(out)
     assert not torch.equal(outs[0], outs[1])
+
+
+def test_plan_key_sees_replaced_and_edited_parameters():
+    """The compiled-plan cache key (ESMStereo._hot_param_token) changes when a hot-path weight is
+    edited in place AND when a hot-path Parameter object is replaced; a backbone edit
+    (out of the hot path) leaves it alone."""
+    m = E.ESMStereo(64, True, False, "mobilenetv2_100", 16, feature_cls=StubFeature)
+    t0 = m._hot_param_token()
+    conv = m.aggregation_out.conv1[0].conv
+    with torch.no_grad():
+        conv.weight.add_(1.0)
+    t1 = m._hot_param_token()
+    assert t1 != t0
+    conv.weight = torch.nn.Parameter(conv.weight.detach().clone())
+    t2 = m._hot_param_token()
+    assert t2 != t1
+    with torch.no_grad():
+        for p in m.feature.parameters():
+            p.add_(1.0)
+    assert m._hot_param_token() == t2
+
+
+def test_confidence_head_weights_key_the_plan():
+    """ESMStereo_confidence emits LAFNet_ESM into the hot path's plan, so its weights are part of the
+    plan key: an in-place edit of a confidence_net weight invalidates the compiled plan."""
+    m = E.ESMStereo_confidence(64, True, False, "mobilenetv2_100", 16, feature_cls=StubFeature)
+    t0 = m._hot_param_token()
+    w = next(m.confidence_net.parameters())
+    with torch.no_grad():
+        w.mul_(2.0)
+    assert m._hot_param_token() != t0

@@ -142,3 +142,44 @@ def test_gloo_world2_bench_step(mode):
     for rank, ok, el, ncalls, b, scaling, total, mx in res:
         assert ok and ncalls == 7 and mx == 1.0
         assert scaling == mode and (b, total) == ((2, 4) if mode == "weak" else (3, 6))
+
+
+def _bench(*argv, env=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *argv], capture_output=True, text=True,
+                       env=e, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, [json.loads(ln) for ln in lines], r.stderr
+
+
+@pytest.mark.parametrize("extra,want", [((), (2, [2, 1, 8, 16], "weak")),
+                                        (("--global-batch", "6"), (6, [2, 3, 8, 16], "strong"))])
+def test_bench_launches_its_own_ranks(extra, want):
+    """`python bench.py --gpus 2` with no launcher starts the 2 ranks itself: one JSON
+    line from rank 0 with n_gpus 2, the per-step gather's [world, b, H, W] buffer, the pairs of both
+    ranks counted.  The ranks run the real launcher / dist path with a gloo CPU stand-in step."""
+    rc, lines, err = _bench("--gpus", "2", "--cpu-standin", "--steps", "3", "--warmup", "1", *extra)
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["global_batch"] == want[0]
+    assert line["gathered_shape"] == want[1] and line["scaling"] == want[2]
+    assert line["value"] > 0
+
+
+def test_bench_gpus_must_match_launcher_world():
+    rc, lines, err = _bench("--gpus", "1", "--cpu-standin", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines and "disagrees with WORLD_SIZE" in err
+
+
+def test_bench_parent_reports_a_failing_rank():
+    """A rank that fails makes the parent exit non-zero (and stops the other rank): a strong-scaling
+    batch that does not split evenly raises in every rank."""
+    rc, lines, err = _bench("--gpus", "2", "--cpu-standin", "--global-batch", "3", "--steps", "1", "--warmup", "0")
+    assert rc != 0 and not lines

@@ -164,6 +164,18 @@ def test_confidence_model_forward():
     err = maxabs(conf, ref.squeeze(1))
     print("confidence model: max |conf - oracle|", err)
     assert err < 1e-3
+    # an in-place edit of a confidence_net weight must reach the compiled plan: the
+    # head's packed weights are part of the plan-cache key
+    with torch.no_grad():
+        for p in model.confidence_net.parameters():
+            p.mul_(1.5)
+        disp2, conf2 = model(left, right)
+        sd2 = {k: v.detach().float().cpu() for k, v in model.state_dict().items() if v.is_floating_point()}
+        ref2 = CO.lafnet(sd2, "confidence_net.", inter["cost"].squeeze(1), inter["init_pred"], cpu(ml), cpu(up[4]),
+                         cpu(up[2]))
+    assert torch.equal(disp2, disp)
+    assert not torch.equal(conf2, conf)
+    assert maxabs(conf2, ref2.squeeze(1)) < 1e-3
 
 
 def test_confidence_small_maxdisp_raises():

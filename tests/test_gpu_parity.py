@@ -520,7 +520,8 @@ def test_convt_c1_form(nd, cin):
 
 
 @pytest.mark.parametrize("nf,r,H,W", [(8, 4, 24, 78), (8, 4, 7, 21), (8, 2, 13, 29), (16, 2, 24, 78), (16, 2, 5, 9),
-                                      (16, 4, 6, 17), (8, 4, 96, 312), (8, 2, 130, 301)])
+                                      (16, 4, 6, 17), (8, 4, 96, 312), (8, 2, 130, 301), (8, 4, 1, 1),
+                                      (8, 4, 9, 17), (8, 4, 33, 50)])
 def test_shuffle_tail(nf, r, H, W):
     """upsampling (1x1 + PixelShuffle + SiLU) fused with tail (3x3 -> 1) vs fp64 torch of the
     reference's two modules (models/ESMStereo.py:264-271,301-302); rel <= 1e-5.  Tiles: 8 x 32 (one
@@ -534,9 +535,10 @@ def test_shuffle_tail(nf, r, H, W):
     ref = F.conv2d(F.silu(F.pixel_shuffle(F.conv2d(x.double(), up.weight.double(), up.bias.double()), r)),
                    tail.weight.double(), tail.bias.double(), 1, 1).float()
     p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), r)
-    y = run_shuffle_tail(Ctx(DEV), x.to(DEV), p)
-    assert y.shape == (2, 1, H * r, W * r)
-    assert rel(y, ref) < 1e-5
+    for form in ((0, 1, 2, 3) if (nf, r) == (8, 4) else (0,)):  # (8, 4): the window and both row forms
+        y = run_shuffle_tail(Ctx(DEV), x.to(DEV), p, form=form)
+        assert y.shape == (2, 1, H * r, W * r)
+        assert rel(y, ref) < 1e-5, form
 
 
 @pytest.mark.parametrize("nf,r,C,H,W", [(8, 4, 16, 24, 78), (8, 4, 16, 96, 312), (8, 4, 16, 7, 13), (8, 2, 16, 13, 29),
@@ -846,7 +848,7 @@ def test_hot_path_fullsize_vs_reference(name):
         init = E.regression_topk(cost, None, 2) if m["cv_scale"] == 4 else E.disparity_regression(cost, D)
     disp0 = model.hot_path(ml, mr, att, up)[0]
     with torch.no_grad():  # upsample_module on the reference's init_pred (models/ESMStereo.py:722-735)
-        d_ref_init = model.upsample_module.emit(E.engine.Ctx(DEV), up, cu(g["init_pred"]), final_scale=4.0)[0]
+        d_ref_init = E.engine.eager_emit(DEV, model.upsample_module.emit, up, cu(g["init_pred"]), final_scale=4.0)[0]
     rep = check_fullsize(name, m, g, cost, init.view(m["B"], 1, *cost.shape[-2:]), disp0,
                          disp0_from_ref_init=d_ref_init[:, 0])
     print(name, rep)
@@ -891,6 +893,54 @@ def test_plan_modes_agree_and_probe():
         t = hp.probe_read()
         assert len(t) == 3 and all(v > 0 for v in t), t
     assert hp_graph.num_ops > 30
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_hot_path_reads_inputs_in_place(graph):
+    """Zero-copy boundary: the plan reads the caller's feature tensors where they lie
+    (esm_plan_rebind), for the S plan (att, four upsampler features) and the L plan.  Against the copy
+    path (load_inputs into the plan's own buffers), bitwise: fresh tensors on every call, the same
+    tensors edited in place (no stale copy), ml / mr swapped between calls (each pointer moves once),
+    a non-contiguous feature (copied into the plan's buffer instead) and back to in place, all with
+    the graph built (its nodes updated in place) and without."""
+    for name in ("hot_S_gwc.npz", "hot_L_gwc.npz"):
+        model, sd, m = _model_from_manifest(name)
+        model.use_graph = graph
+        g = load_golden(name)
+        nup = sum(1 for k in g if k.startswith("up_"))
+        ml, mr = cu(g["match_left"]), cu(g["match_right"])
+        att = cu(g["att"]) if "att" in g else None
+        up = [cu(g[f"up_{i}"]) for i in range(nup)]
+        B, C, h, w = ml.shape
+        ref_hp = E.HotPath(model, B, h, w, 0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], DEV,
+                           graph=False)
+
+        def expect(a, b, at, u):
+            ref_hp.load_inputs(a, b, at, u)
+            ref_hp.launch()
+            return ref_hp.outputs[0].clone()
+
+        with torch.no_grad():
+            first = model.hot_path(ml, mr, att, up)[0]
+            assert torch.equal(first, expect(ml, mr, att, up)), name
+            for it in range(3):  # fresh allocations: the bound pointers move
+                ml2, mr2 = ml * (1.0 + 0.1 * it), mr.clone()
+                up2 = [u + 0.01 * it for u in up]
+                out = model.hot_path(ml2, mr2, att, up2)[0]
+                assert torch.equal(out, expect(ml2, mr2, att, up2)), (name, it)
+            ml2.mul_(0.5)  # same tensors, new values: read in place, nothing stale
+            out = model.hot_path(ml2, mr2, att, up2)[0]
+            assert torch.equal(out, expect(ml2, mr2, att, up2)), name
+            out = model.hot_path(mr2, ml2, att, up2)[0]  # swapped
+            assert torch.equal(out, expect(mr2, ml2, att, up2)), name
+            wide = torch.zeros(up2[0].shape[:-1] + (2 * up2[0].shape[-1],), device=DEV)
+            wide[..., ::2] = up2[0]
+            upn = [wide[..., ::2]] + up2[1:]  # non-contiguous: copied into the plan's own buffer
+            out = model.hot_path(mr2, ml2, att, upn)[0]
+            assert torch.equal(out, expect(mr2, ml2, att, upn)), name
+            out = model.hot_path(ml, mr, att, up)[0]  # and back in place
+            assert torch.equal(out, first), name
+        ref_hp.close()
 
 
 def test_expected_raises():

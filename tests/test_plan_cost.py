@@ -1,0 +1,151 @@
+"""The algorithmic cost the benchmark's rooflines are priced on (``Ctx.meta`` of every launch of the
+compiled hot path, bench.py ``roofline`` / ``roofline_step``), checked on the CPU without a GPU: the
+plan is emitted dry (``esmstereo_amd.model.plan_ops``: shape-only buffers, nothing submitted) for the
+S-K, M-K, L-K and Middlebury plans and every op's flops and bytes are recomputed here, independently
+of engine.py:
+
+* the sum of the conv-like ops' flops equals what ``torch.utils.flop_counter`` counts for the CPU
+  oracle (oracle/esm_oracle.py, the reference's forward restated) run on shape-only tensors: every
+  convolution of models/ESMStereo.py:700-745, the ShuffleMixer heads' 1x1 / 3x3 and the FMBlocks'
+  split-point MLPs / depthwise convs included;
+* each conv / conv-pair / shuffle / FMBlock / volume / regression op's flops and bytes from the
+  layer's own weight shape and the extents, with the conv output extent re-derived from the layer's
+  kernel / stride / padding.
+"""
+import math
+import re
+
+import pytest
+import torch
+from torch.utils.flop_counter import FlopCounterMode
+
+import esmstereo_amd as E
+from esmstereo_amd.backbone import StubFeature
+from esmstereo_amd.model import plan_ops
+from helpers import UP_LAYOUT, load_spec, seeded_state
+from oracle import esm_oracle as O
+
+CASES = {  # name: (variant, backbone, cv_scale, B, H, W, maxdisp)
+    "S-K": ("S", "mobilenetv2_100", 16, 1, 384, 1248, 192),
+    "M-K": ("M", "efficientnet_b2", 8, 1, 384, 1248, 192),
+    "L-K": ("L", "efficientnet_b2", 4, 1, 384, 1248, 192),
+    "L-K B4": ("L", "efficientnet_b2", 4, 4, 384, 1248, 192),
+    "Mid": ("L", "efficientnet_b2", 4, 1, 1024, 1504, 256),
+}
+CONV_KINDS = ("conv", "conv_pair", "shuffle_tail", "shuffle_conv", "fmnet")
+
+
+def _plan(case):
+    var, bb, cvs, B, H, W, md = CASES[case]
+    sd = seeded_state(load_spec(f"spec_{var}_gwc.json"), 1)
+    m = E.ESMStereo(md, True, False, bb, cvs, feature_cls=StubFeature)
+    m.load_state_dict(sd)
+    m.eval()
+    ups = [(B, c, H // s, W // s) for c, s in UP_LAYOUT[cvs]]
+    return m, sd, plan_ops(m, B, H // cvs, W // cvs, 32 if cvs == 16 else 0, ups), (B, H, W, md, cvs, ups)
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_plan_flops_equal_flop_counter_on_oracle(case):
+    m, sd, meta, (B, H, W, md, cvs, ups) = _plan(case)
+    h, w = H // cvs, W // cvs
+    M = lambda *s: torch.empty(*s, device="meta")  # noqa: E731
+    fc = FlopCounterMode(display=False)
+    with fc, torch.no_grad():
+        O.hot_path({k: v.to("meta") for k, v in sd.items()}, cvs, md, True, M(B, 64, h, w), M(B, 64, h, w),
+                   M(B, 32, h, w) if cvs == 16 else None, [M(*u) for u in ups])
+    counted = fc.get_total_flops()
+    ours = sum(x["flops"] for x in meta if x["kind"] in CONV_KINDS)
+    assert ours == counted, (case, ours, counted, ours - counted)
+
+
+def _ext(s):
+    return tuple(int(v) for v in s.split("x"))
+
+
+def _layer(model, name):
+    mod = model.get_submodule(name)
+    return mod.conv if isinstance(mod, E.BasicConv) else mod
+
+
+def _conv_cost(conv, B, ein, eout, scale2=False):
+    """(flops, bytes, output extent re-derived from the layer) of one conv launch."""
+    w = conv.weight
+    nd = w.dim() - 2
+    taps = math.prod(w.shape[2:])
+    tr = isinstance(conv, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d))
+    cin, cout = (w.shape[0], w.shape[1]) if tr else (w.shape[1], w.shape[0])
+    sp = ein[-nd:]
+    if tr:
+        want = tuple(2 * v for v in sp)
+    else:
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        want = tuple((v + 2 * p - k) // s + 1 for v in sp)
+    vin, vout = B * math.prod(sp), B * math.prod(eout[-nd:])
+    flops = 2 * (vin if tr else vout) * cin * cout * taps
+    byts = 4 * (vin * cin + vout * cout + cin * cout * taps)
+    return flops, byts, want, vout * cout
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_plan_per_op_cost(case):
+    m, sd, meta, (B, H, W, md, cvs, ups) = _plan(case)
+    h, w = H // cvs, W // cvs
+    D = md // cvs
+    for op in meta:
+        name, kind, shape = op["name"], op["kind"], op.get("shape", "")
+        if kind == "conv":
+            g = re.search(r"in (\S+) out (\S+)", shape)
+            ein, eout = _ext(g.group(1)), _ext(g.group(2))
+            f, b, want, nout = _conv_cost(_layer(m, name), B, ein, eout)
+            assert want == eout[-len(want):], (name, want, eout)
+            assert op["flops"] == f, name
+            if re.match(r"upsample_module\.ref\d+x\.conv1_up$", name):
+                # the epilogue adds bilinear(previous disparity, r): its 1-channel source is read too
+                r = 4 if cvs == 16 else 2
+                b += 4 * B * (eout[-2] // r) * (eout[-1] // r)
+            assert op["bytes"] == b, (name, op["bytes"], b)
+        elif kind == "conv_pair":
+            sa, sb = shape[len("pair "):].split(" + ")
+            na, nb = name.split("+")
+            nb = na.rsplit(".", 1)[0] + "." + nb
+            ga, gb = re.search(r"in (\S+) out (\S+)", sa), re.search(r"in (\S+) out (\S+)", sb)
+            fa, ba, wa, mid = _conv_cost(_layer(m, na), B, _ext(ga.group(1)), _ext(ga.group(2)))
+            fb, bb, wb, _ = _conv_cost(_layer(m, nb), B, _ext(gb.group(1)), _ext(gb.group(2)))
+            assert op["flops"] == fa + fb, name
+            assert op["bytes"] == ba + bb - 2 * 4 * mid, name  # the intermediate map never reaches HBM
+        elif kind in ("shuffle_tail", "shuffle_conv"):
+            g = re.search(r"nf(\d+) r(\d+) in (\d+)x(\d+)", shape)
+            nf, r, hi, wi = (int(v) for v in g.groups())
+            npix = B * hi * wi * r * r
+            head = 2 * B * hi * wi * nf * nf * r * r + 2 * npix * nf * 9  # 1x1 nf -> nf r^2, then 3x3 nf -> 1
+            if kind == "shuffle_tail":
+                assert op["flops"] == head and op["bytes"] == 4 * (B * nf * hi * wi + npix), name
+            else:
+                g2 = re.search(r"C(\d+) (\d+)x(\d+)$", shape)
+                c, ho, wo = (int(v) for v in g2.groups())
+                assert op["flops"] == head + 2 * B * ho * wo * c * 9, name
+                assert op["bytes"] == 4 * (B * nf * hi * wi + B * c * ho * wo), name
+        elif kind == "fmnet":
+            g = re.search(r"C(\d+) (\d+)x(\d+) dw(\d+)", shape)
+            C, hh, ww, k = (int(v) for v in g.groups())
+            hid = C + 16
+            per_px = 4 * 2 * (C // 2 * C + C * C // 2) + 2 * 2 * C * k * k + 2 * (9 * C * hid + hid * C)
+            assert op["flops"] == B * hh * ww * per_px, name
+            conv_w = 9 * C * hid + hid + hid * C + C
+            assert op["bytes"] == 4 * (2 * B * C * hh * ww + conv_w), name
+        elif kind == "gwc":
+            G = 32
+            assert op["flops"] == 2 * B * 64 * D * h * w
+            assert op["bytes"] == 4 * B * (2 * 64 * h * w + G * D * h * w + (G * h * w if cvs == 16 else 0))
+        elif kind == "regression":
+            assert op["bytes"] == 4 * B * (D + 1) * h * w
+        else:
+            raise AssertionError(f"unchecked op kind {kind} ({name})")
+
+
+def test_shuffle_head_flops_s_k():
+    """upsampling4 + tail4x at S-K is 2 * 384 * 1248 * 8 * (8 + 9) = 130.35 MFLOP."""
+    _, _, meta, _ = _plan("S-K")
+    op = next(x for x in meta if x["name"] == "upsample_module.upsampling4+tail4x")
+    assert op["flops"] == 2 * 384 * 1248 * 8 * 17 == 130_351_104
