@@ -21,6 +21,8 @@ bool wide3_ok(const esm_conv_desc& a);                    // conv_wide3.hip
 int launch_wide3(const esm_conv_desc& a, hipStream_t s);  // conv_wide3.hip
 bool widet_ok(const esm_conv_desc& a);                    // conv_widet.hip
 int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
+bool tile3_auto(const esm_conv_desc& a);                 // conv_tile3.hip
+int launch_tile3(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
@@ -30,6 +32,7 @@ constexpr int kHintSmall = 1 << 21;    // lean K-split form for latency-bound la
 constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-D s1 (conv_wide.hip)
 constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
 constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 form, all 4 classes per wave (conv_widet.hip)
+constexpr int kHintTile3 = 1 << 23;    // LDS-tiled implicit-GEMM 3-D form for the large volumes (conv_tile3.hip)
 
 // Descriptor validation shared by every entry point that takes an esm_conv_desc (launch_conv, the
 // chain of chain.hip); ESM_OK or ESM_ERR_ARG with the message set.
@@ -94,6 +97,9 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return launch_conv(&d, s);
     }
     if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
+    if (a.hint & kHintTile3) return conv::launch_tile3(a, s);
+    // the MFMA-bound 3-D volumes of ESMStereo-L / -M (>= 2^17 output voxels): the LDS-tiled form
+    if (form == 0 && conv::tile3_auto(a)) return conv::launch_tile3(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

@@ -1,0 +1,338 @@
+// LDS-tiled implicit-GEMM 3-D convolution for the large volumes of ESMStereo-L / -M (BasicConv 3-D,
+// models/submodule.py:12-38, in the stems and the aggregation hourglass, models/ESMStereo.py:129-182,
+// 610-622): 3x3x3 stride 1 / 2 padding 1 and 1x1x1, where at KITTI size and above each layer is a dense
+// GEMM of M = Cout (8..72), N = voxels (10^5..10^7), K = 27 Cin (216..1944) and the MFMA pipe, not
+// latency, bounds the launch.  The register-operand forms (conv_direct.h, conv_stem.hip, conv_wide3.hip)
+// fetch every MFMA operand from L1/L2 per wave; here a workgroup stages its input window and the
+// weights of one 4-channel k-step in LDS (global loads for the next k-step in flight while the MFMAs of
+// this one run: double-buffered LDS, one barrier per k-step) and every MFMA operand is a conflict-free
+// ds_read_b32:
+//   * GEMM orientation (v_mfma_f32_16x16x4_f32): A = weights (16 couts x 4 channels), B = input (4
+//     channels x 16 output columns), D = 16 couts x 16 columns -> each store instruction writes 16
+//     consecutive x of one cout;
+//   * a wave owns 16 columns x NT rows of one output plane and MT cout tiles; for each (dz, dx) tap pair
+//     it reads the NT + 2 (stride 2: 2 NT + 1) input rows once and feeds them to the three dy taps;
+//   * <= 8 couts (the stems: group_stem 32 -> 8, agg 8 -> 8): the 16 MFMA rows carry 8 couts of two
+//     output planes (PZ); input plane 2q + p (p = 0..3) reaches the pair q through the composite weight
+//     A_p[(h, co)][ci] = W[dz = p - h][ci][co] (zero outside 0..2), staged in LDS once per k-step, so a
+//     pair costs 36 MFMAs per k-step instead of the 54 of two half-empty tiles;
+//   * bank-conflict-free reads: the input image's channel stride is = 16 (stride 1) or = 1 (stride 2)
+//     mod 32 banks, the weight rows' stride = 16 mod 32 (MI355X_MICROARCH.md LDS table, ds_read_b32);
+//   * partial sums never leave the wave: the K loop runs over every channel chunk in order, so each
+//     output is one fixed-order sum (deterministic, independent of the tiling).
+// Epilogue as the other forms: folded BN scale / shift, activation, optional * mul, + res, * post_scale
+// and the second copy, write-through (sc1) buffer stores.
+#include "conv_direct.h"
+
+namespace esm {
+namespace conv {
+namespace {
+
+constexpr int kT3Threads = 256;
+
+template <int S, int K, int NT, int WZ, bool PZ, int MT>
+struct T3Geo {
+    static constexpr int WY = 4 / WZ;                     // waves along y
+    static constexpr int ZB = PZ ? 2 * WZ : WZ;           // output planes per workgroup
+    static constexpr int YB = WY * NT;                    // output rows per workgroup
+    static constexpr int IZ = (ZB - 1) * S + K, IY = (YB - 1) * S + K, IX = 15 * S + K;  // input window
+    static constexpr int PLANE = IY * IX;
+    static constexpr int CS0 = IZ * PLANE;
+    static constexpr int CMOD = S == 1 ? 16 : 1;          // channel stride mod 32 (bank offset of lanes 16..31)
+    static constexpr int CS = CS0 + ((CMOD - CS0 % 32) % 32 + 32) % 32;
+    static constexpr int XE = 4 * CS0;                    // staged input elements per k-step
+    static constexpr int XL = 4 * CS;                     // LDS floats per input buffer
+    static constexpr int TAPS = K * K * K;
+    static constexpr int WCS = PZ ? 16 : (MT % 2 ? MT * 16 : MT * 16 + 16);  // weight row stride (= 16 mod 32)
+    static constexpr int WE = PZ ? 4 * 9 * 4 * 16 : TAPS * 4 * MT * 16;      // staged weight elements
+    static constexpr int WL = PZ ? WE : TAPS * 4 * WCS;                      // LDS floats per weight buffer
+    static constexpr int XR = (XE + kT3Threads - 1) / kT3Threads;
+    static constexpr int WR = (WE + kT3Threads - 1) / kT3Threads;
+    static constexpr int NR = (NT - 1) * S + K;           // input rows a wave reads per (dz, dx)
+};
+
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN>
+__global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
+    using G = T3Geo<S, K, NT, WZ, PZ, MT>;
+    constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
+    constexpr int XR = G::XR, WR = G::WR, NR = G::NR;
+    __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
+    __shared__ __attribute__((aligned(16))) float ws[2][G::WL];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int zw = wave % WZ, yw = wave / WZ;
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
+    const int xo0 = bk_.x * 16, yo0 = bk_.y * G::YB;
+    const int nzb = (a.Do + G::ZB - 1) / G::ZB;
+    const int zz = bk_.z;
+    const int mg = zz % ncg;
+    const int r1 = zz / ncg;
+    const int b = r1 / nzb;
+    const int zo0 = (r1 - b * nzb) * G::ZB;
+    constexpr int PAD = K == 3 ? 1 : 0;
+    const int zi0 = zo0 * S - PAD, yi0 = yo0 * S - PAD, xi0 = xo0 * S - PAD;
+
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
+        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), static_cast<short>(0), 4 * G::TAPS * a.cin_pad * a.cout_pad, 0x00020000);
+
+    // ---- per-thread staging slots (the same window for every k-step; the k-step's channel offset goes
+    //      into the wave-uniform soffset)
+    // slot k's element e = tid + 256 k: channel e / CS0, LDS index e + channel * (CS - CS0) (recomputed
+    // from e where used: only the global offset is kept in a register)
+    unsigned xoff[XR];
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int e = tid + k * kT3Threads;
+        const int ix = e % IX, iy = (e / IX) % IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
+        const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
+        const bool ok = e < G::XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+        xoff[k] = ok ? 4u * static_cast<unsigned>(ci * sc + zi * sd + yi * sh + xi) : kOOB;
+    }
+    unsigned woff[WR];
+    int wdst[WR];
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        const int e = tid + k * kT3Threads;
+        bool ok = e < G::WE;
+        unsigned off = 0;
+        int dst = -1;
+        if constexpr (PZ) {  // e = ((p * 9 + t9) * 4 + ci) * 16 + m
+            const int m = e & 15, ci = (e >> 4) & 3, t9 = (e >> 6) % 9, p = (e >> 6) / 9;
+            const int dz = p - (m >> 3), co = m & 7;
+            ok = ok && dz >= 0 && dz <= 2 && co < a.Cout;
+            off = 4u * static_cast<unsigned>(((dz * 9 + t9) * a.cin_pad + ci) * a.cout_pad + co);
+            dst = e < G::WE ? e : -1;
+        } else {  // e = (tap * 4 + ci) * (MT * 16) + m
+            const int m = e % (MT * 16), ci = (e / (MT * 16)) & 3, tap = e / (MT * 64);
+            const int co = mg * MT * 16 + m;
+            ok = ok && co < a.cout_pad;
+            off = 4u * static_cast<unsigned>((tap * a.cin_pad + ci) * a.cout_pad + co);
+            dst = e < G::WE ? (tap * 4 + ci) * WCS + m : -1;
+        }
+        woff[k] = ok ? off : kOOB;
+        wdst[k] = dst;
+    }
+    float xv[XR], wv[WR];
+    auto stage_load = [&](int c0) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int ci = (tid + k * kT3Threads) / G::CS0;
+            xv[k] = buf_load_s(rs, c0 + ci < a.Cin ? xoff[k] : kOOB, 4 * c0 * sc);
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int e = tid + k * kT3Threads;
+            if (e < G::XE) xs[buf][e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k)
+            if (wdst[k] >= 0) ws[buf][wdst[k]] = wv[k];
+    };
+
+    // epilogue constants, loaded while the first k-step streams in
+    constexpr int NCO = PZ ? 1 : MT;
+    float scl[NCO][4], shf[NCO][4];
+#pragma unroll
+    for (int mt = 0; mt < NCO; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = PZ ? ((4 * g + j) & 7) : mg * MT * 16 + mt * 16 + 4 * g + j;
+            const int cc = min(co, a.Cout - 1);
+            scl[mt][j] = a.scale ? a.scale[cc] : 1.f;
+            shf[mt][j] = a.shift ? a.shift[cc] : 0.f;
+        }
+
+    floatx4 acc[NT][NCO];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < NCO; ++mt) acc[nt][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int nchunk = (a.Cin + 3) >> 2;
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
+        const float* xw = &xs[buf][g * CS + (yw * NT * S) * IX + n * S];
+        if constexpr (PZ) {
+            const float* wp = &ws[buf][g * 16 + n];
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    float br[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy) {
+                        const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[nt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt][0], 0, 0, 0);
+                    }
+                }
+        } else {
+            const float* wp = &ws[buf][g * WCS + n];
+#pragma unroll
+            for (int dz = 0; dz < K; ++dz)
+#pragma unroll
+                for (int dx = 0; dx < K; ++dx) {
+                    float br[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) br[r] = xw[(zw * S + dz) * PLANE + r * IX + dx];
+#pragma unroll
+                    for (int dy = 0; dy < K; ++dy) {
+                        float av[MT];
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) av[mt] = wp[((dz * K + dy) * K + dx) * 4 * WCS + mt * 16];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                            for (int mt = 0; mt < MT; ++mt)
+                                acc[nt][mt] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], br[nt * S + dy], acc[nt][mt], 0, 0, 0);
+                    }
+                }
+        }
+        if (ch + 1 < nchunk) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane (g, n) holds rows 4g + j of each tile, column n
+    const int x = xo0 + n;
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0),
+        4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
+             (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int y = yo0 + yw * NT + nt;
+#pragma unroll
+        for (int mt = 0; mt < NCO; ++mt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int m = 4 * g + j;
+                const int co = PZ ? (m & 7) : mg * MT * 16 + mt * 16 + m;
+                const int z = PZ ? zo0 + 2 * zw + (m >> 3) : zo0 + zw;
+                const bool ok = co < a.Cout && z < a.Do && y < a.Ho && x < a.Wo;
+                float v = acc[nt][mt][j];
+                v = a.scale ? v * scl[mt][j] + shf[mt][j] : v + shf[mt][j];
+                v = act_t<ACT>(v, a.act);
+                if constexpr (PLAIN) {
+                    const unsigned o = ok ? 4u * static_cast<unsigned>(co * static_cast<int>(a.oc) +
+                                                                       z * static_cast<int>(a.od) +
+                                                                       y * static_cast<int>(a.oh) + x)
+                                          : kOOB;
+                    store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0);
+                } else {
+                    if (!ok) continue;
+                    if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + static_cast<long long>(y) * a.mh + x];
+                    if (a.res)
+                        v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(z) * a.rd +
+                                      static_cast<long long>(y) * a.rh + x];
+                    const long long o = b * a.ob + co * a.oc + static_cast<long long>(z) * a.od +
+                                        static_cast<long long>(y) * a.oh + x;
+                    a.out[o] = v * a.post_scale;
+                    if (a.out2) a.out2[o] = v * a.post_scale2;
+                }
+            }
+    }
+}
+
+template <int S, int K, int MT, int NT, int WZ, bool PZ>
+int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
+    using G = T3Geo<S, K, NT, WZ, PZ, MT>;
+    const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
+    const long long gy = ceil_div(a.Ho, G::YB);
+    if (z > 65535 || gy > 65535) return arg_error("conv(tile3): grid too large");
+    const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
+    const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
+                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
+                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (plain)
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true>), grid, dim3(kT3Threads), 0, s, a, ncg);
+    else
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false>), grid, dim3(kT3Threads), 0, s, a, ncg);
+    return check_launch("conv(tile3)");
+}
+
+// cout tiles per workgroup (MT) and cout groups (ncg) for Cout: MT * 16 * ncg >= Cout
+template <int S, int K, int NT, int WZ>
+int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
+    const int tiles = (a.Cout + 15) / 16;
+    if (tiles <= 3) {
+        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false>(a, s, 1);
+        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false>(a, s, 1);
+        return launch_t3<S, K, 3, NT, WZ, false>(a, s, 1);
+    }
+    // 4+ tiles (72 couts: 5): two cout groups of ceil(tiles / 2) tiles
+    if (tiles <= 4) return launch_t3<S, K, 2, NT, WZ, false>(a, s, 2);
+    if (tiles <= 6) return launch_t3<S, K, 3, NT, WZ, false>(a, s, 2);
+    return arg_error("conv(tile3): at most 96 output channels");
+}
+
+}  // namespace
+
+// 3-D, one source, 3x3x3 stride 1 / 2 padding 1 or 1x1x1 stride 1 padding 0, <= 96 couts, spans within
+// 32-bit buffer offsets.
+bool tile3_ok(const esm_conv_desc& a) {
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    if (!d3 || a.transposed || a.nsrc != 1 || a.up || a.shuffle > 1 || a.Cout > 96) return false;
+    const bool k3 = a.kd == 3 && a.kh == 3 && a.kw == 3 && a.pd == 1 && a.ph == 1 && a.pw == 1 &&
+                    (a.stride == 1 || a.stride == 2);
+    const bool k1 = a.kd == 1 && a.kh == 1 && a.kw == 1 && a.pd == 0 && a.ph == 0 && a.pw == 0 && a.stride == 1;
+    if (!k3 && !k1) return false;
+    if (a.cout_pad < 16 * ((a.Cout + 15) / 16)) return false;
+    return direct_ok(a);
+}
+
+// Automatic choice: the MFMA-bound volumes (>= 2^17 output voxels per launch), where the register-operand
+// forms sit at 0.15-0.41 of the fp32 MFMA peak (profiles/r03_ops_LK4.txt).  The latency-bound small
+// volumes of S / M keep their forms.
+bool tile3_auto(const esm_conv_desc& a) {
+    if (!tile3_ok(a)) return false;
+    const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
+    return vox >= (1LL << 17);
+}
+
+// hint bits 26-27 with TILE3 (bit 23): rows per wave 1 / 2 / 4 (0 = automatic)
+int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
+    if (!tile3_ok(a)) return arg_error("conv: tile3-form hint not applicable");
+    const int rsel = (a.hint >> 26) & 3;
+    const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
+    if (a.kh == 1) {
+        if (rsel == 1) return launch_t3_mt<1, 1, 1, 4>(a, s);
+        if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 1, 2, 4>(a, s);
+        return launch_t3_mt<1, 1, 4, 4>(a, s);
+    }
+    if (a.stride == 2) {
+        if (rsel == 1) return launch_t3_mt<2, 3, 1, 2>(a, s);
+        if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
+        return launch_t3_mt<2, 3, 2, 2>(a, s);
+    }
+    if (a.Cout <= 8) {  // plane pairs
+        if (rsel == 1) return launch_t3<1, 3, 1, 1, 4, true>(a, s, 1);
+        if (rsel == 2 || (rsel == 0 && vox < (1LL << 20))) return launch_t3<1, 3, 1, 2, 4, true>(a, s, 1);
+        return launch_t3<1, 3, 1, 4, 4, true>(a, s, 1);
+    }
+    if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
+    if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);
+    return launch_t3_mt<1, 3, 4, 4>(a, s);
+}
+
+}  // namespace conv
+}  // namespace esm

@@ -257,6 +257,43 @@ def test_conv_every_tile_variant(nd, cin, cout, k, s, tr):
         assert rel(run_conv(Ctx(DEV), p, xs, hint=0x114), ref) < 1e-5
 
 
+HINT_TILE3 = 1 << 23
+TILE3_CASES = [  # (cin, cout, k, s, shape, B): the L / M volumes' layer types, then ragged extents
+    (32, 8, 3, 1, (12, 24, 78), 1),    # group_stem (plane pairs)
+    (8, 8, 3, 1, (9, 13, 37), 2),      # agg, odd depth
+    (1, 8, 3, 1, (7, 10, 21), 1),      # corr_stem (one channel)
+    (24, 24, 3, 1, (6, 12, 39), 1),    # conv1.1 / agg_1.1
+    (40, 40, 3, 1, (5, 7, 19), 2),     # conv2.1 / agg_0.1
+    (72, 72, 3, 1, (3, 6, 20), 1),     # conv3.1: two cout groups
+    (8, 24, 3, 2, (12, 24, 78), 1),    # conv1.0
+    (24, 40, 3, 2, (7, 11, 33), 1),    # conv2.0, odd extents
+    (40, 72, 3, 2, (6, 12, 39), 2),    # conv3.0
+    (48, 24, 1, 1, (6, 12, 39), 1),    # agg_1.0 (one source)
+    (12, 16, 3, 1, (4, 5, 17), 1),
+]
+
+
+@pytest.mark.parametrize("cin,cout,k,s,shape,B", TILE3_CASES)
+def test_conv_tile3_form(cin, cout, k, s, shape, B):
+    """LDS-tiled implicit-GEMM 3-D form (conv_tile3.hip), every rows-per-wave variant (hint bits 26-27)
+    vs fp64 torch (relative 1e-5), and its general epilogue (residual, * mul broadcast over D, out2)."""
+    conv, bn = _mk(3, cin, cout, k, s, k // 2, seed=cin + cout)
+    x = torch.randn(B, cin, *shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    for rsel in (0, 1, 2, 3):
+        y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | (rsel << 26))
+        assert rel(y, ref) < 1e-5, rsel
+    res = torch.randn(ref.shape)
+    mul = torch.rand(B, cout, ref.shape[3], ref.shape[4]) + 0.5
+    want = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res)
+    out2 = torch.empty(ref.shape, device=DEV)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), mul=mul.to(DEV), out2=out2, post_scale2=2.0,
+                 hint=HINT_TILE3)
+    assert rel(y, want) < 1e-5
+    assert rel(out2, want * 2.0) < 1e-5
+
+
 HINT_SMALL = 1 << 21
 SMALL_CASES = [(3, [16], 16, 3, 1, False, (3, 6, 20)), (3, [24], 24, 3, 1, False, (2, 3, 10)),
                (3, [16], 24, 3, 2, False, (3, 6, 20)), (3, [12], 16, 3, 2, False, (6, 12, 39)),
