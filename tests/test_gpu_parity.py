@@ -970,9 +970,10 @@ def test_hot_path_reads_inputs_in_place(graph):
             assert torch.equal(out, expect(ml2, mr2, att, up2)), name
             out = model.hot_path(mr2, ml2, att, up2)[0]  # swapped
             assert torch.equal(out, expect(mr2, ml2, att, up2)), name
-            wide = torch.zeros(up2[0].shape[:-1] + (2 * up2[0].shape[-1],), device=DEV)
-            wide[..., ::2] = up2[0]
-            upn = [wide[..., ::2]] + up2[1:]  # non-contiguous: copied into the plan's own buffer
+            u0 = up2[0]
+            wide = torch.zeros((u0.shape[0], 2 * u0.shape[1]) + tuple(u0.shape[2:]), device=DEV)
+            wide[:, 1::2] = u0
+            upn = [wide[:, 1::2]] + up2[1:]  # non-contiguous (channel stride 2): copied into the plan's buffer
             out = model.hot_path(mr2, ml2, att, upn)[0]
             assert torch.equal(out, expect(mr2, ml2, att, upn)), name
             out = model.hot_path(ml, mr, att, up)[0]  # and back in place
