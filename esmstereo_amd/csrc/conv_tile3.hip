@@ -51,7 +51,9 @@ struct T3Geo {
     static constexpr int NR = (NT - 1) * S + K;           // input rows a wave reads per (dz, dx)
 };
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN>
+// NS: input sources (a channel concat of up to 3, 4-channel aligned splits; 1x1x1 only): every k-step
+// lies inside one source, whose descriptor and offsets are selected per k-step (wave-uniform)
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1>
 __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT>;
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
@@ -74,11 +76,21 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     constexpr int PAD = K == 3 ? 1 : 0;
     const int zi0 = zo0 * S - PAD, yi0 = yo0 * S - PAD, xi0 = xo0 * S - PAD;
 
+    // the sources (named fields, no runtime-indexed kernarg struct array: see DESIGN.md §4.5)
     const esm_src& s0 = a.src[0];
-    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
-        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const esm_src& s1 = a.src[NS > 1 ? 1 : 0];
+    const esm_src& s2 = a.src[NS > 2 ? 2 : 0];
+    auto rsrc = [&](const esm_src& q) {
+        return __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(q.ptr + b * q.sb), static_cast<short>(0),
+            4 * ((q.C - 1) * static_cast<int>(q.sc) + (a.Di - 1) * static_cast<int>(q.sd) +
+                 (a.Hi - 1) * static_cast<int>(q.sh) + a.Wi),
+            0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rs0 = rsrc(s0);
+    const __amdgpu_buffer_rsrc_t rs1 = NS > 1 ? rsrc(s1) : rs0;
+    const __amdgpu_buffer_rsrc_t rs2 = NS > 2 ? rsrc(s2) : rs0;
+    const int lo1 = s0.C, lo2 = s0.C + (NS > 1 ? s1.C : 0);  // first channel of sources 1 and 2
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.w), static_cast<short>(0), 4 * G::TAPS * a.cin_pad * a.cout_pad, 0x00020000);
 
@@ -86,14 +98,20 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     //      into the wave-uniform soffset)
     // slot k's element e = tid + 256 k: channel e / CS0, LDS index e + channel * (CS - CS0) (recomputed
     // from e where used: only the global offset is kept in a register)
-    unsigned xoff[XR];
+    unsigned xoff[NS][XR];
 #pragma unroll
     for (int k = 0; k < XR; ++k) {
         const int e = tid + k * kT3Threads;
         const int ix = e % IX, iy = (e / IX) % IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
         const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
         const bool ok = e < G::XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-        xoff[k] = ok ? 4u * static_cast<unsigned>(ci * sc + zi * sd + yi * sh + xi) : kOOB;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const esm_src& sq = q == 0 ? s0 : (q == 1 ? s1 : s2);
+            xoff[q][k] = ok ? 4u * static_cast<unsigned>(ci * static_cast<int>(sq.sc) + zi * static_cast<int>(sq.sd) +
+                                                         yi * static_cast<int>(sq.sh) + xi)
+                            : kOOB;
+        }
     }
     unsigned woff[WR];
     int wdst[WR];
@@ -121,10 +139,16 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     }
     float xv[XR], wv[WR];
     auto stage_load = [&](int c0) {
+        // the k-step's source (4-channel aligned splits: channels c0 .. c0 + 3 lie in one)
+        const int q = NS == 1 ? 0 : (c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2));
+        const __amdgpu_buffer_rsrc_t rq = q == 0 ? rs0 : (q == 1 ? rs1 : rs2);
+        const int cq = c0 - (q == 0 ? 0 : (q == 1 ? lo1 : lo2));
+        const int scq = static_cast<int>(q == 0 ? s0.sc : (q == 1 ? s1.sc : s2.sc));
 #pragma unroll
         for (int k = 0; k < XR; ++k) {
             const int ci = (tid + k * kT3Threads) / G::CS0;
-            xv[k] = buf_load_s(rs, c0 + ci < a.Cin ? xoff[k] : kOOB, 4 * c0 * sc);
+            const unsigned xo = NS == 1 ? xoff[0][k] : (q == 0 ? xoff[0][k] : (q == 1 ? xoff[NS > 1 ? 1 : 0][k] : xoff[NS - 1][k]));
+            xv[k] = buf_load_s(rq, c0 + ci < a.Cin ? xo : kOOB, 4 * cq * scq);
         }
 #pragma unroll
         for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
@@ -253,7 +277,233 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     }
 }
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ>
+// ConvTranspose3d k4 s2 p1 (the hourglass decoder steps conv3_up 72 -> 40 and conv2_up 40 -> 24,
+// models/ESMStereo.py:137-138,163-168), same LDS pipeline.  Output 2m + q per dim takes input m + q - t
+// with kernel index 1 - q + 2t (t = 0, 1): for one parity class it is a 2x2x2 conv over the input grid,
+// and every class of an m-tile reads the same (ZB+2) x (YB+2) x 18 input window, at window offset
+// d = 1 + q - t.  A workgroup owns one (qd, qh) class pair of an m-tile; each wave computes both qw
+// classes (window columns dx = 0..2 feed qw = 0 through tw = 1 - dx and qw = 1 through tw = 2 - dx), so
+// a lane holds the two adjacent output columns 2m, 2m + 1 and stores them as one 8-byte write.
+template <int MT, int NT, int ACT, bool PLAIN>
+__global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc a, int ncg) {
+    constexpr int WZ = 4, ZB = 4, YB = NT;
+    constexpr int IZ = ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
+    constexpr int CS = CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;
+    constexpr int XE = 4 * CS0, XL = 4 * CS;
+    constexpr int WCS = MT % 2 ? MT * 16 : MT * 16 + 16;
+    constexpr int WE = 16 * 4 * MT * 16, WL = 16 * 4 * WCS;  // [qw][tap 8][ci 4][m]
+    constexpr int XR = (XE + kT3Threads - 1) / kT3Threads, WR = (WE + kT3Threads - 1) / kT3Threads;
+    __shared__ __attribute__((aligned(16))) float xs[2][XL];
+    __shared__ __attribute__((aligned(16))) float ws[2][WL];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int zw = wave;
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
+    const int xm0 = bk_.x * 16, ym0 = bk_.y * YB;
+    const int nzb = (a.Di + ZB - 1) / ZB;
+    int zz = bk_.z;
+    const int cp = zz & 3;  // (qd, qh) class pair
+    zz >>= 2;
+    const int mg = zz % ncg;
+    const int r1 = zz / ncg;
+    const int b = r1 / nzb;
+    const int zm0 = (r1 - b * nzb) * ZB;
+    const int qd = cp >> 1, qh = cp & 1;
+    const int zi0 = zm0 - 1, yi0 = ym0 - 1, xi0 = xm0 - 1;
+
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
+        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), static_cast<short>(0), 4 * 64 * a.cin_pad * a.cout_pad, 0x00020000);
+
+    unsigned xoff[XR];
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int e = tid + k * kT3Threads;
+        const int ix = e % IX, iy = (e / IX) % IY, iz = (e / PLANE) % IZ, ci = e / CS0;
+        const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
+        const bool ok = e < XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+        xoff[k] = ok ? 4u * static_cast<unsigned>(ci * sc + zi * sd + yi * sh + xi) : kOOB;
+    }
+    // weights: packed w[cls][tap][cin_pad][cout_pad], cls = (qd, qh, qw) bits, tap = (td, th, tw) bits
+    unsigned woff[WR];
+    int wdst[WR];
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+        const int e = tid + k * kT3Threads;  // e = ((qw * 8 + tap) * 4 + ci) * (MT * 16) + m
+        const int m = e % (MT * 16), ci = (e / (MT * 16)) & 3, tq = e / (MT * 64);  // tq = qw * 8 + tap
+        const int cls = (cp << 1) | (tq >> 3), tap = tq & 7;
+        const int co = mg * MT * 16 + m;
+        const bool ok = e < WE && co < a.cout_pad;
+        woff[k] = ok ? 4u * static_cast<unsigned>(((cls * 8 + tap) * a.cin_pad + ci) * a.cout_pad + co) : kOOB;
+        wdst[k] = e < WE ? (tq * 4 + ci) * WCS + m : -1;
+    }
+    float xv[XR], wv[WR];
+    auto stage_load = [&](int c0) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int ci = (tid + k * kT3Threads) / CS0;
+            xv[k] = buf_load_s(rs, c0 + ci < a.Cin ? xoff[k] : kOOB, 4 * c0 * sc);
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int e = tid + k * kT3Threads;
+            if (e < XE) xs[buf][e + (e / CS0) * (CS - CS0)] = xv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k)
+            if (wdst[k] >= 0) ws[buf][wdst[k]] = wv[k];
+    };
+    float scl[MT][4], shf[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cc = min(mg * MT * 16 + mt * 16 + 4 * g + j, a.Cout - 1);
+            scl[mt][j] = a.scale ? a.scale[cc] : 1.f;
+            shf[mt][j] = a.shift ? a.shift[cc] : 0.f;
+        }
+    floatx4 acc[2][NT][MT];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[q][nt][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int nchunk = (a.Cin + 3) >> 2;
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nchunk) stage_load(4 * (ch + 1));
+        const float* xw = &xs[buf][g * CS + n];
+        const float* wp = &ws[buf][g * WCS + n];
+#pragma unroll
+        for (int td = 0; td < 2; ++td) {
+            const int dz = 1 + qd - td;  // window plane offset (wave-uniform)
+#pragma unroll
+            for (int th = 0; th < 2; ++th) {
+                const int dy = 1 + qh - th;
+                const float* xr = xw + (zw + dz) * PLANE + dy * IX;
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    float br[NT];
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) br[nt] = xr[nt * IX + dx];
+#pragma unroll
+                    for (int qw = 0; qw < 2; ++qw) {
+                        const int tw = 1 + qw - dx;
+                        if (tw < 0 || tw > 1) continue;
+                        const int tq = qw * 8 + (td * 4 + th * 2 + tw);
+                        float av[MT];
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) av[mt] = wp[tq * 4 * WCS + mt * 16];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                            for (int mt = 0; mt < MT; ++mt)
+                                acc[qw][nt][mt] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], br[nt], acc[qw][nt][mt], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (ch + 1 < nchunk) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane (g, n) holds output columns 2m, 2m + 1 (m = xm0 + n) of rows 4g + j
+    const int x = 2 * (xm0 + n);
+    const int z = 2 * (zm0 + zw) + qd;
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0),
+        4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
+             (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int y = 2 * (ym0 + nt) + qh;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = mg * MT * 16 + mt * 16 + 4 * g + j;
+                const bool ok = co < a.Cout && z < a.Do && y < a.Ho && x < a.Wo;
+                float v[2];
+#pragma unroll
+                for (int qw = 0; qw < 2; ++qw) {
+                    float t = acc[qw][nt][mt][j];
+                    t = a.scale ? t * scl[mt][j] + shf[mt][j] : t + shf[mt][j];
+                    v[qw] = act_t<ACT>(t, a.act);
+                }
+                if constexpr (PLAIN) {
+                    const unsigned o = ok ? 4u * static_cast<unsigned>(co * static_cast<int>(a.oc) +
+                                                                       z * static_cast<int>(a.od) +
+                                                                       y * static_cast<int>(a.oh) + x)
+                                          : kOOB;
+                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(v[0]), __float_as_uint(v[1])}, ro_,
+                                                          static_cast<int>(o), 0, kStoreAux);
+                } else {
+                    if (!ok) continue;
+#pragma unroll
+                    for (int qw = 0; qw < 2; ++qw) {
+                        float t = v[qw];
+                        if (a.res)
+                            t = t + a.res[b * a.rb + co * a.rc + static_cast<long long>(z) * a.rd +
+                                          static_cast<long long>(y) * a.rh + x + qw];
+                        const long long o = b * a.ob + co * a.oc + static_cast<long long>(z) * a.od +
+                                            static_cast<long long>(y) * a.oh + x + qw;
+                        a.out[o] = t * a.post_scale;
+                        if (a.out2) a.out2[o] = t * a.post_scale2;
+                    }
+                }
+            }
+    }
+}
+
+template <int MT, int NT>
+int launch_tt3(const esm_conv_desc& a, hipStream_t s, int ncg) {
+    const long long z = static_cast<long long>(a.B) * ((a.Di + 3) / 4) * ncg * 4;
+    const long long gy = ceil_div(a.Hi, NT);
+    if (z > 65535 || gy > 65535) return arg_error("conv(tile3 transposed): grid too large");
+    const dim3 grid(ceil_div(a.Wi, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
+    // the plain form stores 8-byte pairs: 8-byte aligned rows
+    const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
+                       (a.oh % 2) == 0 && (a.od % 2) == 0 && (a.oc % 2) == 0 &&
+                       (reinterpret_cast<uintptr_t>(a.out) & 7) == 0 &&
+                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
+                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (plain)
+        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, ESM_ACT_GELU, true>), grid, dim3(kT3Threads), 0, s, a, ncg);
+    else
+        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, -1, false>), grid, dim3(kT3Threads), 0, s, a, ncg);
+    return check_launch("conv(tile3 transposed)");
+}
+
+template <int NT>
+int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
+    const int tiles = (a.Cout + 15) / 16;
+    if (tiles == 1) return launch_tt3<1, NT>(a, s, 1);
+    if (tiles == 2) return launch_tt3<2, NT>(a, s, 1);
+    if (tiles == 3) return launch_tt3<3, NT>(a, s, 1);
+    if (tiles <= 4) return launch_tt3<2, NT>(a, s, 2);
+    if (tiles <= 6) return launch_tt3<3, NT>(a, s, 2);
+    return arg_error("conv(tile3 transposed): at most 96 output channels");
+}
+
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1>
 int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
@@ -264,25 +514,34 @@ int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS>), grid, dim3(kT3Threads), 0, s, a,
+                           ncg);
     else
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS>), grid, dim3(kT3Threads), 0, s, a, ncg);
     return check_launch("conv(tile3)");
 }
 
 // cout tiles per workgroup (MT) and cout groups (ncg) for Cout: MT * 16 * ncg >= Cout
-template <int S, int K, int NT, int WZ>
+template <int S, int K, int NT, int WZ, int NS = 1>
 int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
     const int tiles = (a.Cout + 15) / 16;
     if (tiles <= 3) {
-        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false>(a, s, 1);
-        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false>(a, s, 1);
-        return launch_t3<S, K, 3, NT, WZ, false>(a, s, 1);
+        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false, NS>(a, s, 1);
+        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false, NS>(a, s, 1);
+        return launch_t3<S, K, 3, NT, WZ, false, NS>(a, s, 1);
     }
     // 4+ tiles (72 couts: 5): two cout groups of ceil(tiles / 2) tiles
-    if (tiles <= 4) return launch_t3<S, K, 2, NT, WZ, false>(a, s, 2);
-    if (tiles <= 6) return launch_t3<S, K, 3, NT, WZ, false>(a, s, 2);
+    if (tiles <= 4) return launch_t3<S, K, 2, NT, WZ, false, NS>(a, s, 2);
+    if (tiles <= 6) return launch_t3<S, K, 3, NT, WZ, false, NS>(a, s, 2);
     return arg_error("conv(tile3): at most 96 output channels");
+}
+
+// 1x1x1 over 1..3 sources
+template <int NT>
+int launch_t3_k1(const esm_conv_desc& a, hipStream_t s) {
+    if (a.nsrc == 1) return launch_t3_mt<1, 1, NT, 4, 1>(a, s);
+    if (a.nsrc == 2) return launch_t3_mt<1, 1, NT, 4, 2>(a, s);
+    return launch_t3_mt<1, 1, NT, 4, 3>(a, s);
 }
 
 }  // namespace
@@ -291,11 +550,15 @@ int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
 // 32-bit buffer offsets.
 bool tile3_ok(const esm_conv_desc& a) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
-    if (!d3 || a.transposed || a.nsrc != 1 || a.up || a.shuffle > 1 || a.Cout > 96) return false;
+    if (a.transposed)  // ConvTranspose3d k4 s2 p1, one source, >= 2 couts (one output: convt_c1)
+        return d3 && a.kd == 4 && a.kh == 4 && a.stride == 2 && a.nsrc == 1 && !a.up && !a.mul && a.Cout > 1 &&
+               a.Cout <= 96 && a.cout_pad >= 16 * ((a.Cout + 15) / 16) && direct_ok(a);
+    if (!d3 || a.up || a.shuffle > 1 || a.Cout > 96) return false;
     const bool k3 = a.kd == 3 && a.kh == 3 && a.kw == 3 && a.pd == 1 && a.ph == 1 && a.pw == 1 &&
                     (a.stride == 1 || a.stride == 2);
     const bool k1 = a.kd == 1 && a.kh == 1 && a.kw == 1 && a.pd == 0 && a.ph == 0 && a.pw == 0 && a.stride == 1;
     if (!k3 && !k1) return false;
+    if (a.nsrc != 1 && !k1) return false;  // channel concats: 1x1x1 only (the hourglass's agg_0.0 / agg_1.0)
     if (a.cout_pad < 16 * ((a.Cout + 15) / 16)) return false;
     return direct_ok(a);
 }
@@ -306,7 +569,7 @@ bool tile3_ok(const esm_conv_desc& a) {
 bool tile3_auto(const esm_conv_desc& a) {
     if (!tile3_ok(a)) return false;
     const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
-    return vox >= (1LL << 17);
+    return vox >= (a.transposed ? (1LL << 16) : (1LL << 17));
 }
 
 // hint bits 26-27 with TILE3 (bit 23): rows per wave 1 / 2 / 4 (0 = automatic)
@@ -314,10 +577,15 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     if (!tile3_ok(a)) return arg_error("conv: tile3-form hint not applicable");
     const int rsel = (a.hint >> 26) & 3;
     const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
+    if (a.transposed) {
+        if (rsel == 1) return launch_tt3_mt<1>(a, s);
+        if (rsel == 3) return launch_tt3_mt<4>(a, s);
+        return launch_tt3_mt<2>(a, s);
+    }
     if (a.kh == 1) {
-        if (rsel == 1) return launch_t3_mt<1, 1, 1, 4>(a, s);
-        if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 1, 2, 4>(a, s);
-        return launch_t3_mt<1, 1, 4, 4>(a, s);
+        if (rsel == 1) return launch_t3_k1<1>(a, s);
+        if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_k1<2>(a, s);
+        return launch_t3_k1<4>(a, s);
     }
     if (a.stride == 2) {
         if (rsel == 1) return launch_t3_mt<2, 3, 1, 2>(a, s);

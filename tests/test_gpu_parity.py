@@ -294,6 +294,40 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
     assert rel(out2, want * 2.0) < 1e-5
 
 
+@pytest.mark.parametrize("cin,cout,shape,B", [(40, 24, (6, 12, 39), 1), (72, 40, (3, 6, 20), 2), (24, 16, (5, 7, 17), 1),
+                                              (40, 72, (3, 5, 9), 1), (16, 2, (4, 4, 20), 1)])
+def test_conv_tile3_transposed(cin, cout, shape, B):
+    """The tile3 ConvTranspose3d k4 s2 p1 form (the hourglass's conv3_up / conv2_up; both qw classes per
+    wave, 8-byte stores) vs fp64 torch, every rows-per-wave variant, plain and general epilogues."""
+    conv, bn = _mk(3, cin, cout, 4, 2, 1, transposed=True, seed=cin * 3 + cout)
+    x = torch.randn(B, cin, *shape)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    for rsel in (0, 1, 3):
+        y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | (rsel << 26))
+        assert rel(y, ref) < 1e-5, rsel
+    res = torch.randn(ref.shape)
+    want = _ref_conv([x], conv, bn, ACT_GELU, res=res)
+    y = run_conv(Ctx(DEV), p, [x.to(DEV)], res=res.to(DEV), hint=HINT_TILE3)
+    assert rel(y, want) < 1e-5
+
+
+@pytest.mark.parametrize("cins,cout,shape", [((24, 24), 24, (6, 12, 39)), ((16, 16, 8), 16, (3, 7, 21)),
+                                             ((40, 40), 40, (5, 6, 20))])
+def test_conv_tile3_multisource_crop(cins, cout, shape):
+    """The tile3 1x1x1 form over a channel concat with a cropped source (the hourglass's agg_1.0 /
+    agg_0.0: cat(conv_up(x)[..., :D, :H, :W], skip)), vs fp64 torch."""
+    conv, bn = _mk(3, sum(cins), cout, 1, 1, 0, seed=sum(cins))
+    big = torch.randn(2, cins[0], shape[0] + 1, shape[1] + 2, shape[2] + 3)
+    xs = [big[:, :, :shape[0], :shape[1], :shape[2]]] + [torch.randn(2, c, *shape) for c in cins[1:]]
+    ref = _ref_conv(xs, conv, bn, ACT_GELU)
+    bigd = big.to(DEV)
+    xd = [bigd[:, :, :shape[0], :shape[1], :shape[2]]] + [x.to(DEV) for x in xs[1:]]
+    for rsel in (0, 1, 2, 3):
+        y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), xd, hint=HINT_TILE3 | (rsel << 26))
+        assert rel(y, ref) < 1e-5, rsel
+
+
 HINT_SMALL = 1 << 21
 SMALL_CASES = [(3, [16], 16, 3, 1, False, (3, 6, 20)), (3, [24], 24, 3, 1, False, (2, 3, 10)),
                (3, [16], 24, 3, 2, False, (3, 6, 20)), (3, [12], 16, 3, 2, False, (6, 12, 39)),
