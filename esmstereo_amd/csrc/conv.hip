@@ -23,6 +23,8 @@ bool widet_ok(const esm_conv_desc& a);                    // conv_widet.hip
 int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
 bool tile3_auto(const esm_conv_desc& a);                 // conv_tile3.hip
 int launch_tile3(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
+bool tile2_auto(const esm_conv_desc& a);                 // conv_tile3.hip
+int launch_tile2(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
@@ -98,9 +100,9 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         return launch_conv(&d, s);
     }
     if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
-    if (a.hint & kHintTile3) return conv::launch_tile3(a, s);
-    // the MFMA-bound 3-D volumes of ESMStereo-L / -M (>= 2^17 output voxels): the LDS-tiled form
-    if (form == 0 && conv::tile3_auto(a)) return conv::launch_tile3(a, s);
+    if (a.hint & kHintTile3) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
+    // the MFMA-bound 3-D volumes / 2-D maps of ESMStereo-L / -M: the LDS-tiled form
+    if (form == 0 && (d3 ? conv::tile3_auto(a) : conv::tile2_auto(a))) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

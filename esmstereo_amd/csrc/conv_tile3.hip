@@ -30,19 +30,21 @@ namespace {
 
 constexpr int kT3Threads = 256;
 
-template <int S, int K, int NT, int WZ, bool PZ, int MT>
+// D2: a 2-D conv (one plane, kd = 1): the same pipeline with the depth dimension of extent 1
+template <int S, int K, int NT, int WZ, bool PZ, int MT, bool D2 = false>
 struct T3Geo {
     static constexpr int WY = 4 / WZ;                     // waves along y
     static constexpr int ZB = PZ ? 2 * WZ : WZ;           // output planes per workgroup
     static constexpr int YB = WY * NT;                    // output rows per workgroup
-    static constexpr int IZ = (ZB - 1) * S + K, IY = (YB - 1) * S + K, IX = 15 * S + K;  // input window
+    static constexpr int KD = D2 ? 1 : K;                 // depth taps
+    static constexpr int IZ = D2 ? 1 : (ZB - 1) * S + K, IY = (YB - 1) * S + K, IX = 15 * S + K;  // input window
     static constexpr int PLANE = IY * IX;
     static constexpr int CS0 = IZ * PLANE;
     static constexpr int CMOD = S == 1 ? 16 : 1;          // channel stride mod 32 (bank offset of lanes 16..31)
     static constexpr int CS = CS0 + ((CMOD - CS0 % 32) % 32 + 32) % 32;
     static constexpr int XE = 4 * CS0;                    // staged input elements per k-step
     static constexpr int XL = 4 * CS;                     // LDS floats per input buffer
-    static constexpr int TAPS = K * K * K;
+    static constexpr int TAPS = KD * K * K;
     static constexpr int WCS = PZ ? 16 : (MT % 2 ? MT * 16 : MT * 16 + 16);  // weight row stride (= 16 mod 32)
     static constexpr int WE = PZ ? 4 * 9 * 4 * 16 : TAPS * 4 * MT * 16;      // staged weight elements
     static constexpr int WL = PZ ? WE : TAPS * 4 * WCS;                      // LDS floats per weight buffer
@@ -53,9 +55,9 @@ struct T3Geo {
 
 // NS: input sources (a channel concat of up to 3, 4-channel aligned splits; 1x1x1 only): every k-step
 // lies inside one source, whose descriptor and offsets are selected per k-step (wave-uniform)
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false>
 __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
-    using G = T3Geo<S, K, NT, WZ, PZ, MT>;
+    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
     constexpr int XR = G::XR, WR = G::WR, NR = G::NR;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
@@ -73,24 +75,38 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     const int r1 = zz / ncg;
     const int b = r1 / nzb;
     const int zo0 = (r1 - b * nzb) * G::ZB;
-    constexpr int PAD = K == 3 ? 1 : 0;
-    const int zi0 = zo0 * S - PAD, yi0 = yo0 * S - PAD, xi0 = xo0 * S - PAD;
+    const int zi0 = D2 ? 0 : zo0 * S - a.pd, yi0 = yo0 * S - a.ph, xi0 = xo0 * S - a.pw;
 
-    // the sources (named fields, no runtime-indexed kernarg struct array: see DESIGN.md §4.5)
-    const esm_src& s0 = a.src[0];
-    const esm_src& s1 = a.src[NS > 1 ? 1 : 0];
-    const esm_src& s2 = a.src[NS > 2 ? 2 : 0];
-    auto rsrc = [&](const esm_src& q) {
-        return __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(q.ptr + b * q.sb), static_cast<short>(0),
-            4 * ((q.C - 1) * static_cast<int>(q.sc) + (a.Di - 1) * static_cast<int>(q.sd) +
-                 (a.Hi - 1) * static_cast<int>(q.sh) + a.Wi),
-            0x00020000);
+    // the sources as opaque wave-uniform scalars: selecting between fields of a.src[0..2] by the k-step's
+    // source lets the optimizer fold the select into a run-time index of the kernarg struct, which it then
+    // copies to scratch; read through readfirstlane, the fields cannot be merged
+    auto u32 = [](int v) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(v); };
+    auto u64 = [&](long long v) __attribute__((always_inline)) {
+        const unsigned long long w = static_cast<unsigned long long>(v);
+        return static_cast<long long>((static_cast<unsigned long long>(static_cast<unsigned>(u32(static_cast<int>(w >> 32))))
+                                       << 32) |
+                                      static_cast<unsigned>(u32(static_cast<int>(w & 0xffffffffu))));
     };
-    const __amdgpu_buffer_rsrc_t rs0 = rsrc(s0);
-    const __amdgpu_buffer_rsrc_t rs1 = NS > 1 ? rsrc(s1) : rs0;
-    const __amdgpu_buffer_rsrc_t rs2 = NS > 2 ? rsrc(s2) : rs0;
-    const int lo1 = s0.C, lo2 = s0.C + (NS > 1 ? s1.C : 0);  // first channel of sources 1 and 2
+    auto uptr = [&](const float* ptr) __attribute__((always_inline)) {
+        return reinterpret_cast<const float*>(u64(static_cast<long long>(reinterpret_cast<uintptr_t>(ptr))));
+    };
+    const float* p0 = a.src[0].ptr;
+    const float* p1 = NS > 1 ? uptr(a.src[1].ptr) : p0;
+    const float* p2 = NS > 2 ? uptr(a.src[2].ptr) : p0;
+    const int C0 = a.src[0].C, C1 = NS > 1 ? u32(a.src[1].C) : 0, C2 = NS > 2 ? u32(a.src[2].C) : 0;
+    const int sc0 = static_cast<int>(a.src[0].sc), sd0 = static_cast<int>(a.src[0].sd), sh0 = static_cast<int>(a.src[0].sh);
+    const int sc1 = NS > 1 ? u32(static_cast<int>(a.src[1].sc)) : sc0, sd1 = NS > 1 ? u32(static_cast<int>(a.src[1].sd)) : sd0,
+              sh1 = NS > 1 ? u32(static_cast<int>(a.src[1].sh)) : sh0;
+    const int sc2 = NS > 2 ? u32(static_cast<int>(a.src[2].sc)) : sc0, sd2 = NS > 2 ? u32(static_cast<int>(a.src[2].sd)) : sd0,
+              sh2 = NS > 2 ? u32(static_cast<int>(a.src[2].sh)) : sh0;
+    const long long sb0 = a.src[0].sb, sb1 = NS > 1 ? u64(a.src[1].sb) : sb0, sb2 = NS > 2 ? u64(a.src[2].sb) : sb0;
+    auto rsrc = [&](const float* ptr, long long sb, int C, int sc, int sd, int sh) __attribute__((always_inline)) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr + b * sb), static_cast<short>(0),
+                                                 4 * ((C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi),
+                                                 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rs0 = rsrc(p0, sb0, C0, sc0, sd0, sh0);
+    const int lo1 = C0, lo2 = C0 + C1;  // first channel of sources 1 and 2
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.w), static_cast<short>(0), 4 * G::TAPS * a.cin_pad * a.cout_pad, 0x00020000);
 
@@ -107,10 +123,9 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         const bool ok = e < G::XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-            const esm_src& sq = q == 0 ? s0 : (q == 1 ? s1 : s2);
-            xoff[q][k] = ok ? 4u * static_cast<unsigned>(ci * static_cast<int>(sq.sc) + zi * static_cast<int>(sq.sd) +
-                                                         yi * static_cast<int>(sq.sh) + xi)
-                            : kOOB;
+            const int scq = q == 0 ? sc0 : (q == 1 ? sc1 : sc2), sdq = q == 0 ? sd0 : (q == 1 ? sd1 : sd2);
+            const int shq = q == 0 ? sh0 : (q == 1 ? sh1 : sh2);
+            xoff[q][k] = ok ? 4u * static_cast<unsigned>(ci * scq + zi * sdq + yi * shq + xi) : kOOB;
         }
     }
     unsigned woff[WR];
@@ -138,22 +153,33 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         wdst[k] = dst;
     }
     float xv[XR], wv[WR];
-    auto stage_load = [&](int c0) {
-        // the k-step's source (4-channel aligned splits: channels c0 .. c0 + 3 lie in one)
-        const int q = NS == 1 ? 0 : (c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2));
-        const __amdgpu_buffer_rsrc_t rq = q == 0 ? rs0 : (q == 1 ? rs1 : rs2);
-        const int cq = c0 - (q == 0 ? 0 : (q == 1 ? lo1 : lo2));
-        const int scq = static_cast<int>(q == 0 ? s0.sc : (q == 1 ? s1.sc : s2.sc));
+    // the k-step's loads from source Q (compile-time: every array index stays constant; a run-time select
+    // between xoff[0][k] and xoff[1][k] becomes a dynamic index of a private array, i.e. scratch)
+    auto load_src = [&](auto qc, int c0) __attribute__((always_inline)) {
+        constexpr int Q = decltype(qc)::value;
+        const __amdgpu_buffer_rsrc_t rq =
+            Q == 0 ? rs0 : (Q == 1 ? rsrc(p1, sb1, C1, sc1, sd1, sh1) : rsrc(p2, sb2, C2, sc2, sd2, sh2));
+        const int cq = c0 - (Q == 0 ? 0 : (Q == 1 ? lo1 : lo2));
+        const int scq = Q == 0 ? sc0 : (Q == 1 ? sc1 : sc2);
 #pragma unroll
         for (int k = 0; k < XR; ++k) {
             const int ci = (tid + k * kT3Threads) / G::CS0;
-            const unsigned xo = NS == 1 ? xoff[0][k] : (q == 0 ? xoff[0][k] : (q == 1 ? xoff[NS > 1 ? 1 : 0][k] : xoff[NS - 1][k]));
-            xv[k] = buf_load_s(rq, c0 + ci < a.Cin ? xo : kOOB, 4 * cq * scq);
+            xv[k] = buf_load_s(rq, c0 + ci < a.Cin ? xoff[Q][k] : kOOB, 4 * cq * scq);
+        }
+    };
+    auto stage_load = [&](int c0) __attribute__((always_inline)) {
+        // the k-step's source (4-channel aligned splits: channels c0 .. c0 + 3 lie in one); uniform branch
+        if (NS == 1 || c0 < lo1) {
+            load_src(std::integral_constant<int, 0>{}, c0);
+        } else if (NS == 2 || c0 < lo2) {
+            load_src(std::integral_constant<int, (NS > 1 ? 1 : 0)>{}, c0);
+        } else {
+            load_src(std::integral_constant<int, (NS > 2 ? 2 : 0)>{}, c0);
         }
 #pragma unroll
         for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
     };
-    auto stage_store = [&](int buf) {
+    auto stage_store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < XR; ++k) {
             const int e = tid + k * kT3Threads;
@@ -211,7 +237,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         } else {
             const float* wp = &ws[buf][g * WCS + n];
 #pragma unroll
-            for (int dz = 0; dz < K; ++dz)
+            for (int dz = 0; dz < G::KD; ++dz)
 #pragma unroll
                 for (int dx = 0; dx < K; ++dx) {
                     float br[NR];
@@ -344,7 +370,7 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
         wdst[k] = e < WE ? (tq * 4 + ci) * WCS + m : -1;
     }
     float xv[XR], wv[WR];
-    auto stage_load = [&](int c0) {
+    auto stage_load = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < XR; ++k) {
             const int ci = (tid + k * kT3Threads) / CS0;
@@ -353,7 +379,7 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
 #pragma unroll
         for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
     };
-    auto stage_store = [&](int buf) {
+    auto stage_store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < XR; ++k) {
             const int e = tid + k * kT3Threads;
@@ -503,9 +529,9 @@ int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
     return arg_error("conv(tile3 transposed): at most 96 output channels");
 }
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false>
 int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
-    using G = T3Geo<S, K, NT, WZ, PZ, MT>;
+    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
     const long long gy = ceil_div(a.Ho, G::YB);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3): grid too large");
@@ -514,25 +540,25 @@ int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS>), grid, dim3(kT3Threads), 0, s, a,
-                           ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2>), grid, dim3(kT3Threads), 0, s,
+                           a, ncg);
     else
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2>), grid, dim3(kT3Threads), 0, s, a, ncg);
     return check_launch("conv(tile3)");
 }
 
 // cout tiles per workgroup (MT) and cout groups (ncg) for Cout: MT * 16 * ncg >= Cout
-template <int S, int K, int NT, int WZ, int NS = 1>
+template <int S, int K, int NT, int WZ, int NS = 1, bool D2 = false>
 int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
     const int tiles = (a.Cout + 15) / 16;
     if (tiles <= 3) {
-        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false, NS>(a, s, 1);
-        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false, NS>(a, s, 1);
-        return launch_t3<S, K, 3, NT, WZ, false, NS>(a, s, 1);
+        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false, NS, D2>(a, s, 1);
+        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false, NS, D2>(a, s, 1);
+        return launch_t3<S, K, 3, NT, WZ, false, NS, D2>(a, s, 1);
     }
     // 4+ tiles (72 couts: 5): two cout groups of ceil(tiles / 2) tiles
-    if (tiles <= 4) return launch_t3<S, K, 2, NT, WZ, false, NS>(a, s, 2);
-    if (tiles <= 6) return launch_t3<S, K, 3, NT, WZ, false, NS>(a, s, 2);
+    if (tiles <= 4) return launch_t3<S, K, 2, NT, WZ, false, NS, D2>(a, s, 2);
+    if (tiles <= 6) return launch_t3<S, K, 3, NT, WZ, false, NS, D2>(a, s, 2);
     return arg_error("conv(tile3): at most 96 output channels");
 }
 
@@ -544,7 +570,48 @@ int launch_t3_k1(const esm_conv_desc& a, hipStream_t s) {
     return launch_t3_mt<1, 1, NT, 4, 3>(a, s);
 }
 
+// 2-D: 4 waves along y (NT rows each), 1..3 sources
+template <int S, int K, int NT>
+int launch_t2_ns(const esm_conv_desc& a, hipStream_t s) {
+    if (a.nsrc == 1) return launch_t3_mt<S, K, NT, 1, 1, true>(a, s);
+    if (a.nsrc == 2) return launch_t3_mt<S, K, NT, 1, 2, true>(a, s);
+    return launch_t3_mt<S, K, NT, 1, 3, true>(a, s);
+}
+
+template <int S, int K>
+int launch_t2_nt(const esm_conv_desc& a, hipStream_t s) {
+    const int rsel = (a.hint >> 26) & 3;
+    if (rsel == 1) return launch_t2_ns<S, K, 1>(a, s);
+    if (rsel == 3) return launch_t2_ns<S, K, 4>(a, s);
+    if (rsel == 2) return launch_t2_ns<S, K, 2>(a, s);
+    const long long px = static_cast<long long>(a.B) * a.Ho * a.Wo;
+    return px >= (1LL << 18) ? launch_t2_ns<S, K, 4>(a, s) : launch_t2_ns<S, K, 2>(a, s);
+}
+
 }  // namespace
+
+// 2-D (the upsamplers' large maps at ESMStereo-L / -M): k3 stride 1 / 2 or k1 stride 1, any padding, 1..3
+// sources, <= 96 couts
+bool tile2_ok(const esm_conv_desc& a) {
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    if (d3 || a.transposed || a.up || a.shuffle > 1 || a.Cout > 96) return false;
+    if (!((a.kh == 3 && (a.stride == 1 || a.stride == 2)) || (a.kh == 1 && a.stride == 1))) return false;
+    if (a.cout_pad < 16 * ((a.Cout + 15) / 16)) return false;
+    return direct_ok(a);
+}
+
+bool tile2_auto(const esm_conv_desc& a) {
+    if (!tile2_ok(a) || a.Cin < 4) return false;  // one input channel: the VALU form (conv_stem.hip c1in)
+    const long long units = static_cast<long long>(a.B) * a.Ho * a.Wo * ((a.Cout + 15) / 16);
+    return units >= (1LL << 19);
+}
+
+int launch_tile2(const esm_conv_desc& a, hipStream_t s) {
+    if (!tile2_ok(a)) return arg_error("conv: tile2-form hint not applicable");
+    if (a.kh == 1) return launch_t2_nt<1, 1>(a, s);
+    if (a.stride == 2) return launch_t2_nt<2, 3>(a, s);
+    return launch_t2_nt<1, 3>(a, s);
+}
 
 // 3-D, one source, 3x3x3 stride 1 / 2 padding 1 or 1x1x1 stride 1 padding 0, <= 96 couts, spans within
 // 32-bit buffer offsets.

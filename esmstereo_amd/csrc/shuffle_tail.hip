@@ -311,20 +311,8 @@ __global__ void __launch_bounds__(64 * L) shuffle_tail4_kernel(const esm_shuffle
             *reinterpret_cast<conv::floatx4*>(&sh[c][1 + 4 * wave + g][4 + 4 * n]) = o;
         }
     }
-    // ---- the ring (VALU): ring rows 0 and SR - 1 over cols 3..68, ring cols 3 and 68 over rows 1..TR
-    constexpr int RROW = SC - 6;  // 66 columns per ring row
-    constexpr int NRING = 2 * RROW + 2 * G::TR;
-    for (int i = tid; i < NF * NRING; i += NT) {
-        const int c = i / NRING, q = i - c * NRING;
-        int tr, tc;
-        if (q < 2 * RROW) {
-            tr = q < RROW ? 0 : SR - 1;
-            tc = 3 + (q < RROW ? q : q - RROW);
-        } else {
-            const int e = q - 2 * RROW;
-            tr = 1 + (e < G::TR ? e : e - G::TR);
-            tc = e < G::TR ? 3 : 68;
-        }
+    // ---- the ring (VALU): ring rows 0 and SR - 1 over cols 3..68, then ring cols 3 and 68 over rows 1..TR
+    auto ring_value = [&](int c, int tr, int tc) __attribute__((always_inline)) {
         const int Y = Y0 - 1 + tr, X = X0 - 4 + tc;
         float v = 0.f;
         if (Y >= 0 && Y < HO && X >= 0 && X < WO) {
@@ -336,25 +324,44 @@ __global__ void __launch_bounds__(64 * L) shuffle_tail4_kernel(const esm_shuffle
             v = silu_fast(acc + wsh[G::OW_UB + m]);
         }
         sh[c][tr][tc] = v;
+    };
+    constexpr int RROW = SC - 6;  // 66 columns per ring row
+    for (int i = tid; i < NF * 2 * RROW; i += NT) {
+        const int c = i / (2 * RROW), q = i - c * (2 * RROW);
+        const int bot = q >= RROW;
+        ring_value(c, bot ? SR - 1 : 0, 3 + q - bot * RROW);
+    }
+    for (int i = tid; i < NF * 2 * G::TR; i += NT) {
+        const int c = i / (2 * G::TR), q = i - c * (2 * G::TR);
+        const int right = q >= G::TR;
+        ring_value(c, 1 + q - right * G::TR, right ? 68 : 3);
     }
     __syncthreads();
 
     // ---- 3x3 tail: lane (g, n) of wave w -> output row 4w + g, columns 4n .. 4n + 3
     const int oy = Y0 + 4 * wave + g, ox = X0 + 4 * n;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    // a lane's own 4 columns are one conflict-free 16-byte read; its neighbours' edge columns come from
+    // lanes n -+ 1 by DPP row shifts, except at the strip's ends (n = 0, 15), which read the ring column
+    // (every other lane reads the same ring word: a broadcast).  The 4-byte reads at stride 4 words this
+    // replaces were 4-way bank conflicts (SQ_LDS_BANK_CONFLICT 1.0 M cycles per launch at S-K)
+    const int edge = n == 0 ? 3 : 68;
 #pragma unroll 2
     for (int c = 0; c < NF; ++c) {
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
             const float* row = &sh[c][4 * wave + g + ky][0];
             float v[6];
-            v[0] = row[3 + 4 * n];
             const conv::floatx4 mid4 = *reinterpret_cast<const conv::floatx4*>(row + 4 + 4 * n);
+            const float ev = row[edge];
+            const float lf = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mid4[3]), 0x111, 0xf, 0xf, false));
+            const float rt = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mid4[0]), 0x101, 0xf, 0xf, false));
+            v[0] = n == 0 ? ev : lf;   // row_shr:1 -> lane n - 1's column 3
             v[1] = mid4[0];
             v[2] = mid4[1];
             v[3] = mid4[2];
             v[4] = mid4[3];
-            v[5] = row[8 + 4 * n];
+            v[5] = n == 15 ? ev : rt;  // row_shl:1 -> lane n + 1's column 0
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
                 const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];

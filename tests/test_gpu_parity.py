@@ -312,6 +312,40 @@ def test_conv_tile3_transposed(cin, cout, shape, B):
     assert rel(y, want) < 1e-5
 
 
+TILE2_CASES = [  # (cins, cout, k, s, p, H, W, B): the L / M upsamplers' 2-D layers, then ragged / odd ones
+    ((32, 32), 32, 3, 1, 1, 48, 156, 1),       # spx_4x.0: cat(d, feature)
+    ((32, 32, 32), 32, 1, 1, 0, 24, 78, 2),    # ref agg_1.0: 1x1 over three sources
+    ((32,), 32, 3, 2, 1, 48, 156, 1),          # conv2.0 (stride 2)
+    ((32,), 32, 1, 1, 1, 20, 62, 1),           # dm.3 (1x1, padding 1: the map grows)
+    ((16,), 8, 3, 1, 1, 33, 70, 1),            # spx_4x.1 at S
+    ((16,), 16, 3, 1, 1, 37, 45, 2),
+    ((1,), 32, 3, 2, 1, 29, 41, 1),            # one input channel (forced)
+    ((24, 16), 40, 3, 1, 1, 9, 23, 1),
+]
+
+
+@pytest.mark.parametrize("cins,cout,k,s,p,H,W,B", TILE2_CASES)
+def test_conv_tile2_form(cins, cout, k, s, p, H, W, B):
+    """The LDS-tiled form for 2-D convs (conv_tile3.hip with one plane): every rows-per-wave variant vs fp64
+    torch (relative 1e-5), with a cropped first source, and the general epilogue (residual, out2)."""
+    conv, bn = _mk(2, sum(cins), cout, k, s, p, seed=sum(cins) + H)
+    big = torch.randn(B, cins[0], H + 2, W + 3)
+    xs = [big[:, :, :H, :W]] + [torch.randn(B, c, H, W) for c in cins[1:]]
+    ref = _ref_conv(xs, conv, bn, ACT_GELU)
+    bigd = big.to(DEV)
+    xd = [bigd[:, :, :H, :W]] + [x.to(DEV) for x in xs[1:]]
+    pc = pk(conv, bn, ACT_GELU)
+    for rsel in (0, 1, 2, 3):
+        y = run_conv(Ctx(DEV), pc, xd, hint=HINT_TILE3 | (rsel << 26))
+        assert rel(y, ref) < 1e-5, rsel
+    res = torch.randn(ref.shape)
+    want = _ref_conv(xs, conv, bn, ACT_GELU, res=res)
+    out2 = torch.empty(ref.shape, device=DEV)
+    y = run_conv(Ctx(DEV), pc, xd, res=res.to(DEV), out2=out2, post_scale2=0.5, hint=HINT_TILE3)
+    assert rel(y, want) < 1e-5
+    assert rel(out2, want * 0.5) < 1e-5
+
+
 @pytest.mark.parametrize("cins,cout,shape", [((24, 24), 24, (6, 12, 39)), ((16, 16, 8), 16, (3, 7, 21)),
                                              ((40, 40), 40, (5, 6, 20))])
 def test_conv_tile3_multisource_crop(cins, cout, shape):
