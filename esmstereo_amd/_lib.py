@@ -63,7 +63,7 @@ class EsmFmnetDesc(Structure):
                 ("dw_k", c_int32), ("reserved", c_int32), ("stage", EsmSmixStage * 4),
                 ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32),
                 ("conv0_w", c_void_p), ("conv0_b", c_void_p), ("conv2_w", c_void_p), ("conv2_b", c_void_p),
-                ("hid", c_int32), ("reserved2", c_int32)]
+                ("hid", c_int32), ("reserved2", c_int32), ("work", c_void_p)]
 
 
 class EsmShuffleTailDesc(Structure):

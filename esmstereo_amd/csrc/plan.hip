@@ -237,7 +237,7 @@ struct esm_plan {
                 int n = rb(op.fm.x) + rb(op.fm.out);
                 for (int k = 0; k < 2; ++k) n += rb(op.fm.dw_w[k]) + rb(op.fm.dw_b[k]);
                 for (int k = 0; k < 4; ++k) n += rb.stage(op.fm.stage[k]);
-                return n + rb(op.fm.conv0_w) + rb(op.fm.conv0_b) + rb(op.fm.conv2_w) + rb(op.fm.conv2_b);
+                return n + rb(op.fm.conv0_w) + rb(op.fm.conv0_b) + rb(op.fm.conv2_w) + rb(op.fm.conv2_b) + rb(op.fm.work);
             }
             case kShuffleTail: return rb.tail(op.st);
             case kShuffleConv:

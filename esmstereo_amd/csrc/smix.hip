@@ -547,6 +547,353 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The whole FMBlock as TWO launches for large maps (esm_fmnet_desc.work given): the block split at its
+// second depthwise conv, so each launch recomputes only a 3-pixel halo (the fused form above recomputes
+// the t1 region 10.6x its tile at L-K, whose halo is the whole block's 7 + 1 pixels), and FMBlock.conv on
+// the fp32 matrix cores (the fused form ran its 9C x (C+16) and (C+16) x C GEMMs on the VALU from LDS):
+//   fm2a: t1 = mlp1_0(x) on tile + 3, dw0 on the tile, d = mlp1_1(mlp2_0(.)) -> work
+//   fm2b: dw1(d) on tile + 1, t3 = mlp2_1(.) + x, h = silu(conv0(t3) + b0) (MFMA), out = conv2(h) + b2 + t3
+//         (MFMA); t3 stays in LDS.
+// Per pixel and channel the per-pixel chain and the depthwise convs run the operations of the fused
+// form in its order; the two GEMMs sum over (tap, channel) k-steps in MFMA order (rel. 1e-5 vs the chain).
+constexpr int kF2TH = 8, kF2TW = 32;  // output tile: 256 pixels, 4 waves
+typedef float f2x4 __attribute__((ext_vector_type(4)));
+constexpr int kF2Threads = 256;
+
+// the mlp stage weights (SmixLayout blocks), the depthwise weights and bias: staged in LDS by the
+// launch's first loads (index order of fmnet_kernel's warm-up)
+template <int C, int NSTAGE>
+__device__ __forceinline__ void f2_stage_weights(const esm_fmnet_desc& a, const float* dww, const float* dwb,
+                                                 float (&rw)[(NSTAGE * SmixLayout<C>::STAGE + C * 49 + C +
+                                                               kF2Threads - 1) / kF2Threads]) {
+    using Lyt = SmixLayout<C>;
+    constexpr int NW = NSTAGE * Lyt::STAGE + C * 49 + C;
+    constexpr int NWR = (NW + kF2Threads - 1) / kF2Threads;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NWR; ++k) {
+        const int i = tid + k * kF2Threads;
+        const float* p = nullptr;
+        int off = 0;
+        // stage s's fields with a compile-time index (a run-time a.stage[i / STAGE] puts the kernarg
+        // struct in scratch)
+        static_for<0, NSTAGE>([&](auto sc) {
+            constexpr int S = decltype(sc)::value;
+            const int j = i - S * Lyt::STAGE;
+            if (j >= 0 && j < Lyt::STAGE) {
+                const esm_smix_stage& g = a.stage[S];
+                p = j < Lyt::F0W ? g.ln_w : j < Lyt::F0B ? g.fc0_w : j < Lyt::F2W ? g.fc0_b : j < Lyt::F2B ? g.fc2_w : g.fc2_b;
+                off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
+            }
+        });
+        if (i >= NSTAGE * Lyt::STAGE && i < NW) {
+            const int j = i - NSTAGE * Lyt::STAGE;
+            p = j < C * 49 ? dww : dwb;
+            off = j < C * 49 ? j : j - C * 49;
+        }
+        rw[k] = (p ? p : dww)[p ? off : 0];
+    }
+}
+
+// depthwise 7x7 + bias of an OH x OW region from the [C][SH][SWP] LDS image src (region row r reads source
+// rows r .. r + 6) into dst [C][OH][OW]; a wave owns a channel, a lane 4 consecutive outputs of a row
+template <int C, int OH, int OW, int SH, int SWP>
+__device__ __forceinline__ void f2_dw(const float* src, float* dst, const float* lw, const float* lb, int wave, int lane) {
+    constexpr int SEG = 4, NSEG = (OW + SEG - 1) / SEG, ITEMS = OH * NSEG, NWAVES = kF2Threads / 64;
+    for (int c = wave; c < C; c += NWAVES) {
+        float w[49];
+#pragma unroll
+        for (int i = 0; i < 49; ++i) w[i] = lw[c * 49 + i];
+        const float bias = lb[c];
+        for (int it = lane; it < ITEMS; it += 64) {
+            const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
+            float acc[SEG];
+#pragma unroll
+            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
+#pragma unroll
+            for (int ky = 0; ky < 7; ++ky) {
+                float row[SEG + 6];
+                const float* sr = src + (c * SH + py + ky) * SWP + px0;
+#pragma unroll
+                for (int j = 0; j < SEG + 6; ++j) row[j] = sr[j];
+#pragma unroll
+                for (int kx = 0; kx < 7; ++kx)
+#pragma unroll
+                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * 7 + kx] * row[j + kx];
+            }
+#pragma unroll
+            for (int j = 0; j < SEG; ++j)
+                if (px0 + j < OW) dst[(c * OH + py) * OW + px0 + j] = acc[j] + bias;
+        }
+    }
+}
+
+template <int C>
+__global__ void __launch_bounds__(kF2Threads) fm2a_kernel(const esm_fmnet_desc a) {
+    using Lyt = SmixLayout<C>;
+    constexpr int TH = kF2TH, TW = kF2TW;
+    constexpr int AH = TH + 6, AW = TW + 6, AP = AH * AW, AWP = AW + 1 + 6;  // + slack for the 4-wide dw reads
+    constexpr int NW = 3 * Lyt::STAGE + C * 49 + C;
+    constexpr int NWR = (NW + kF2Threads - 1) / kF2Threads;
+    constexpr int NPA = (AP + kF2Threads - 1) / kF2Threads;  // region-A pixels per thread
+    __shared__ float sw[NW];
+    __shared__ float sa[C * AH * AWP];
+    __shared__ float sb[C * TH * TW];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int H = a.H, W = a.W, b = blockIdx.z;
+    const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+    const long long plane = static_cast<long long>(H) * W;
+    const float* xb = a.x + static_cast<long long>(b) * C * plane;
+
+    // weights (stages: SMLayer0.mlp1, SMLayer0.mlp2, SMLayer1.mlp1; dw0) and region A's pixels, one batch
+    float rw[NWR];
+    f2_stage_weights<C, 3>(a, a.dw_w[0], a.dw_b[0], rw);
+    float t[NPA][C];
+    bool in[NPA];
+#pragma unroll
+    for (int k = 0; k < NPA; ++k) {
+        const int p = tid + k * kF2Threads;
+        const int py = p / AW, px = p - (p / AW) * AW;
+        const int gy = y0 - 3 + py, gx = x0 - 3 + px;
+        in[k] = p < AP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const float v = xb[in[k] ? c * plane + gy * W + gx : 0];
+            t[k][c] = in[k] ? v : 0.f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NWR; ++k)
+        if (tid + k * kF2Threads < NW) sw[tid + k * kF2Threads] = rw[k];
+    __syncthreads();
+    // t1 = SMLayer0.mlp1 (x) on region A (zero outside the image: dw0's padding)
+#pragma unroll
+    for (int k = 0; k < NPA; ++k) {
+        const int p = tid + k * kF2Threads;
+        if (p >= AP) continue;
+        const int py = p / AW, px = p - (p / AW) * AW;
+        if (in[k]) mix_stage<C>(t[k], sw);
+#pragma unroll
+        for (int c = 0; c < C; ++c) sa[(c * AH + py) * AWP + px] = in[k] ? t[k][c] : 0.f;
+    }
+    __syncthreads();
+    f2_dw<C, TH, TW, AH, AWP>(sa, sb, sw + 3 * Lyt::STAGE, sw + 3 * Lyt::STAGE + C * 49, wave, lane);
+    __syncthreads();
+    // d = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on the tile -> work
+    {
+        const int py = tid / TW, px = tid - (tid / TW) * TW;
+        const int gy = y0 + py, gx = x0 + px;
+        if (gy < H && gx < W) {
+            float u[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) u[c] = sb[(c * TH + py) * TW + px];
+            mix_stage<C>(u, sw + Lyt::STAGE);
+            mix_stage<C>(u, sw + 2 * Lyt::STAGE);
+            float* wb = a.work + static_cast<long long>(b) * C * plane + gy * W + gx;
+#pragma unroll
+            for (int c = 0; c < C; ++c) wb[c * plane] = u[c];
+        }
+    }
+}
+
+template <int C>
+__global__ void __launch_bounds__(kF2Threads) fm2b_kernel(const esm_fmnet_desc a) {
+    using Lyt = SmixLayout<C>;
+    constexpr int HID = C + 16, HT = 2;                      // hidden channels, their 16-row MFMA tiles
+    constexpr int TH = kF2TH, TW = kF2TW;
+    constexpr int DH = TH + 8, DW = TW + 8, DP = DH * DW, DWP = DW + 1 + 6;  // d on tile + 4
+    constexpr int CH = TH + 2, CW = TW + 2, CP = CH * CW, CWP = CW + 2;      // t3 on tile + 1
+    constexpr int NW1 = Lyt::STAGE + C * 49 + C;                             // mlp2_1, dw1
+    constexpr int W0 = 9 * C * 32, B0 = 32, W2 = 32 * 16, B2 = 16;           // conv0 [tap][c][32], conv2 [h][16]
+    constexpr int NW = NW1 + W0 + B0 + W2 + B2;
+    constexpr int NWR = (NW + kF2Threads - 1) / kF2Threads;
+    constexpr int NPD = (DP + kF2Threads - 1) / kF2Threads;
+    constexpr int NPC = (CP + kF2Threads - 1) / kF2Threads;
+    constexpr int SH_ = C * DH * DWP > HID * TH * TW ? C * DH * DWP : HID * TH * TW;
+    __shared__ float sw[NW];
+    __shared__ float sd[SH_];        // d on region D, then h = silu(conv0 + b0) [HID][TH * TW]
+    __shared__ float sc_[C * CH * CWP];  // dw1 on region C, then t3 in place
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int g = lane >> 4, n = lane & 15;
+    const int H = a.H, W = a.W, b = blockIdx.z;
+    const int y0 = blockIdx.y * TH, x0 = blockIdx.x * TW;
+    const long long plane = static_cast<long long>(H) * W;
+    const float* db = a.work + static_cast<long long>(b) * C * plane;
+    const float* xb = a.x + static_cast<long long>(b) * C * plane;
+
+    // weights: mlp2_1 + dw1 (as fm2a), conv0 as the MFMA A image [tap][c][32 hidden] (zero past HID), b0,
+    // conv2 as [h][16 out channels] (zero past C), b2
+    float rw[NWR];
+#pragma unroll
+    for (int k = 0; k < NWR; ++k) {
+        const int i = tid + k * kF2Threads;
+        const float* p = nullptr;
+        int off = 0;
+        if (i < Lyt::STAGE) {
+            const esm_smix_stage& st = a.stage[3];
+            const int j = i;
+            p = j < Lyt::F0W ? st.ln_w : j < Lyt::F0B ? st.fc0_w : j < Lyt::F2W ? st.fc0_b : j < Lyt::F2B ? st.fc2_w : st.fc2_b;
+            off = j - (j < Lyt::F0W ? Lyt::LN : j < Lyt::F0B ? Lyt::F0W : j < Lyt::F2W ? Lyt::F0B : j < Lyt::F2B ? Lyt::F2W : Lyt::F2B);
+        } else if (i < NW1) {
+            const int j = i - Lyt::STAGE;
+            p = j < C * 49 ? a.dw_w[1] : a.dw_b[1];
+            off = j < C * 49 ? j : j - C * 49;
+        } else if (i < NW1 + W0) {  // conv0_w [HID][C][3][3] -> [tap][c][h]
+            const int j = i - NW1;
+            const int h = j % 32, c = (j / 32) % C, tap = j / (32 * C);
+            if (h < HID) {
+                p = a.conv0_w;
+                off = (h * C + c) * 9 + tap;
+            }
+        } else if (i < NW1 + W0 + B0) {
+            const int h = i - NW1 - W0;
+            if (h < HID) {
+                p = a.conv0_b;
+                off = h;
+            }
+        } else if (i < NW1 + W0 + B0 + W2) {  // conv2_w [C][HID] -> [h][16]
+            const int j = i - NW1 - W0 - B0;
+            const int co = j % 16, h = j / 16;
+            if (co < C && h < HID) {
+                p = a.conv2_w;
+                off = co * HID + h;
+            }
+        } else if (i < NW) {
+            const int co = i - NW1 - W0 - B0 - W2;
+            if (co < C) {
+                p = a.conv2_b;
+                off = co;
+            }
+        }
+        const float v = (p ? p : a.x)[p ? off : 0];
+        rw[k] = p ? v : 0.f;
+    }
+    // d on region D (zero outside the image: dw1's padding); x on region C (t3's residual), in registers
+#pragma unroll
+    for (int k = 0; k < NPD; ++k) {
+        const int p = tid + k * kF2Threads;
+        const int py = p / DW, px = p - (p / DW) * DW;
+        const int gy = y0 - 4 + py, gx = x0 - 4 + px;
+        const bool ok = p < DP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        float v[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const float u = db[ok ? c * plane + gy * W + gx : 0];
+            v[c] = ok ? u : 0.f;
+        }
+        if (p < DP) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) sd[(c * DH + py) * DWP + px] = v[c];
+        }
+    }
+    float xr[NPC][C];
+#pragma unroll
+    for (int k = 0; k < NPC; ++k) {
+        const int p = tid + k * kF2Threads;
+        const int py = p / CW, px = p - (p / CW) * CW;
+        const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+        const bool ok = p < CP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const float u = xb[ok ? c * plane + gy * W + gx : 0];
+            xr[k][c] = ok ? u : 0.f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NWR; ++k)
+        if (tid + k * kF2Threads < NW) sw[tid + k * kF2Threads] = rw[k];
+    __syncthreads();
+    // dw1 on region C
+    f2_dw<C, CH, CW, DH, DWP>(sd, sc_, sw + Lyt::STAGE, sw + Lyt::STAGE + C * 49, wave, lane);
+    __syncthreads();
+    // t3 = SMLayer1.mlp2 (dw1) + x on region C, zero outside the image (conv0's padding), in place
+#pragma unroll
+    for (int k = 0; k < NPC; ++k) {
+        const int p = tid + k * kF2Threads;
+        if (p >= CP) continue;
+        const int py = p / CW, px = p - (p / CW) * CW;
+        const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+        const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        float u[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) u[c] = sc_[(c * CH + py) * CWP + px];
+        if (ok) mix_stage<C>(u, sw);
+#pragma unroll
+        for (int c = 0; c < C; ++c) sc_[(c * CH + py) * CWP + px] = ok ? u[c] + xr[k][c] : 0.f;
+    }
+    __syncthreads();
+    // h = silu(conv0(t3) + b0) on the tile (MFMA): wave w owns tile rows 2w, 2w + 1 (N tiles: 16 pixels of
+    // a row half), both 16-row hidden tiles; A = conv0 [tap][c][h], B = t3 window rows
+    const float* w0 = sw + NW1;
+    f2x4 acc[4][HT];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < HT; ++mt) acc[nt][mt] = f2x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+        for (int ks = 0; ks < C / 4; ++ks) {
+            const int c = 4 * ks + g;
+            float av[HT];
+#pragma unroll
+            for (int mt = 0; mt < HT; ++mt) av[mt] = w0[(tap * C + c) * 32 + 16 * mt + n];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const int row = 2 * wave + (nt >> 1), col = 16 * (nt & 1) + n;
+                const float bv = sc_[(c * CH + row + dy) * CWP + col + dx];
+#pragma unroll
+                for (int mt = 0; mt < HT; ++mt)
+                    acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv, acc[nt][mt], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // every wave is done reading d (sd) before h overwrites it
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int pp = (2 * wave + (nt >> 1)) * TW + 16 * (nt & 1) + n;
+#pragma unroll
+        for (int mt = 0; mt < HT; ++mt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int h = 16 * mt + 4 * g + j;
+                if (h < HID) sd[h * (TH * TW) + pp] = silu(acc[nt][mt][j] + w0[W0 + h]);
+            }
+    }
+    __syncthreads();
+    // out = conv2(h) + b2 + t3 on the tile (MFMA): A = conv2 [h][16], B = h
+    const float* w2 = sw + NW1 + W0 + B0;
+    f2x4 o[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) o[nt] = f2x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HID / 4; ++ks) {
+        const int h = 4 * ks + g;
+        const float av = w2[h * 16 + n];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const int pp = (2 * wave + (nt >> 1)) * TW + 16 * (nt & 1) + n;
+            o[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sd[h * (TH * TW) + pp], o[nt], 0, 0, 0);
+        }
+    }
+    float* ob = a.out + static_cast<long long>(b) * C * plane;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int row = 2 * wave + (nt >> 1), col = 16 * (nt & 1) + n;
+        const int gy = y0 + row, gx = x0 + col;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = 4 * g + j;
+            if (co < C && gy < H && gx < W)
+                ob[co * plane + gy * W + gx] = o[nt][j] + w2[W2 + co] + sc_[(co * CH + row + 1) * CWP + col + 1];
+        }
+    }
+}
+
 }  // namespace
 
 int launch_smix(const esm_smix_desc* d, hipStream_t s) {
@@ -584,6 +931,22 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
     const bool conv = a.conv0_w != nullptr;
     if (conv && (!a.conv0_b || !a.conv2_w || !a.conv2_b || a.hid != a.C + 16))
         return arg_error("fmnet: the fused FMBlock.conv needs conv0/conv2 weights and biases, hid = C + 16");
+    if (conv && a.work) {  // two launches (large maps): fm2a writes d to work, fm2b the block's output
+        if (a.work == a.x || a.work == a.out) return arg_error("fmnet: work must not alias x / out");
+        const dim3 grid2(ceil_div(a.W, kF2TW), ceil_div(a.H, kF2TH), a.B);
+        if (grid2.y > 65535u || grid2.z > 65535u) return arg_error("fmnet: grid too large");
+        if (a.C == 8) {
+            hipLaunchKernelGGL((fm2a_kernel<8>), grid2, dim3(kF2Threads), 0, s, a);
+            hipLaunchKernelGGL((fm2b_kernel<8>), grid2, dim3(kF2Threads), 0, s, a);
+        } else if (a.C == 16) {
+            hipLaunchKernelGGL((fm2a_kernel<16>), grid2, dim3(kF2Threads), 0, s, a);
+            hipLaunchKernelGGL((fm2b_kernel<16>), grid2, dim3(kF2Threads), 0, s, a);
+        } else {
+            set_error("fmnet: C must be 8 or 16");
+            return ESM_ERR_UNSUPPORTED;
+        }
+        return check_launch("fmnet(two launches)");
+    }
     const bool tall = conv && static_cast<long long>(ceil_div(a.W, kFConvTW)) * ceil_div(a.H, 3) * a.B >= kFConvTallMinTiles;
     const int th = conv ? (tall ? 3 : 1) : 4;
     const dim3 grid(ceil_div(a.W, conv ? kFConvTW : kFTW), ceil_div(a.H, th), a.B);

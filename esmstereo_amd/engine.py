@@ -740,13 +740,21 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
     return out
 
 
+# The whole FMBlock as two launches (esm_fmnet_desc.work, smix.hip fm2a / fm2b) on maps of at least this
+# many pixels (B x H x W); smaller maps keep the one-launch form, whose halo recompute is cheap there and
+# whose single launch boundary matters (S-K: 24 x 78)
+FM2_MIN_PIX = int(os.environ.get("ESM_FM2_MIN_PIX", "16384"))
+
+
 def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
               dw1: Tuple[torch.Tensor, torch.Tensor], out: Optional[torch.Tensor] = None,
-              tag: str = "fmnet", conv: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
+              tag: str = "fmnet", conv: Optional[Tuple[torch.Tensor, ...]] = None,
+              two_launch: Optional[bool] = None) -> torch.Tensor:
     """``FMBlock.net(x) + x`` (shufflemixer.py:129-130) in one launch: stages = SMLayer0.mlp1, .mlp2,
     SMLayer1.mlp1, .mlp2; dw0 / dw1 = the two SMLayers' depthwise convs (weight, bias).  With ``conv`` =
     (conv0 weight [C+16, C, 3, 3], bias, conv2 weight [C, C+16, 1, 1], bias) the whole FMBlock
-    (shufflemixer.py:129-131: ``t = net(x) + x; conv(t) + t``) is the one launch."""
+    (shufflemixer.py:129-131: ``t = net(x) + x; conv(t) + t``) is the one launch, or on large maps
+    (``two_launch``; default: B x H x W >= FM2_MIN_PIX) two launches through a scratch buffer."""
     require_device(x, "fmnet input")
     if not x.is_contiguous():
         raise ValueError("fmnet: input must be contiguous")
@@ -782,6 +790,12 @@ def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple
         d.conv0_w, d.conv0_b, d.conv2_w, d.conv2_b = (t.data_ptr() for t in conv)
         d.hid = hid
         ctx.hold(*conv)
+        if two_launch is None:
+            two_launch = B * H * W >= FM2_MIN_PIX
+        if two_launch:
+            work = ctx.empty(B, C, H, W)
+            d.work = work.data_ptr()
+            ctx.hold(work)
     ctx.hold(x, out, *dw0, *dw1)
     npix = B * H * W
     # algorithmic flops per pixel: four split-point MLPs (C/2 -> C -> C/2: 2 * C * C), two depthwise

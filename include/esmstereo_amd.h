@@ -188,6 +188,10 @@ typedef struct {
     const float* conv2_b;
     int32_t hid;
     int32_t reserved2;
+    /* optional, with conv0_w: a [B, C, H, W] scratch buffer; when given, the block runs as two launches
+     * split at the second depthwise conv (halo 3 each side instead of the whole block's 7) with FMBlock.conv
+     * on the matrix cores: the form for large maps (ESMStereo-L at KITTI size and up) */
+    float* work;
 } esm_fmnet_desc;
 
 /* Fused `tail(upsampling(x))` of the ESM upsamplers: out[b,0] = tail_b + conv3x3(tail_w,

@@ -741,7 +741,8 @@ def test_conv_multisource_crop_and_epilogues():
 
 
 @pytest.mark.parametrize("C", [8, 16])
-def test_fmblock_vs_oracle(C):
+@pytest.mark.parametrize("H,W", [(21, 45), (90, 101)])  # (90, 101) x B 2: the two-launch form (>= FM2_MIN_PIX)
+def test_fmblock_vs_oracle(C, H, W):
     torch.manual_seed(7)
     blk = E.FMBlock(C, 7, 2).eval()
     with torch.no_grad():
@@ -749,7 +750,7 @@ def test_fmblock_vs_oracle(C):
             if n.endswith("norm1.body.weight") or n.endswith("norm2.body.weight"):
                 p.uniform_(0.8, 1.2)
     sd = {k: v.clone() for k, v in blk.state_dict().items()}
-    x = torch.randn(2, C, 21, 45)
+    x = torch.randn(2, C, H, W)
     y = blk.to(DEV)(x.to(DEV))
     assert rel(y, O.fm_block(sd, "", x)) < 1e-5
 
@@ -1081,9 +1082,12 @@ def test_fmnet_fused_bitwise(C, H, W):
     t3 = run_smix(ctx, t2, [p["b2"]], dw=p["dw1"], res=x)
     assert rel(fused, t3) < 1e-6
     # the whole block in one launch (FMBlock.conv fused behind net) vs net + the two conv launches
-    whole = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"])
+    whole = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"], two_launch=False)
     ref = run_conv(ctx, p["c2"], [run_conv(ctx, p["c0"], [t3])], res=t3)
     assert rel(whole, ref) < 1e-5
+    # the two-launch form (smix.hip fm2a / fm2b: split at dw1, FMBlock.conv on the matrix cores)
+    two = run_fmnet(ctx, x, [p["a1"], p["a2"], p["b1"], p["b2"]], p["dw0"], p["dw1"], conv=p["cw"], two_launch=True)
+    assert rel(two, ref) < 1e-5
 
 
 @pytest.mark.parametrize("cout,k,s,p,H,W", [(16, 3, 2, 1, 384, 1248), (16, 5, 1, 0, 96, 312), (32, 5, 1, 0, 37, 50),
