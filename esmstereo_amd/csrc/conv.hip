@@ -86,7 +86,8 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     const int form = a.hint & ~kHintXcd;  // the form / tile bits (bit 30 only orders the tiles)
     if (a.transposed) {
         if (a.hint & kHintWideT) return conv::launch_widet(a, s);
-        if ((a.hint & kHintTile3) || (form == 0 && conv::tile3_auto(a))) return conv::launch_tile3(a, s);
+        if (a.hint & kHintTile3) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
+        if (form == 0 && d3 && conv::tile3_auto(a)) return conv::launch_tile3(a, s);
         if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
     }

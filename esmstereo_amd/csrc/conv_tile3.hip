@@ -310,14 +310,17 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
 // d = 1 + q - t.  A workgroup owns one (qd, qh) class pair of an m-tile; each wave computes both qw
 // classes (window columns dx = 0..2 feed qw = 0 through tw = 1 - dx and qw = 1 through tw = 2 - dx), so
 // a lane holds the two adjacent output columns 2m, 2m + 1 and stores them as one 8-byte write.
-template <int MT, int NT, int ACT, bool PLAIN>
+// D2: ConvTranspose2d k4 s2 p1 (the refinement hourglasses' conv3_up / conv2_up): one qh class per
+// workgroup, the 4 waves along y (NT rows each), 4 taps per class
+template <int MT, int NT, int ACT, bool PLAIN, bool D2 = false>
 __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc a, int ncg) {
-    constexpr int WZ = 4, ZB = 4, YB = NT;
-    constexpr int IZ = ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
+    constexpr int ZB = D2 ? 1 : 4, YB = D2 ? 4 * NT : NT;
+    constexpr int NTAP = D2 ? 4 : 8;  // taps per class
+    constexpr int IZ = D2 ? 1 : ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
     constexpr int CS = CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;
     constexpr int XE = 4 * CS0, XL = 4 * CS;
     constexpr int WCS = MT % 2 ? MT * 16 : MT * 16 + 16;
-    constexpr int WE = 16 * 4 * MT * 16, WL = 16 * 4 * WCS;  // [qw][tap 8][ci 4][m]
+    constexpr int WE = 2 * NTAP * 4 * MT * 16, WL = 2 * NTAP * 4 * WCS;  // [qw][tap][ci 4][m]
     constexpr int XR = (XE + kT3Threads - 1) / kT3Threads, WR = (WE + kT3Threads - 1) / kT3Threads;
     __shared__ __attribute__((aligned(16))) float xs[2][XL];
     __shared__ __attribute__((aligned(16))) float ws[2][WL];
@@ -325,19 +328,19 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
     const int tid = threadIdx.x;
     const int lane = tid & 63, g = lane >> 4, n = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int zw = wave;
+    const int zw = D2 ? 0 : wave, yw = D2 ? wave : 0;
     const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
     const int xm0 = bk_.x * 16, ym0 = bk_.y * YB;
     const int nzb = (a.Di + ZB - 1) / ZB;
     int zz = bk_.z;
-    const int cp = zz & 3;  // (qd, qh) class pair
-    zz >>= 2;
+    const int cp = D2 ? (zz & 1) : (zz & 3);  // (qd, qh) class pair (2-D: qh)
+    zz >>= D2 ? 1 : 2;
     const int mg = zz % ncg;
     const int r1 = zz / ncg;
     const int b = r1 / nzb;
     const int zm0 = (r1 - b * nzb) * ZB;
-    const int qd = cp >> 1, qh = cp & 1;
-    const int zi0 = zm0 - 1, yi0 = ym0 - 1, xi0 = xm0 - 1;
+    const int qd = D2 ? 0 : cp >> 1, qh = cp & 1;
+    const int zi0 = D2 ? 0 : zm0 - 1, yi0 = ym0 - 1, xi0 = xm0 - 1;
 
     const esm_src& s0 = a.src[0];
     const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
@@ -345,7 +348,8 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
         const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
         4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.w), static_cast<short>(0), 4 * 64 * a.cin_pad * a.cout_pad, 0x00020000);
+        const_cast<float*>(a.w), static_cast<short>(0), 4 * NTAP * NTAP * a.cin_pad * a.cout_pad,
+        0x00020000);
 
     unsigned xoff[XR];
 #pragma unroll
@@ -362,11 +366,11 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
 #pragma unroll
     for (int k = 0; k < WR; ++k) {
         const int e = tid + k * kT3Threads;  // e = ((qw * 8 + tap) * 4 + ci) * (MT * 16) + m
-        const int m = e % (MT * 16), ci = (e / (MT * 16)) & 3, tq = e / (MT * 64);  // tq = qw * 8 + tap
-        const int cls = (cp << 1) | (tq >> 3), tap = tq & 7;
+        const int m = e % (MT * 16), ci = (e / (MT * 16)) & 3, tq = e / (MT * 64);  // tq = qw * NTAP + tap
+        const int cls = (cp << 1) | (tq / NTAP), tap = tq % NTAP;
         const int co = mg * MT * 16 + m;
         const bool ok = e < WE && co < a.cout_pad;
-        woff[k] = ok ? 4u * static_cast<unsigned>(((cls * 8 + tap) * a.cin_pad + ci) * a.cout_pad + co) : kOOB;
+        woff[k] = ok ? 4u * static_cast<unsigned>(((cls * NTAP + tap) * a.cin_pad + ci) * a.cout_pad + co) : kOOB;
         wdst[k] = e < WE ? (tq * 4 + ci) * WCS + m : -1;
     }
     float xv[XR], wv[WR];
@@ -416,12 +420,12 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
         const float* xw = &xs[buf][g * CS + n];
         const float* wp = &ws[buf][g * WCS + n];
 #pragma unroll
-        for (int td = 0; td < 2; ++td) {
-            const int dz = 1 + qd - td;  // window plane offset (wave-uniform)
+        for (int td = 0; td < (D2 ? 1 : 2); ++td) {
+            const int dz = D2 ? 0 : 1 + qd - td;  // window plane offset (wave-uniform)
 #pragma unroll
             for (int th = 0; th < 2; ++th) {
                 const int dy = 1 + qh - th;
-                const float* xr = xw + (zw + dz) * PLANE + dy * IX;
+                const float* xr = xw + (zw + dz) * PLANE + (yw * NT + dy) * IX;
 #pragma unroll
                 for (int dx = 0; dx < 3; ++dx) {
                     float br[NT];
@@ -431,7 +435,7 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
                     for (int qw = 0; qw < 2; ++qw) {
                         const int tw = 1 + qw - dx;
                         if (tw < 0 || tw > 1) continue;
-                        const int tq = qw * 8 + (td * 4 + th * 2 + tw);
+                        const int tq = qw * NTAP + (D2 ? th * 2 + tw : td * 4 + th * 2 + tw);
                         float av[MT];
 #pragma unroll
                         for (int mt = 0; mt < MT; ++mt) av[mt] = wp[tq * 4 * WCS + mt * 16];
@@ -451,7 +455,7 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
 
     // ---- epilogue: lane (g, n) holds output columns 2m, 2m + 1 (m = xm0 + n) of rows 4g + j
     const int x = 2 * (xm0 + n);
-    const int z = 2 * (zm0 + zw) + qd;
+    const int z = D2 ? 0 : 2 * (zm0 + zw) + qd;
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
         4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
@@ -459,7 +463,7 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
         0x00020000);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const int y = 2 * (ym0 + nt) + qh;
+        const int y = 2 * (ym0 + yw * NT + nt) + qh;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -499,10 +503,10 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
     }
 }
 
-template <int MT, int NT>
+template <int MT, int NT, bool D2 = false>
 int launch_tt3(const esm_conv_desc& a, hipStream_t s, int ncg) {
-    const long long z = static_cast<long long>(a.B) * ((a.Di + 3) / 4) * ncg * 4;
-    const long long gy = ceil_div(a.Hi, NT);
+    const long long z = D2 ? static_cast<long long>(a.B) * ncg * 2 : static_cast<long long>(a.B) * ((a.Di + 3) / 4) * ncg * 4;
+    const long long gy = ceil_div(a.Hi, D2 ? 4 * NT : NT);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3 transposed): grid too large");
     const dim3 grid(ceil_div(a.Wi, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
     // the plain form stores 8-byte pairs: 8-byte aligned rows
@@ -512,20 +516,20 @@ int launch_tt3(const esm_conv_desc& a, hipStream_t s, int ncg) {
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, ESM_ACT_GELU, true>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, ESM_ACT_GELU, true, D2>), grid, dim3(kT3Threads), 0, s, a, ncg);
     else
-        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, -1, false>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconvt3_kernel<MT, NT, -1, false, D2>), grid, dim3(kT3Threads), 0, s, a, ncg);
     return check_launch("conv(tile3 transposed)");
 }
 
-template <int NT>
+template <int NT, bool D2 = false>
 int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
     const int tiles = (a.Cout + 15) / 16;
-    if (tiles == 1) return launch_tt3<1, NT>(a, s, 1);
-    if (tiles == 2) return launch_tt3<2, NT>(a, s, 1);
-    if (tiles == 3) return launch_tt3<3, NT>(a, s, 1);
-    if (tiles <= 4) return launch_tt3<2, NT>(a, s, 2);
-    if (tiles <= 6) return launch_tt3<3, NT>(a, s, 2);
+    if (tiles == 1) return launch_tt3<1, NT, D2>(a, s, 1);
+    if (tiles == 2) return launch_tt3<2, NT, D2>(a, s, 1);
+    if (tiles == 3) return launch_tt3<3, NT, D2>(a, s, 1);
+    if (tiles <= 4) return launch_tt3<2, NT, D2>(a, s, 2);
+    if (tiles <= 6) return launch_tt3<3, NT, D2>(a, s, 2);
     return arg_error("conv(tile3 transposed): at most 96 output channels");
 }
 
@@ -593,7 +597,10 @@ int launch_t2_nt(const esm_conv_desc& a, hipStream_t s) {
 // 2-D (the upsamplers' large maps at ESMStereo-L / -M): k3 stride 1 / 2 or k1 stride 1, any padding, 1..3
 // sources, <= 96 couts
 bool tile2_ok(const esm_conv_desc& a) {
-    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
+    if (!d3 && a.transposed)  // ConvTranspose2d k4 s2 p1, one source, >= 2 couts (one output: convt_c1)
+        return a.kh == 4 && a.stride == 2 && a.nsrc == 1 && !a.up && !a.mul && a.shuffle <= 1 && a.Cout > 1 &&
+               a.Cout <= 96 && a.cout_pad >= 16 * ((a.Cout + 15) / 16) && direct_ok(a);
     if (d3 || a.transposed || a.up || a.shuffle > 1 || a.Cout > 96) return false;
     if (!((a.kh == 3 && (a.stride == 1 || a.stride == 2)) || (a.kh == 1 && a.stride == 1))) return false;
     if (a.cout_pad < 16 * ((a.Cout + 15) / 16)) return false;
@@ -608,6 +615,12 @@ bool tile2_auto(const esm_conv_desc& a) {
 
 int launch_tile2(const esm_conv_desc& a, hipStream_t s) {
     if (!tile2_ok(a)) return arg_error("conv: tile2-form hint not applicable");
+    if (a.transposed) {
+        const int rsel = (a.hint >> 26) & 3;
+        if (rsel == 1) return launch_tt3_mt<1, true>(a, s);
+        if (rsel == 3) return launch_tt3_mt<4, true>(a, s);
+        return launch_tt3_mt<2, true>(a, s);
+    }
     if (a.kh == 1) return launch_t2_nt<1, 1>(a, s);
     if (a.stride == 2) return launch_t2_nt<2, 3>(a, s);
     return launch_t2_nt<1, 3>(a, s);

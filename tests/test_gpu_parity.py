@@ -346,6 +346,18 @@ def test_conv_tile2_form(cins, cout, k, s, p, H, W, B):
     assert rel(out2, want * 0.5) < 1e-5
 
 
+@pytest.mark.parametrize("cin,cout,H,W,B", [(32, 32, 24, 78, 1), (16, 16, 13, 40, 2), (32, 16, 7, 21, 1)])
+def test_conv_tile2_transposed(cin, cout, H, W, B):
+    """The tile form of ConvTranspose2d k4 s2 p1 (the refinements' conv3_up / conv2_up) vs fp64 torch."""
+    conv, bn = _mk(2, cin, cout, 4, 2, 1, transposed=True, seed=cin + H)
+    x = torch.randn(B, cin, H, W)
+    ref = _ref_conv([x], conv, bn, ACT_GELU)
+    p = pk(conv, bn, ACT_GELU)
+    for rsel in (0, 1, 3):
+        y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | (rsel << 26))
+        assert rel(y, ref) < 1e-5, rsel
+
+
 @pytest.mark.parametrize("cins,cout,shape", [((24, 24), 24, (6, 12, 39)), ((16, 16, 8), 16, (3, 7, 21)),
                                              ((40, 40), 40, (5, 6, 20))])
 def test_conv_tile3_multisource_crop(cins, cout, shape):
