@@ -35,6 +35,7 @@ constexpr int kHintWide = 1 << 22;     // register-weight row-streaming form, 2-
 constexpr int kHintWide3 = 1 << 24;    // register-weight plane-streaming 3x3x3 form, <= 16 couts (conv_wide3.hip)
 constexpr int kHintWideT = 1 << 25;    // register-weight ConvTranspose2d k4s2 form, all 4 classes per wave (conv_widet.hip)
 constexpr int kHintTile3 = 1 << 23;    // LDS-tiled implicit-GEMM 3-D form for the large volumes (conv_tile3.hip)
+constexpr int kHintNoTile = 1 << 19;   // automatic choice, without the LDS-tiled forms (A/B measurements)
 
 // Descriptor validation shared by every entry point that takes an esm_conv_desc (launch_conv, the
 // chain of chain.hip); ESM_OK or ESM_ERR_ARG with the message set.
@@ -83,18 +84,20 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     const int rc = conv_check(a);
     if (rc != ESM_OK) return rc;
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
-    const int form = a.hint & ~kHintXcd;  // the form / tile bits (bit 30 only orders the tiles)
+    const int form = a.hint & ~(kHintXcd | kHintNoTile);  // the form / tile bits (bit 30 only orders the tiles)
+    const bool tile_auto = form == 0 && !(a.hint & kHintNoTile);
     if (a.transposed) {
         if (a.hint & kHintWideT) return conv::launch_widet(a, s);
         if (a.hint & kHintTile3) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
-        if (form == 0 && d3 && conv::tile3_auto(a)) return conv::launch_tile3(a, s);
+        // large maps (L at B = 4: ref4x.conv2_up 103 -> 61 us, r04 probe): the LDS-tiled form
+        if (tile_auto && (d3 ? conv::tile3_auto(a) : conv::tile2_auto(a))) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
         if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
     }
     if (a.hint & kHintSmall) return conv::launch_small(a, s);
     if (a.hint & kHintWide) {
-        // a tuned choice for a concat whose sources lie outside one buffer window (eager use, outside
-        // a launch list's arena): the automatic rules instead
+        // a tuned choice for a layer the wide form cannot take after all (concat sources with different
+        // row strides, e.g. a cropped view): the automatic rules instead
         if (conv::wide_ok(a)) return conv::launch_wide(a, s);
         esm_conv_desc d = a;
         d.hint &= kHintXcd;
@@ -103,7 +106,7 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     if (a.hint & kHintWide3) return conv::launch_wide3(a, s);
     if (a.hint & kHintTile3) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
     // the MFMA-bound 3-D volumes / 2-D maps of ESMStereo-L / -M: the LDS-tiled form
-    if (form == 0 && (d3 ? conv::tile3_auto(a) : conv::tile2_auto(a))) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
+    if (tile_auto && (d3 ? conv::tile3_auto(a) : conv::tile2_auto(a))) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
     if (a.hint & kHintStem) return conv::launch_stem(a, s);
     if (a.hint & kHintC1in) return conv::launch_c1in(a, s);
     // one input channel, 2-D, large map: the VALU form (an MFMA k-step would be 3/4 padding).

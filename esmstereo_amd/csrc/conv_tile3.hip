@@ -643,13 +643,14 @@ bool tile3_ok(const esm_conv_desc& a) {
     return direct_ok(a);
 }
 
-// Automatic choice: the MFMA-bound volumes (>= 2^17 output voxels per launch), where the register-operand
-// forms sit at 0.15-0.41 of the fp32 MFMA peak (profiles/r03_ops_LK4.txt).  The latency-bound small
-// volumes of S / M keep their forms.
+// Automatic choice: the MFMA-bound volumes (>= 2^16 output voxels per launch), where the register-operand
+// forms sit at 0.15-0.41 of the fp32 MFMA peak (profiles/r03_ops_LK4.txt; r04 probe at L-K B = 4:
+// conv2.0 232 -> 86 us, conv2.1 298 -> 100 us at 89,856 voxels).  The latency-bound small volumes of S / M
+// keep their forms.
 bool tile3_auto(const esm_conv_desc& a) {
     if (!tile3_ok(a)) return false;
     const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
-    return vox >= (a.transposed ? (1LL << 16) : (1LL << 17));
+    return vox >= (1LL << 16);
 }
 
 // hint bits 26-27 with TILE3 (bit 23): rows per wave 1 / 2 / 4 (0 = automatic)
@@ -667,10 +668,10 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
         if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_k1<2>(a, s);
         return launch_t3_k1<4>(a, s);
     }
-    if (a.stride == 2) {
-        if (rsel == 1) return launch_t3_mt<2, 3, 1, 2>(a, s);
+    if (a.stride == 2) {  // one row per wave unless asked (r04 probe, L-K B = 4: conv1.0 274 -> 226 us, conv2.0 92 -> 86)
+        if (rsel == 2) return launch_t3_mt<2, 3, 2, 2>(a, s);
         if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
-        return launch_t3_mt<2, 3, 2, 2>(a, s);
+        return launch_t3_mt<2, 3, 1, 2>(a, s);
     }
     if (a.Cout <= 8) {  // plane pairs
         if (rsel == 1) return launch_t3<1, 3, 1, 1, 4, true>(a, s, 1);

@@ -415,11 +415,14 @@ int launch_nr(const esm_shuffle_tail_desc& a, hipStream_t s) {
     // nf = 8, r = 4 (ESMStereo-S 4x head): 16 x 32 tiles measured faster than 16 x 64 (15.1 vs 16.5 us
     // at 384x1248, 8 x 64: 16.8, 8 x 32: 18.1; in the S-K launch sequence)
     if constexpr (NF == 8 && R == 4) {
-        // flags bits 1-2 (esm_shuffle_tail_desc): 0 automatic (the 4-row form), 1 the window form below,
-        // 2 / 3 the row form with 4 / 8 low-res rows per workgroup
+        // flags bits 1-2 (esm_shuffle_tail_desc): 0 automatic, 1 the window form below, 2 / 3 the row form
+        // with 4 / 8 low-res rows per workgroup.  Automatic (r04 probe, back to back): the 8-row form where
+        // it still gives >= 128 workgroups (96x312 in: 8.9 us vs 10.3 for 4 rows, 12.9 window), else the
+        // window form (24x78 in: 8.5 vs 10.6 / 8.8)
         const int form = (a.flags >> 1) & 3;
-        if (form == 3) return launch_tile4<8>(a, s);
-        if (form != 1) return launch_tile4<4>(a, s);
+        const long long t8 = static_cast<long long>(ceil_div(a.W * R, 64)) * ceil_div(a.H * R, 32) * a.B;
+        if (form == 3 || (form == 0 && t8 >= 128)) return launch_tile4<8>(a, s);
+        if (form == 2) return launch_tile4<4>(a, s);
         if (big >= 256) return launch_tile<NF, R, 16, 32>(a, s);
     }
     // nf = 16 (ESMStereo-L heads): 8 x 32 tiles (4x head at 384x1248: 38.9 vs 48.2 us for 8 x 64;

@@ -597,8 +597,9 @@ __device__ __forceinline__ void f2_stage_weights(const esm_fmnet_desc& a, const 
 }
 
 // depthwise 7x7 + bias of an OH x OW region from the [C][SH][SWP] LDS image src (region row r reads source
-// rows r .. r + 6) into dst [C][OH][OW]; a wave owns a channel, a lane 4 consecutive outputs of a row
-template <int C, int OH, int OW, int SH, int SWP>
+// rows r .. r + 6) into dst [C][OH][DWS] (row stride DWS >= OW); a wave owns a channel, a lane 4
+// consecutive outputs of a row
+template <int C, int OH, int OW, int SH, int SWP, int DWS = OW>
 __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float* lw, const float* lb, int wave, int lane) {
     constexpr int SEG = 4, NSEG = (OW + SEG - 1) / SEG, ITEMS = OH * NSEG, NWAVES = kF2Threads / 64;
     for (int c = wave; c < C; c += NWAVES) {
@@ -624,7 +625,7 @@ __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float*
             }
 #pragma unroll
             for (int j = 0; j < SEG; ++j)
-                if (px0 + j < OW) dst[(c * OH + py) * OW + px0 + j] = acc[j] + bias;
+                if (px0 + j < OW) dst[(c * OH + py) * DWS + px0 + j] = acc[j] + bias;
         }
     }
 }
@@ -807,7 +808,7 @@ __global__ void __launch_bounds__(kF2Threads) fm2b_kernel(const esm_fmnet_desc a
         if (tid + k * kF2Threads < NW) sw[tid + k * kF2Threads] = rw[k];
     __syncthreads();
     // dw1 on region C
-    f2_dw<C, CH, CW, DH, DWP>(sd, sc_, sw + Lyt::STAGE, sw + Lyt::STAGE + C * 49, wave, lane);
+    f2_dw<C, CH, CW, DH, DWP, CWP>(sd, sc_, sw + Lyt::STAGE, sw + Lyt::STAGE + C * 49, wave, lane);
     __syncthreads();
     // t3 = SMLayer1.mlp2 (dw1) + x on region C, zero outside the image (conv0's padding), in place
 #pragma unroll

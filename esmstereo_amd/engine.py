@@ -184,9 +184,7 @@ class Ctx:
     only recorded (``dry=True``: shape-only ``meta`` buffers, nothing submitted; use as a context
     manager, ``with Ctx(dev, dry=True) as ctx: ...``)."""
 
-    def __init__(self, device: torch.device, plan: bool = False, dry: bool = False, arena: int = 0):
-        """``arena`` (eager contexts): carve every buffer out of one chunk of that many bytes (the
-        ``arena_bytes`` of a dry emission of the same calls: ``eager_emit``)."""
+    def __init__(self, device: torch.device, plan: bool = False, dry: bool = False):
         self.device = torch.device(device)
         self.dry = bool(dry)
         self.plan = lib.esm_plan_create() if plan and not dry else None
@@ -201,9 +199,6 @@ class Ctx:
         self.arena_bytes = 0   # bytes carved out of the arena (256-B granules)
         self.arena_chunks = 0
         self.num_ops = 0       # ops submitted (or, dry, recorded)
-        if arena and not plan and not dry:
-            self.ARENA_FIRST = int(arena)
-            self._eager_arena = True
 
     def __enter__(self) -> "Ctx":
         global _DRY_DEPTH
@@ -252,15 +247,14 @@ class Ctx:
     ARENA_FIRST = 16 << 20   # the first chunk; each further chunk doubles, up to ARENA_CHUNK
 
     def empty(self, *shape: int) -> torch.Tensor:
-        """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of arena chunks, so the
-        buffers of one launch list sit close together: kernels that address several sources through
-        one buffer descriptor (the wide form over a channel concat) need them inside one 1 GiB window
-        (``_check_window``).  Chunks start at 16 MiB and double, so small plans stay small."""
+        """A float32 buffer.  A plan's buffers are carved (256-B aligned) out of arena chunks (one
+        chunk sized by a dry emission for a compiled plan; 16 MiB doubling chunks otherwise), so a
+        launch list's buffers sit together and come from one allocation."""
         if self.dry:  # the plan's arena accounting, with shape-only buffers
             n = math.prod(shape)
             self.arena_bytes += (4 * n + 255) // 256 * 256
             return torch.empty(shape, device="meta", dtype=torch.float32)
-        if not self.plan and not getattr(self, "_eager_arena", False):
+        if not self.plan:
             return torch.empty(shape, device=self.device, dtype=torch.float32)
         n = math.prod(shape)
         nb = (4 * n + 255) // 256 * 256
@@ -291,28 +285,6 @@ class Ctx:
     def _tail_lo(self) -> int:
         t = getattr(self, "_tail", None)
         return self._arena.numel() if t is None or t > self._arena.numel() else t
-
-    WINDOW = 1 << 30  # conv_direct.h kOOB: a concat's sources must span less than this
-    _window_warned = False
-
-    def check_window(self, srcs: Sequence[torch.Tensor], tag: str) -> None:
-        """Warn (once per process) when a channel concat's sources span >= 1 GiB: the register-weight
-        forms then cannot address them through one descriptor and the launch silently takes a slower
-        form (conv_direct.h source_window)."""
-        if len(srcs) < 2 or Ctx._window_warned or self.dry:
-            return
-        lo = min(t.data_ptr() for t in srcs)
-        hi = max(t.data_ptr() + 4 * (1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()))) for t in srcs)
-        if hi - lo >= self.WINDOW:
-            Ctx._window_warned = True
-            import warnings
-            warnings.warn(f"{tag}: concat sources span {(hi - lo) >> 20} MiB (>= 1 GiB); the wide conv forms fall "
-                          "back to slower ones for this launch", RuntimeWarning, stacklevel=3)
-
-    def eager_arena_release(self) -> None:
-        """Forget the eager arena (the buffers handed out stay valid while referenced)."""
-        self._arena = None
-        self.keep.clear()
 
     def hold(self, *objs) -> None:
         if self.plan:
@@ -449,21 +421,9 @@ class Ctx:
 
 
 def eager_emit(device: torch.device, fn, *args, **kw):
-    """Run ``fn(ctx, *args, **kw)`` (a module's ``emit``) eagerly, with every buffer it allocates carved
-    out of ONE arena chunk sized by a dry emission of the same call: the channel-concat sources of the
-    multi-launch modules (the hourglasses, the upsamplers) then sit inside one buffer window and every
-    launch keeps its register-weight form, as in the compiled plan (conv_direct.h source_window).  The
-    returned tensors are copied out of the arena, which is released with the intermediates."""
-    with Ctx(device, dry=True) as dry:
-        fn(dry, *args, **kw)
-    ctx = Ctx(device, arena=dry.arena_bytes + 256)
-    out = fn(ctx, *args, **kw)
-    if isinstance(out, (list, tuple)):
-        out = type(out)(o.clone() for o in out)
-    else:
-        out = out.clone()
-    ctx.eager_arena_release()
-    return out
+    """Run ``fn(ctx, *args, **kw)`` (a module's ``emit``) eagerly: every launch is submitted on the
+    current stream as it is emitted, its buffers from PyTorch's allocator."""
+    return fn(Ctx(device), *args, **kw)
 
 
 # ----------------------------------------------------------------------------- ops
@@ -619,7 +579,6 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.out2 = out2.data_ptr()
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
-    ctx.check_window(srcs, tag)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
     if B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX:
         d.hint |= HINT_XCD_SLAB

@@ -132,10 +132,7 @@ class HotPath:
         self.device = torch.device(device)
         args = (model, B, h, w, att_ch, up_shapes, train_status, channels)
         # size the arena with a dry emission (shape-only buffers, nothing submitted), then emit once
-        # into ONE arena chunk: chunks allocated one by one can land more than 1 GiB apart, and a
-        # channel concat whose sources straddle two of them cannot be addressed through one buffer
-        # descriptor by the register-weight forms (conv_direct.h source_window), which then fall back
-        # to slower ones (measured: the S-K step 346.6 vs 363-366 us)
+        # into ONE arena chunk (one allocation; the plan's buffers together)
         with Ctx(self.device, dry=True) as dry:
             self._emit(dry, *args)
         self.ctx = Ctx(self.device, plan=True)
@@ -158,8 +155,7 @@ class HotPath:
         self.mr = e(B, channels, h, w)
         self.att = e(B, att_ch, h, w) if att_ch else None
         # the upsampler's feature inputs at the arena's far end, next to the buffers allocated last
-        # (the upsampler's own, which they are concatenated with): a concat's sources stay within one
-        # 1 GiB window even when the cost volume between them is larger (configs[2]: B = 8)
+        # (the upsampler's own, which they are concatenated with)
         self.up = [ctx.empty_tail(*s) for s in up_shapes]
         self.outputs = model._emit_hot(ctx, self.ml, self.mr, self.att, self.up, train_status)
 
@@ -191,8 +187,6 @@ class HotPath:
             check(lib.esm_plan_run(self.ctx.plan, s), "plan_run")
 
     # ------------------------------------------------------------------ inputs
-    WINDOW = 1 << 30  # conv_direct.h kOOB: the span a concat's sources must stay inside
-
     def _slots(self, ml, mr, att, up) -> list:
         if len(up) != len(self.up):
             raise ValueError(f"hot path: expected {len(self.up)} upsampler features, got {len(up)}")
@@ -204,17 +198,15 @@ class HotPath:
     def _in_place_ok(self, i: int, t: torch.Tensor) -> bool:
         """Whether the plan may read ``t`` where it lies: contiguous fp32 on the plan's device, not
         overlapping the plan's arena (whose buffers the launches overwrite) unless it IS the slot's own
-        buffer, and for an upsampler feature (a channel-concat source, slots 3+) within one buffer window
-        of the arena, so every launch keeps its register-weight form."""
+        buffer.  Every kernel addresses each concat source through a descriptor of its own, so a
+        feature may lie anywhere."""
         if t.data_ptr() == self._own[i].data_ptr():
             return True
         if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
             return False
         lo, hi = t.data_ptr(), t.data_ptr() + 4 * t.numel()
         a_lo, a_hi = self._arena_span
-        if lo < a_hi and a_lo < hi:
-            return False
-        return i < 3 or max(hi, a_hi) - min(lo, a_lo) < self.WINDOW
+        return not (lo < a_hi and a_lo < hi)
 
     def _rebind(self, ptrs: Sequence[Optional[int]]) -> None:
         olds, sizes, news = [], [], []
@@ -232,7 +224,7 @@ class HotPath:
     def bind(self, ml, mr, att, up) -> None:
         """Point the plan at the caller's tensors (zero-copy; models/ESMStereo.py:700-745 reads its
         features where they lie).  A tensor the plan cannot read in place (non-contiguous, another
-        device, aliasing the plan's buffers, or a concat source outside the window) is copied into the
+        device, or aliasing the plan's buffers) is copied into the
         plan's own buffer instead.  The plan keeps no reference: the caller keeps the tensors alive
         until the launch that reads them has run (stream order, as for any PyTorch op).  When the
         pointers are the ones already bound (a serving loop whose allocator hands back the same

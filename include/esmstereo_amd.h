@@ -119,8 +119,13 @@ typedef struct {
                      (tuning sweeps / tests; see conv_impl.h launch_geom) |
                      SMALL << 21: the lean K-split form for latency-bound layers (conv_small.hip;
                      plain epilogues: no mul / up / shuffle) |
+                     NO_TILE << 19: the automatic choice without the LDS-tiled forms (A/B measurements) |
                      WIDE << 22: register-resident-weight row-streaming form (conv_wide.hip; 2-D, stride 1,
-                     k1 / k3 / k5, one source window, Cout <= 32) |
+                     k1 / k3 / k5, concat sources with one row stride, Cout <= 32) |
+                     TILE3 << 23: LDS-tiled implicit-GEMM form (conv_tile3.hip; 3-D k3 s1 / s2 p1, k1 s1 over up
+                     to 3 sources and ConvTranspose3d k4 s2; 2-D k3 s1 / s2, k1 s1 and ConvTranspose2d k4 s2;
+                     <= 96 couts; bits 26-27: rows per wave 1 / 2 / 4, 0 automatic; chosen automatically
+                     for 3-D volumes of >= 2^16 output voxels and 2-D maps of >= 2^19 pixel x cout-tiles) |
                      WIDE3 << 24: register-weight plane-streaming form for 3x3x3 s1 p1 3-D convs with <= 16 couts
                      and <= 32 input channels (conv_wide3.hip; plain, `* mul` and residual epilogues) |
                      WIDET << 25: register-weight ConvTranspose2d k4 s2 form computing all 4 parity classes per

@@ -444,8 +444,10 @@ def test_conv_wide_form(cin, cout, k, p, shape):
 @pytest.mark.parametrize("cins,cout,k,p,shape", [((16, 24), 16, 3, 1, (96, 312)), ((16, 16, 24), 16, 1, 0, (96, 312)),
                                                   ((16, 16, 32), 16, 1, 0, (47, 157)), ((8, 8), 24, 3, 1, (19, 40))])
 def test_conv_wide_form_multisource(cins, cout, k, p, shape):
-    """Wide form over a channel concat (spx_Nx.0, agg_N.0): the sources carved out of one allocation, as a
-    launch list's arena carves them, so one buffer window covers them; vs fp64 torch (1e-5 relative)."""
+    """Wide form over a channel concat (spx_Nx.0, agg_N.0), one descriptor per source: the sources carved
+    out of one allocation (as a launch list's arena carves them), then allocated apart with 1.5 GiB
+    between them, in both address orders; vs fp64 torch (1e-5 relative), and the two placements bitwise
+    equal."""
     conv, bn = _mk(2, sum(cins), cout, k, 1, p, seed=10)
     n = [2 * c * shape[0] * shape[1] for c in cins]
     pool = torch.randn(sum(n) + 1000, device=DEV)
@@ -456,6 +458,13 @@ def test_conv_wide_form_multisource(cins, cout, k, p, shape):
     ref = _ref_conv([x.cpu() for x in xs], conv, bn, ACT_GELU)
     y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), xs, hint=HINT_WIDE)
     assert rel(y, ref) < 1e-5
+    far, spacers = [], []
+    for x in reversed(xs):
+        far.append(x.clone())
+        spacers.append(torch.empty(3 << 28, device=DEV))
+    far.reverse()
+    y2 = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), far, hint=HINT_WIDE)
+    assert torch.equal(y2, y)
 
 
 HINT_WIDE3 = 1 << 24
@@ -1019,8 +1028,9 @@ def test_hot_path_reads_inputs_in_place(graph):
     (esm_plan_rebind), for the S plan (att, four upsampler features) and the L plan.  Against the copy
     path (load_inputs into the plan's own buffers), bitwise: fresh tensors on every call, the same
     tensors edited in place (no stale copy), ml / mr swapped between calls (each pointer moves once),
-    a non-contiguous feature (copied into the plan's buffer instead) and back to in place, all with
-    the graph built (its nodes updated in place) and without."""
+    features allocated far (> 1 GiB) from the plan's arena (still read in place: every kernel has a
+    descriptor per concat source), a non-contiguous feature (copied into the plan's buffer instead) and
+    back to in place, all with the graph built (its nodes updated in place) and without."""
     for name in ("hot_S_gwc.npz", "hot_L_gwc.npz"):
         model, sd, m = _model_from_manifest(name)
         model.use_graph = graph
@@ -1046,6 +1056,13 @@ def test_hot_path_reads_inputs_in_place(graph):
                 up2 = [u + 0.01 * it for u in up]
                 out = model.hot_path(ml2, mr2, att, up2)[0]
                 assert torch.equal(out, expect(ml2, mr2, att, up2)), (name, it)
+            spacer = torch.empty(3 << 28, device=DEV)  # 1.5 GiB allocated between the plan's arena and the features
+            upf = [u + 0.02 for u in up]
+            out = model.hot_path(ml2, mr2, att, upf)[0]
+            assert torch.equal(out, expect(ml2, mr2, att, upf)), name
+            hp = list(model._plans.values())[-1]
+            assert hp._bound[3:] == [u.data_ptr() for u in upf], name  # every feature read where it lies
+            del spacer
             ml2.mul_(0.5)  # same tensors, new values: read in place, nothing stale
             out = model.hot_path(ml2, mr2, att, up2)[0]
             assert torch.equal(out, expect(ml2, mr2, att, up2)), name
