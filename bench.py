@@ -617,7 +617,8 @@ def main() -> None:
         # back-to-back batch), for the position-based trace mapping of scripts/prof_ops.py / pmc_traffic.py
         has_stem = marg is not None and any(m["name"] == "group_stem" for m in meta)
         with open(args.kernel_table + ".meta.json", "w") as f:  # dominant-op batch (+ group_stem's batch)
-            json.dump({"timed_steps": args.steps, "trailing_dispatches": 3 + args.steps + (23 if has_stem else 0)}, f)
+            json.dump({"timed_steps": args.steps,
+                       "trailing_dispatches": meta[dom].get("launches", 1) * (3 + args.steps) + (23 if has_stem else 0)}, f)
 
     # the timed region: the plain plan (one hipGraph per step) + the per-step disparity all-gather
     gather = D.DisparityGather(hp.outputs[0]) if world > 1 and not args.no_gather else None
@@ -665,7 +666,7 @@ def main() -> None:
                        "variant": args.variant, "cv": args.cv, "global_batch": total_batch,
                        "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                        "parallelism": f"dp{world}", "graph": hp.graph,
-                       "launches_per_step": hp.num_ops},
+                       "launches_per_step": sum(m.get("launches", 1) for m in meta), "ops_per_step": hp.num_ops},
             "roofline": roof,
             "roofline_step": step_roofline(meta, ms_step, args.batch),
         }

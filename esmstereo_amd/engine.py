@@ -763,7 +763,7 @@ def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple
     ctx.meta.append(dict(name=tag, kind="fmnet", flops=npix * flops,
                          bytes=4 * npix * C * 2 + 4 * (sum(int(t.numel()) for t in conv) if conv is not None else 0),
                          shape=f"C{C} {H}x{W} dw{d.dw_k} x2" + (f" +conv{d.hid}" if conv is not None else ""),
-                         reads=_spans(x), writes=_spans(out)))
+                         reads=_spans(x), writes=_spans(out), launches=2 if d.work else 1))
     ctx.fmnet(d)
     return out
 

@@ -36,11 +36,11 @@ def per_dispatch(d: str):
 def main():
     ops_json, dirs = sys.argv[1], sys.argv[2:]
     ops = json.load(open(ops_json))
-    n, tr = len(ops), trailing(ops_json)
+    tr = trailing(ops_json)
     per = {}
     for d in dirs:
         for c, seq in per_dispatch(d).items():
-            per[c] = assign(seq[:len(seq) - tr], n, timed_steps(ops_json))
+            per[c] = assign(seq[:len(seq) - tr], ops, timed_steps(ops_json))
     out = []
     for i, op in enumerate(ops):
         row = {"op": i, "name": op["name"], "median_us": round(op.get("median_ms", 0) * 1e3, 2)}

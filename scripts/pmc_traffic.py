@@ -41,20 +41,33 @@ def per_dispatch(d: str, counter: str):
     return [vals[k] for k in order]
 
 
-def assign(seq, n, timed=0):
-    """Average per launch-list position over the timed steps (``timed`` of them, the last whole
-    steps before the trailing dispatches; 0 = every whole step but the oldest)."""
-    steps = len(seq) // n
+def kernel_ops(ops) -> list:
+    """Launch-list op index of each kernel dispatch of one step (an op may launch several kernels:
+    ``launches`` in its table entry, e.g. the two-launch FMBlock)."""
+    return [i for i, op in enumerate(ops) for _ in range(int(op.get("launches", 1)))]
+
+
+def whole_steps(seq, nk, timed=0):
+    """The dispatches of the timed steps (``timed`` of them, the last whole steps before the trailing
+    dispatches; 0 = every whole step but the oldest), ``nk`` kernels a step."""
+    steps = len(seq) // nk
     if steps == 0:
         raise SystemExit("fewer dispatches than one step")
     if timed:
-        tail = seq[-min(timed, steps) * n:]
-    else:
-        tail = seq[-(steps - 1) * n:] if steps > 1 else seq[-n:]
-    acc = defaultdict(list)
+        return seq[-min(timed, steps) * nk:]
+    return seq[-(steps - 1) * nk:] if steps > 1 else seq[-nk:]
+
+
+def assign(seq, ops, timed=0):
+    """Per-op average over the timed steps; an op's value is the sum over its kernels."""
+    kop = kernel_ops(ops)
+    nk = len(kop)
+    tail = whole_steps(seq, nk, timed)
+    acc = defaultdict(float)
     for i, v in enumerate(tail):
-        acc[i % n].append(v)
-    return {i: sum(v) / len(v) for i, v in acc.items()}
+        acc[kop[i % nk]] += v
+    steps = len(tail) // nk
+    return {i: v / steps for i, v in acc.items()}
 
 
 def trailing(ops_json: str) -> int:
@@ -78,11 +91,10 @@ def _meta(ops_json: str) -> dict:
 def main():
     fdir, wdir, ops_json, workload, out = sys.argv[1:6]
     ops = json.load(open(ops_json))
-    n = len(ops)
     tr = trailing(ops_json)
     fs, ws = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
-    fetch = assign(fs[:len(fs) - tr], n, timed_steps(ops_json))
-    write = assign(ws[:len(ws) - tr], n, timed_steps(ops_json))
+    fetch = assign(fs[:len(fs) - tr], ops, timed_steps(ops_json))
+    write = assign(ws[:len(ws) - tr], ops, timed_steps(ops_json))
     tab = json.load(open(out)) if os.path.exists(out) else {}
     rows = {}
     for i, op in enumerate(ops):

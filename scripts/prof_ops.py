@@ -36,40 +36,37 @@ def load_trace(d: str):
 
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_traffic import timed_steps, trailing  # noqa: E402
+from pmc_traffic import kernel_ops, timed_steps, trailing, whole_steps  # noqa: E402
 
 
 def main():
     d, ops_json = sys.argv[1], sys.argv[2]
     ops = json.load(open(ops_json))
-    n = len(ops)
+    kop = kernel_ops(ops)
+    nk = len(kop)
     rows = [r for r in load_trace(d) if any(s in (r.get("Kernel_Name") or r.get("kernel_name") or "") for s in OURS)]
     rows = rows[:len(rows) - trailing(ops_json)]
-    steps = len(rows) // n
-    if steps == 0:
+    if len(rows) < nk:
         raise SystemExit("trace shorter than one step")
-    timed = timed_steps(ops_json)
-    if timed:  # the timed region only (bench.py replays graphs with dropped ops before it)
-        tail = rows[-min(timed, steps) * n:]
-    else:
-        tail = rows[-(steps - 1) * n:] if steps > 1 else rows[-n:]  # drop the oldest partial/probe block
-    nsteps = len(tail) // n
-    dur = defaultdict(list)
+    tail = whole_steps(rows, nk, timed_steps(ops_json))  # the timed region only when bench.py says so
+    nsteps = len(tail) // nk
+    per_step = defaultdict(lambda: defaultdict(float))  # op -> step -> summed kernel duration
     gaps = []
     prev_end = None
     for i, r in enumerate(tail):
         s = int(r.get("Start_Timestamp") or r["start_timestamp"])
         e = int(r.get("End_Timestamp") or r["end_timestamp"])
-        dur[i % n].append((e - s) / 1e3)
-        if prev_end is not None and i % n != 0:
+        per_step[kop[i % nk]][i // nk] += (e - s) / 1e3
+        if prev_end is not None and i % nk != 0:
             gaps.append((s - prev_end) / 1e3)
         prev_end = e
     table = []
     for i, op in enumerate(ops):
-        v = sorted(dur[i])
+        v = sorted(per_step[i].values())
         table.append((sum(v) / len(v), v[len(v) // 2], op))
     total = sum(t[0] for t in table)
-    print(f"{nsteps} steps x {n} ops; kernel sum {total:.1f} us/step; mean gap {sum(gaps) / max(1, len(gaps)):.2f} us")
+    print(f"{nsteps} steps x {len(ops)} ops ({nk} kernels); kernel sum {total:.1f} us/step; "
+          f"mean gap {sum(gaps) / max(1, len(gaps)):.2f} us")
     for avg, med, op in sorted(table, key=lambda t: -t[0]):
         ach = (op["flops"] / (avg * 1e-6) / 1e12, "TF") if op["kind"] == "conv" else (op["bytes"] / (avg * 1e-6) / 1e9, "GB/s")
         print(f"{avg:8.2f} us (med {med:7.2f})  {op['kind']:6s} {op['name'][:44]:44s} {op.get('shape', '')[:50]:50s} "
