@@ -610,6 +610,214 @@ __global__ void __launch_bounds__(kThreads) shuffle_conv_kernel(const esm_shuffl
     }
 }
 
+// nf = 8, r = 4, C = 16 on large maps (ESMStereo-S's 4x stage: upsampling4 + tail4x + ref4x.conv1[0]):
+// shuffle_tail4_kernel's tile (L low-res rows x 16 low-res pixels -> a (4L) x 64 x tile, its shuffled
+// map built by MFMA, the tail on the VALU with DPP neighbour columns) plus the one x row above and the
+// one x column left of it that the stride-2 conv needs; x stays in LDS and the conv's (2L) x 32 output
+// tile (all 16 channels) is computed from it, one output pixel per thread.  The tail's arithmetic is
+// shuffle_tail4_kernel's, the conv's the c1in / shuffle_conv_kernel order (taps outer, BN, exact GELU).
+template <int L>
+struct Sc4Geo {
+    static constexpr int NF = 8, R = 4, C = 16;
+    static constexpr int TR = 4 * L;                     // x tile rows (64 columns)
+    static constexpr int SR = TR + 3, SC = 72;           // shuffled map: row 0 = Y0 - 2, col 4 = X0 (cols 2..68 used)
+    static constexpr int LH = L + 2, LW = 18;            // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
+    static constexpr int XR = TR + 1, XC = 72;           // x: row 0 = Y0 - 1, col 4 = X0 (col 3 = X0 - 1)
+    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = OW_TB + 1,
+                         OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, WN = OW_SH + C;
+    static constexpr int XN = NF * LH * LW;
+};
+
+template <int L>
+__global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle_conv_desc d) {
+    using G = Sc4Geo<L>;
+    constexpr int NF = G::NF, C = G::C, SR = G::SR, SC = G::SC, LH = G::LH, LW = G::LW, WN = G::WN, XN = G::XN;
+    constexpr int TR = G::TR, NT = 64 * L;
+    const esm_shuffle_tail_desc& a = d.st;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ float lr[NF][LH][LW];
+    __shared__ __attribute__((aligned(16))) float sh[NF][SR][SC];
+    __shared__ __attribute__((aligned(16))) float xs[G::XR][G::XC];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, HO = 4 * H, WO = 4 * W;
+    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
+    const int b = bk_.z;
+    const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
+    const int Y0 = 4 * ly0, X0 = 4 * lx0;
+    const float* xb = a.x + b * a.xb;
+
+    // ---- stage (one round trip): every weight (head, tail, conv, BN) and the low-res window
+    constexpr int WRN = (WN + NT - 1) / NT, XRN = (XN + NT - 1) / NT;
+    float rw[WRN], rx[XRN];
+#pragma unroll
+    for (int k = 0; k < WRN; ++k) {
+        const int i = tid + k * NT;
+        const float* p;
+        int off;
+        if (i < G::OW_UB) { p = a.up_w; off = i; }
+        else if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
+        else if (i < G::OW_TB) { p = a.tail_w; off = i - G::OW_TW; }
+        else if (i < G::OW_CW) { p = a.tail_b; off = 0; }
+        else if (i < G::OW_SC) { p = d.w; off = (i - G::OW_CW) / C * d.cin_pad * d.cout_pad + (i - G::OW_CW) % C; }
+        else if (i < G::OW_SH) { p = d.scale; off = i - G::OW_SC; }
+        else { p = d.shift; off = i - G::OW_SH; }
+        const bool ok = i < WN && p != nullptr;
+        const float v = (ok ? p : a.up_w)[ok ? off : 0];
+        rw[k] = ok ? v : (i >= G::OW_SC && i < G::OW_SH ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < XRN; ++k) {
+        const int i = tid + k * NT;
+        const int c = i / (LH * LW), rem = i - c * (LH * LW);
+        const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
+        const bool ok = i < XN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+        rx[k] = ok ? v : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < WRN; ++k)
+        if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
+#pragma unroll
+    for (int k = 0; k < XRN; ++k)
+        if (tid + k * NT < XN) (&lr[0][0][0])[tid + k * NT] = rx[k];
+    __syncthreads();
+
+    // ---- shuffled interior (MFMA, as shuffle_tail4_kernel), rows 2 .. TR + 1
+    {
+        const int Y = Y0 + 4 * wave + g, Xl = X0 + 4 * n;
+        float bk[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) bk[kk] = lr[4 * kk + g][wave + 1][n + 1];
+#pragma unroll
+        for (int c = 0; c < NF; ++c) {
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wsh[(c * 16 + n) * NF + 4 * kk + g], bk[kk], acc, 0, 0, 0);
+            conv::floatx4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
+                o[j] = (Y < HO && Xl + j < WO) ? v : 0.f;
+            }
+            *reinterpret_cast<conv::floatx4*>(&sh[c][2 + 4 * wave + g][4 + 4 * n]) = o;
+        }
+    }
+    // ---- the ring (VALU): rows 0, 1 and SR - 1 over cols 2..68, cols 2, 3 and 68 over rows 2..TR + 1
+    auto ring_value = [&](int c, int tr, int tc) __attribute__((always_inline)) {
+        const int Y = Y0 - 2 + tr, X = X0 - 4 + tc;
+        float v = 0.f;
+        if (Y >= 0 && Y < HO && X >= 0 && X < WO) {
+            const int py = (Y >> 2) - (ly0 - 1), px = (X >> 2) - (lx0 - 1);
+            const int m = c * 16 + (Y & 3) * 4 + (X & 3);
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < NF; ++k) acc += wsh[m * NF + k] * lr[k][py][px];
+            v = silu_fast(acc + wsh[G::OW_UB + m]);
+        }
+        sh[c][tr][tc] = v;
+    };
+    constexpr int RROW = SC - 5;  // 67 columns per ring row (2..68)
+    for (int i = tid; i < NF * 3 * RROW; i += NT) {
+        const int c = i / (3 * RROW), q = i - c * (3 * RROW);
+        const int k = q / RROW;
+        ring_value(c, k == 2 ? SR - 1 : k, 2 + q - k * RROW);
+    }
+    for (int i = tid; i < NF * 3 * TR; i += NT) {
+        const int c = i / (3 * TR), q = i - c * (3 * TR);
+        const int k = q / TR;
+        ring_value(c, 2 + q - k * TR, k == 0 ? 2 : (k == 1 ? 3 : 68));
+    }
+    __syncthreads();
+
+    // ---- tail -> x in LDS: lane (g, n) of wave w -> x row Y0 + 4w + g, columns X0 + 4n .. + 3
+    const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
+    {
+        const int oy = Y0 + 4 * wave + g, ox = X0 + 4 * n;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const int edge = n == 0 ? 3 : 68;
+#pragma unroll 2
+        for (int c = 0; c < NF; ++c) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const float* row = &sh[c][4 * wave + g + 1 + ky][0];
+                float v[6];
+                const conv::floatx4 mid4 = *reinterpret_cast<const conv::floatx4*>(row + 4 + 4 * n);
+                const float ev = row[edge];
+                const float lf = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mid4[3]), 0x111, 0xf, 0xf, false));
+                const float rt = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mid4[0]), 0x101, 0xf, 0xf, false));
+                v[0] = n == 0 ? ev : lf;
+                v[1] = mid4[0];
+                v[2] = mid4[1];
+                v[3] = mid4[2];
+                v[4] = mid4[3];
+                v[5] = n == 15 ? ev : rt;
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                }
+            }
+        }
+        conv::floatx4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (oy < HO && ox + j < WO) ? acc[j] + tb : 0.f;  // the conv's zero padding
+        *reinterpret_cast<conv::floatx4*>(&xs[1 + 4 * wave + g][4 + 4 * n]) = o;
+    }
+    // the x row above the tile (row 0, cols 3..67) and the column left of it (col 3, rows 1..TR): VALU
+    for (int i = tid; i < 65 + TR; i += NT) {
+        const int xr = i < 65 ? 0 : 1 + (i - 65), xc = i < 65 ? 3 + i : 3;
+        const int Y = Y0 - 1 + xr, X = X0 - 4 + xc;
+        float acc = 0.f;
+#pragma unroll 2
+        for (int c = 0; c < NF; ++c)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) acc += wsh[G::OW_TW + (c * 3 + ky) * 3 + kx] * sh[c][xr + ky][xc - 1 + kx];
+        xs[xr][xc] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc + tb : 0.f;
+    }
+    __syncthreads();
+
+    // ---- c1 = GELU(BN(conv 3x3 s2 p1 (x))): thread = one output pixel of the (2L) x 32 tile, all C channels
+    {
+        const int yy = tid >> 5, xx = tid & 31;
+        const int oy = Y0 / 2 + yy, ox = X0 / 2 + xx;
+        float xv[9];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) xv[ky * 3 + kx] = xs[2 * yy + ky][3 + 2 * xx + kx];
+        const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
+        const bool ok = oy < Ho2 && ox < Wo2;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            d.out + b * d.ob, static_cast<short>(0), static_cast<int>(4 * ((C - 1) * d.oc + (Ho2 - 1) * d.oh + Wo2)),
+            0x00020000);
+        const unsigned pix = 4u * static_cast<unsigned>(oy * d.oh + ox);
+#pragma unroll
+        for (int co = 0; co < C; ++co) {
+            float acc = 0.f;
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) acc += wsh[G::OW_CW + tp * C + co] * xv[tp];
+            const float v = gelu_erf(acc * wsh[G::OW_SC + co] + wsh[G::OW_SH + co]);
+            conv::store_b32(__float_as_uint(v), ro, static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
+        }
+    }
+}
+
+template <int L>
+int launch_sc4(const esm_shuffle_conv_desc& a, hipStream_t s) {
+    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
+    hipLaunchKernelGGL((shuffle_conv4_kernel<L>), grid, dim3(64 * L), 0, s, a);
+    return check_launch("shuffle_conv");
+}
+
 template <int NF, int R, int C>
 int launch_sc(const esm_shuffle_conv_desc& a, hipStream_t s) {
     const esm_shuffle_tail_desc& t = a.st;
@@ -655,7 +863,14 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
     const long long Ho2 = (static_cast<long long>(t.H) * t.r + 1) / 2, Wo2 = (static_cast<long long>(t.W) * t.r + 1) / 2;
     if (a.oh < Wo2 || a.oc < Ho2 * a.oh || a.ob < a.C * a.oc) return arg_error("shuffle_conv: output strides");
     if (4 * (a.C * a.oc) >= 0x7fffffffLL) return arg_error("shuffle_conv: output too large");
-    if (t.nf == 8 && t.r == 4 && a.C == 16) return launch_sc<8, 4, 16>(a, s);
+    if (t.nf == 8 && t.r == 4 && a.C == 16) {
+        // st.flags bits 1-2: 0 automatic, 1 the window form, 2 the row form (shuffle_conv4_kernel, 8 low-res
+        // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
+        const int form = (t.flags >> 1) & 3;
+        const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
+        if (form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
+        return launch_sc<8, 4, 16>(a, s);
+    }
     if (t.nf == 8 && t.r == 2 && a.C == 16) return launch_sc<8, 2, 16>(a, s);
     if (t.nf == 16 && t.r == 2 && a.C == 32) return launch_sc<16, 2, 32>(a, s);
     if (t.nf == 16 && t.r == 4 && a.C == 32) return launch_sc<16, 4, 32>(a, s);

@@ -830,9 +830,10 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
 # tail(upsampling(x)) and the refinement's first conv in one launch (esm_shuffle_conv_f32);
 # ESM_SHUFFLE_CONV=0 runs them as two launches (A/B measurements)
 SHUFFLE_CONV_ENABLED = os.environ.get("ESM_SHUFFLE_CONV", "1") != "0"
-# largest low-resolution input (B * H * W) it is used on: measured faster than the two launches at S-K's 2x
-# stage (24x78 in: 8.4 vs 10.5 us) and slower at the 4x stage (96x312 in: 23.2 vs 20.8 us)
-SHUFFLE_CONV_MAX_PIX = int(os.environ.get("ESM_SHUFFLE_CONV_MAXPIX", "8192"))
+# largest low-resolution input (B * H * W) it is used on.  Round 3: faster than the two launches at S-K's
+# 2x stage (24x78 in: 8.4 vs 10.5 us), slower at the 4x stage (96x312 in: 23.2 vs 20.8 us) with the
+# window form; round 4 adds the row form there (shuffle_conv4_kernel)
+SHUFFLE_CONV_MAX_PIX = int(os.environ.get("ESM_SHUFFLE_CONV_MAXPIX", str(1 << 30)))
 
 
 def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[torch.Tensor] = None) -> bool:
@@ -844,10 +845,11 @@ def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[t
 
 
 def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: PackedConv,
-                     tag: str = "shuffle_conv") -> torch.Tensor:
+                     tag: str = "shuffle_conv", form: int = 0) -> torch.Tensor:
     """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
     3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
-    stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)]."""
+    stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)].  ``form`` (nf 8, r 4, C 16): 0
+    automatic, 1 the window form, 2 the row form."""
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
@@ -866,6 +868,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     t.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
     t.out = None
     t.B, t.nf, t.H, t.W, t.r = B, nf, H, W, r
+    t.flags = (1 if B * H * W * r * r >= XCD_SLAB_MIN_PIX else 0) | (int(form) & 3) << 1
     d.w = conv.w.data_ptr()
     d.scale = conv.scale.data_ptr() if conv.scale is not None else None
     d.shift = conv.shift.data_ptr() if conv.shift is not None else None

@@ -223,7 +223,8 @@ typedef struct {
  * (up_refinement.conv1[0], models/ESMStereo.py:190-191), in one launch; the 1-channel map between
  * them is never stored.  w: packed conv weights [9][cin_pad][cout_pad] (cin 1); scale/shift: the
  * folded BN (scale NULL = 1); out: [B, C, ceil(r*H/2), ceil(r*W/2)] with strides ob, oc, oh.
- * (nf, r, C) in {(8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)}. */
+ * (nf, r, C) in {(8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)}.  st.flags bit 0: XCD-slab tile order;
+ * bits 1-2, (8, 4, 16) only: 0 automatic, 1 the low-res-window form, 2 the MFMA row form. */
 typedef struct {
     esm_shuffle_tail_desc st;
     const float* w;

@@ -13,4 +13,8 @@ timeout -k 10 200 python -u scripts/probes/conv_forms.py > gpurun_out/conv_forms
 tail -40 gpurun_out/conv_forms.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_t.log 2>&1 || { tail -20 gpurun_out/bench_t.log; exit 1; }
 tail -1 gpurun_out/bench_t.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['forward_e2e'], d['epe_vs_reference'])"
+timeout -k 10 300 env ESM_SHUFFLE_CONV_MAXPIX=8192 python -u bench.py --no-extra --no-cpu-baseline > gpurun_out/bench_t_ab.log 2>&1 || { tail -20 gpurun_out/bench_t_ab.log; exit 1; }
+tail -1 gpurun_out/bench_t_ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('A/B 4x shuffle_conv off:', d['value'], d['ms_per_step'])"
+NO_PMC=1 bash scripts/gpu_prof.sh SK > gpurun_out/prof_SK_summary.txt 2>&1 || { tail -20 gpurun_out/prof_SK_summary.txt; exit 1; }
+head -16 gpurun_out/prof_SK_summary.txt
 NO_PMC=1 CONFIGS=1 bash scripts/gpu_r04_L.sh

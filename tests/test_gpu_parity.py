@@ -668,7 +668,8 @@ def test_shuffle_tail(nf, r, H, W):
 
 
 @pytest.mark.parametrize("nf,r,C,H,W", [(8, 4, 16, 24, 78), (8, 4, 16, 96, 312), (8, 4, 16, 7, 13), (8, 2, 16, 13, 29),
-                                         (16, 2, 32, 17, 40), (16, 4, 32, 9, 21), (8, 2, 16, 48, 156)])
+                                         (16, 2, 32, 17, 40), (16, 4, 32, 9, 21), (8, 2, 16, 48, 156),
+                                         (8, 4, 16, 21, 37)])
 def test_shuffle_conv_fused(nf, r, C, H, W):
     """tail(upsampling(x)) + the refinement's first BasicConv(1, C, 3, 2, 1) in one launch
     (esm_shuffle_conv_f32, models/ESMStereo.py:301-303 + :190-191) vs fp64 torch of the three reference
@@ -685,11 +686,12 @@ def test_shuffle_conv_fused(nf, r, C, H, W):
     p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), r)
     pc = pk(conv, bn, ACT_GELU)
     ctx = Ctx(DEV)
-    y = run_shuffle_conv(ctx, x.to(DEV), p, pc)
-    assert y.shape == ref.shape
-    assert rel(y, ref) < 1e-5
     two = run_conv(ctx, pc, [run_shuffle_tail(ctx, x.to(DEV), p)])
-    assert rel(y, two) < 1e-5
+    for form in ((0, 1, 2) if (nf, r) == (8, 4) else (0,)):  # (8, 4): the window and the row form
+        y = run_shuffle_conv(ctx, x.to(DEV), p, pc, form=form)
+        assert y.shape == ref.shape
+        assert rel(y, ref) < 1e-5, form
+        assert rel(y, two) < 1e-5, form
 
 
 PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones
