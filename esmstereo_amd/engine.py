@@ -437,6 +437,9 @@ def eager_emit(device: torch.device, fn, *args, **kw):
 # (round 3, S-K, rocprofv3 op maps; every launch remapped: +10 us on the S-K step).
 HINT_XCD_SLAB = 1 << 30
 XCD_SLAB_MIN_PIX = int(os.environ.get("ESM_XCD_SLAB_MIN_PIX", "65536"))
+# the same order on 3-D volumes (B x D x H x W output or input voxels over the threshold); ESM_XCD_SLAB_3D=0
+# leaves every 3-D launch in the default order (A/B measurements)
+XCD_SLAB_3D = os.environ.get("ESM_XCD_SLAB_3D", "1") != "0"
 
 # shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
 _TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
@@ -580,7 +583,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
-    if B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX:
+    if B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX and (nd == 2 or XCD_SLAB_3D):
         d.hint |= HINT_XCD_SLAB
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd

@@ -17,5 +17,5 @@ pass() {
 pass 1 SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU &&
 pass 2 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE || exit $?
 python3 scripts/pmc_ops.py $OUT/ops.json $OUT/p1 $OUT/p2 > $OUT/summary.txt
-grep -E "agg_1|conv1.1 |op name" $OUT/summary.txt
+head -70 $OUT/summary.txt
 rm -rf $OUT/p1 $OUT/p2
