@@ -31,8 +31,11 @@ constexpr int kWideThreads = 256;
 // so a 192x624 layer runs ~2 waves per SIMD instead of ~1 (one wave alone leaves the MFMA pipe idle
 // across its dependency and memory stalls); the two partial row blocks meet in
 // LDS once, after the last MFMA, and each wave finishes half of the rows.
-template <int K, int NG, int MT, int R, int ACT, bool PLAIN, int KS = 1>
-__global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a) {
+// WIN: every source inside one buffer window (conv_direct.h source_window: the plan's arena) -> one
+// descriptor, a group's source folded into its voffsets; else a descriptor per source, picked per group.
+template <int K, int NG, int MT, int R, int ACT, bool PLAIN, int KS, bool WIN>
+__global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc a, const float* wbase, int wspan,
+                                                             int d0, int d1, int d2) {
     constexpr int NR = R + K - 1;  // input rows a wave reads
     constexpr int NGW = (NG + KS - 1) / KS;  // channel groups per wave
     static_assert(KS == 1 || (KS == 2 && R % 2 == 0), "K split: two waves, an even row block");
@@ -72,10 +75,11 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
             shf[mt][j] = a.shift ? a.shift[co] : 0.f;
         }
 
-    // ---- input addressing: one descriptor per source over this batch item (the sources may lie
-    //      anywhere: a caller's feature map next to the plan's own buffers); a concat splits on 4-channel
-    //      boundaries (direct_ok), so a group's source is wave-uniform and picked per group by a scalar
-    //      select; the group's channel is folded into its per-lane voffsets once
+    // ---- input addressing.  WIN: one descriptor over the sources' window, a group's source, batch item
+    //      and channel folded into its per-lane voffsets once.  Else one descriptor per source over this
+    //      batch item (the sources may lie anywhere: a caller's feature map next to the plan's own
+    //      buffers); a concat splits on 4-channel boundaries (direct_ok), so a group's source is
+    //      wave-uniform and picked per group by a scalar select
     const int sh = static_cast<int>(a.src[0].sh);
     const int ns = a.nsrc;
     const int lo1 = a.src[0].C, lo2 = a.src[0].C + (ns > 1 ? a.src[1].C : 0);
@@ -84,25 +88,32 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
                                                  4 * ((q.C - 1) * static_cast<int>(q.sc) + (a.Hi - 1) * sh + a.Wi),
                                                  0x00020000);
     };
-    const __amdgpu_buffer_rsrc_t rs0 = src_rsrc(a.src[0]);
-    const __amdgpu_buffer_rsrc_t rs1 = ns > 1 ? src_rsrc(a.src[1]) : rs0;
-    const __amdgpu_buffer_rsrc_t rs2 = ns > 2 ? src_rsrc(a.src[2]) : rs0;
-    const int sc0 = static_cast<int>(a.src[0].sc);
-    const int sc1 = ns > 1 ? static_cast<int>(a.src[1].sc) : sc0, sc2 = ns > 2 ? static_cast<int>(a.src[2].sc) : sc0;
+    const __amdgpu_buffer_rsrc_t rs0 = WIN ? __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), static_cast<short>(0),
+                                                                               wspan, 0x00020000)
+                                           : src_rsrc(a.src[0]);
+    const __amdgpu_buffer_rsrc_t rs1 = !WIN && ns > 1 ? src_rsrc(a.src[1]) : rs0;
+    const __amdgpu_buffer_rsrc_t rs2 = !WIN && ns > 2 ? src_rsrc(a.src[2]) : rs0;
     const int xo = x0 + n16;
     int gs[NGW];          // source of group g (wave-uniform)
-    unsigned vo[NGW][K];  // per-lane byte offset of group g's channel at column shift dx, in its source
+    unsigned vo[NGW][K];  // per-lane byte offset of group g's channel at column shift dx
 #pragma unroll
     for (int g = 0; g < NGW; ++g) {
         const int cg = 4 * (gb + g);
         gs[g] = cg < lo1 ? 0 : (cg < lo2 ? 1 : 2);
         const int c = cg + kq;
-        const int cl = c - (gs[g] == 0 ? 0 : (gs[g] == 1 ? lo1 : lo2));
-        const int sc = gs[g] == 0 ? sc0 : (gs[g] == 1 ? sc1 : sc2);
+        const int s = gs[g];
+        const int cl = c - (s == 0 ? 0 : (s == 1 ? lo1 : lo2));
+        const long long sb = s == 0 ? a.src[0].sb : (s == 1 ? a.src[1].sb : a.src[2].sb);
+        const long long sc = s == 0 ? a.src[0].sc : (s == 1 ? a.src[1].sc : a.src[2].sc);
+        const int dl = s == 0 ? d0 : (s == 1 ? d1 : d2);
 #pragma unroll
         for (int dx = 0; dx < K; ++dx) {
             const int xi = xo - a.pw + dx;
-            vo[g][dx] = (c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi) ? 4u * static_cast<unsigned>(cl * sc + xi) : kOOB;
+            const bool ok = c < a.Cin && xo < a.Wo && xi >= 0 && xi < a.Wi;
+            if constexpr (WIN)
+                vo[g][dx] = ok ? static_cast<unsigned>(dl + 4 * (b * sb + cl * sc + xi)) : kOOB;
+            else
+                vo[g][dx] = ok ? 4u * static_cast<unsigned>(cl * static_cast<int>(sc) + xi) : kOOB;
         }
     }
     auto load_row = [&](float (&dst)[NGW][K], int r) {  // input row y0 - ph + r
@@ -112,7 +123,7 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
         for (int g = 0; g < NGW; ++g)
 #pragma unroll
             for (int dx = 0; dx < K; ++dx)
-                dst[g][dx] = buf_load_s(gs[g] == 0 ? rs0 : (gs[g] == 1 ? rs1 : rs2), vo[g][dx], roff);
+                dst[g][dx] = buf_load_s(WIN ? rs0 : (gs[g] == 0 ? rs0 : (gs[g] == 1 ? rs1 : rs2)), vo[g][dx], roff);
     };
 
     floatx4 acc[R][MT];
@@ -229,14 +240,24 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
     const bool ks2 = (a.hint & (1 << 28)) && NG >= 2 && R >= 4;
     const dim3 grid(ceil_div(a.Wo, ks2 ? 32 : 64), ceil_div(a.Ho, R), static_cast<unsigned>(a.B));
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv(wide): grid too large");
+    const float* base = nullptr;
+    int span = 0, dl[ESM_MAX_SRC] = {0, 0, 0};
+    const bool win = source_window(a, &base, &span, dl);
     // BasicConv (BN + GELU, nothing else: the hot path's common case) compiled with the activation
     // folded in and the branch-free buffer-store epilogue; anything else takes the general epilogue
     const bool gelu = a.act == ESM_ACT_GELU && !a.res && !a.out2 && a.post_scale == 1.f &&
                       static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
-#define ESM_WIDE(RR, AC)                                                                                         \
-    hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU)>), grid, dim3(kWideThreads), 0, s, a)
-#define ESM_WIDE2(RR, AC)                                                                                        \
-    hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU), 2>), grid, dim3(kWideThreads), 0, s, a)
+#define ESM_WIDE_W(RR, AC, KSP)                                                                                \
+    do {                                                                                                        \
+        if (win)                                                                                                \
+            hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU), KSP, true>), grid,         \
+                               dim3(kWideThreads), 0, s, a, base, span, dl[0], dl[1], dl[2]);                   \
+        else                                                                                                    \
+            hipLaunchKernelGGL((wconv_kernel<K, NG, MT, RR, AC, (AC == ESM_ACT_GELU), KSP, false>), grid,        \
+                               dim3(kWideThreads), 0, s, a, base, span, 0, 0, 0);                               \
+    } while (0)
+#define ESM_WIDE(RR, AC) ESM_WIDE_W(RR, AC, 1)
+#define ESM_WIDE2(RR, AC) ESM_WIDE_W(RR, AC, 2)
     if constexpr (NG >= 2) {
         if (ks2) {
             if (R == 8) {
@@ -261,6 +282,7 @@ int launch_wide_r(const esm_conv_desc& a, hipStream_t s) {
     }
 #undef ESM_WIDE
 #undef ESM_WIDE2
+#undef ESM_WIDE_W
     return check_launch("conv(wide)");
 }
 
