@@ -620,6 +620,10 @@ def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]
     return len(srcs) == 1 or all(int(t.shape[1]) % 4 == 0 for t in srcs)
 
 
+# every supported pair on maps of at most this many output pixels (A/B knob; 0 = the rules below only)
+PAIR2_SMALL_MAXPIX = int(os.environ.get("ESM_PAIR2_SMALL_MAXPIX", "0"))
+
+
 def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
     """Where the hot path takes the fused pair.  Measured in the S-K chain (rocprofv3, round 3): the pair
     wins where convA is light -- the dm stacks' 5x5 single-channel head (dm.0 + dm.1: 6.1 vs 9.1 us at
@@ -634,6 +638,8 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     Ho = (int(srcs[0].shape[2]) + 2 * pa.pad - pa.k) // pa.stride + 1
     Wo = (int(srcs[0].shape[3]) + 2 * pa.pad - pa.k) // pa.stride + 1
     light = pa.cin * pa.k * pa.k
+    if B * Ho * Wo <= PAIR2_SMALL_MAXPIX:
+        return True
     return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 

@@ -12,6 +12,8 @@ dev = torch.device("cuda")
 T3 = 1 << 23
 NOTILE = 1 << 19  # conv.hip kHintNoTile: the automatic rules without the tiled forms
 CASES = [  # name, nd, cins, cout, k, s, p, spatial, B
+    ("L group_stem B4", 3, (32,), 8, 3, 1, 1, (48, 96, 312), 4),
+    ("L agg B4", 3, (8,), 8, 3, 1, 1, (48, 96, 312), 4),
     ("S ref4x.conv1.1", 2, (16,), 16, 3, 1, 1, (192, 624), 1),
     ("S ref4x.agg_1.0", 2, (16, 16, 24), 16, 1, 1, 0, (192, 624), 1),
     ("S ref4x.conv2.0", 2, (16,), 16, 3, 2, 1, (192, 624), 1),
@@ -57,8 +59,11 @@ for name, nd, cins, cout, k, s, p, sp, B in CASES:
     ctx = Ctx(dev)
     out = run_conv(ctx, pc, xs)
     res = {}
-    for label, hint in [("auto", 0), ("no tile", NOTILE), ("tile r1", T3 | 1 << 26), ("tile r2", T3 | 2 << 26),
-                        ("tile r4", T3 | 3 << 26)]:
+    forms = [("auto", 0), ("no tile", NOTILE), ("tile r1", T3 | 1 << 26), ("tile r2", T3 | 2 << 26),
+             ("tile r4", T3 | 3 << 26)]
+    if len(sys.argv) > 1 and not any(f in name for f in sys.argv[1:]):
+        continue
+    for label, hint in forms:
         try:
             y = run_conv(ctx, pc, xs, hint=hint)
             err = float((y - out).abs().max() / out.abs().max())
