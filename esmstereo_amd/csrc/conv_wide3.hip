@@ -194,11 +194,12 @@ __global__ void __launch_bounds__(64 * KSW) wconv3r_kernel(const esm_conv_desc a
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int n16 = lane & 15, kq = lane >> 4;
-    const int x0 = blockIdx.x * 16;
-    const int y0 = blockIdx.y * RB;
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
+    const int x0 = bk_.x * 16;
+    const int y0 = bk_.y * RB;
     const int nzb = (a.Do + 1) / 2;
-    const int b = blockIdx.z / nzb;
-    const int z0 = (blockIdx.z - b * nzb) * 2;  // the plane pair z0, z0 + 1
+    const int b = bk_.z / nzb;
+    const int z0 = (bk_.z - b * nzb) * 2;  // the plane pair z0, z0 + 1
 
     // weights of group `wave` for the 4 pair-relative input planes (rows 8-15 of the MFMA lag one plane)
     float wv[4][9];

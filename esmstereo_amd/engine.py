@@ -440,6 +440,12 @@ XCD_SLAB_MIN_PIX = int(os.environ.get("ESM_XCD_SLAB_MIN_PIX", "65536"))
 # the same order on 3-D volumes (B x D x H x W output or input voxels over the threshold); ESM_XCD_SLAB_3D=0
 # leaves every 3-D launch in the default order (A/B measurements)
 XCD_SLAB_3D = os.environ.get("ESM_XCD_SLAB_3D", "1") != "0"
+# 3-D launches with >= 32 input channels from this many output voxels: the S / M `group_stem` (12x24x78),
+# whose 32-channel input each workgroup re-reads with its halo: 15.8 -> 7.8 MB per launch, step time
+# unchanged (round 4, two alternations, profiles/r04_xcd_group_stem_SK.txt)
+XCD_SLAB_MIN_VOX_WIDE = int(os.environ.get("ESM_XCD_SLAB_MIN_VOX_WIDE", "16384"))
+# launches (by name, comma-separated) given the slab order whatever their size (A/B measurements)
+XCD_SLAB_OPS = tuple(t for t in os.environ.get("ESM_XCD_SLAB_OPS", "").split(",") if t)
 
 # shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
 _TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
@@ -583,7 +589,9 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
     d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
-    if B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX and (nd == 2 or XCD_SLAB_3D):
+    if (B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX and (nd == 2 or XCD_SLAB_3D)) or \
+            (nd == 3 and XCD_SLAB_3D and pc.cin >= 32 and B * Do * Ho * Wo >= XCD_SLAB_MIN_VOX_WIDE) or \
+            tag in XCD_SLAB_OPS:
         d.hint |= HINT_XCD_SLAB
     ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
     taps = pc.k ** nd
