@@ -145,7 +145,14 @@ def test_plan_per_op_cost(case):
 
 
 def test_shuffle_head_flops_s_k():
-    """upsampling4 + tail4x at S-K is 2 * 384 * 1248 * 8 * (8 + 9) = 130.35 MFLOP."""
+    """upsampling4 + tail4x at S-K is 2 * 384 * 1248 * 8 * (8 + 9) = 130.35 MFLOP; fused with
+    ref4x.conv1[0] (the row-form shuffle_conv, round 4) plus the 1 -> 16 3x3 stride-2 conv on 192 x 624."""
     _, _, meta, _ = _plan("S-K")
-    op = next(x for x in meta if x["name"] == "upsample_module.upsampling4+tail4x")
-    assert op["flops"] == 2 * 384 * 1248 * 8 * 17 == 130_351_104
+    op = next(x for x in meta if x["name"].startswith("upsample_module.upsampling4+tail4x"))
+    head = 2 * 384 * 1248 * 8 * 17
+    assert head == 130_351_104
+    if op["name"].endswith("+ref4x.conv1.0"):
+        assert op["kind"] == "shuffle_conv"
+        assert op["flops"] == head + 2 * 192 * 624 * 16 * 9
+    else:
+        assert op["flops"] == head
