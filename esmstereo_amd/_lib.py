@@ -77,7 +77,10 @@ class EsmShuffleTailDesc(Structure):
 class EsmShuffleConvDesc(Structure):
     _fields_ = [("st", EsmShuffleTailDesc), ("w", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
                 ("out", c_void_p), ("ob", c_int64), ("oc", c_int64), ("oh", c_int64),
-                ("C", c_int32), ("cin_pad", c_int32), ("cout_pad", c_int32), ("reserved", c_int32)]
+                ("C", c_int32), ("cin_pad", c_int32), ("cout_pad", c_int32), ("reserved", c_int32),
+                ("pre_x", c_void_p), ("pb", c_int64), ("pc", c_int64), ("ph", c_int64), ("pre_w", c_void_p),
+                ("pre_scale", c_void_p), ("pre_shift", c_void_p), ("pre_cin", c_int32), ("pre_cin_pad", c_int32),
+                ("pre_cout_pad", c_int32), ("pre_reserved", c_int32)]
 
 
 class EsmConfDesc(Structure):

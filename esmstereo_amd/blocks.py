@@ -23,8 +23,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail, param_token, run_conv,
-                     run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_supported)
+from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail, pair2_auto, param_token,
+                     run_conv, run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_pre_supported,
+                     shuffle_conv_supported)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -259,7 +260,17 @@ class _ESMUpsampler(nn.Module):
             d = _pair(ctx, dm[0], [prev], dm[1])
             d = _pair(ctx, dm[2], [d], dm[3])
             spx = getattr(self, f"spx_{tag}")
-            c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
+            ref = getattr(self, f"ref{tag}")
+            # spx_<t>[1] inside the row-form head + ref conv launch where it fits (stages after the first;
+            # the first one's c feeds to_feat and the FMBlocks), else the pair / two launches
+            pre = None
+            if i > 0 and not pair2_auto(spx[0].packed(), p[f"spx1_{tag}"], [d, feats[cat_i]]) and \
+                    shuffle_conv_pre_supported(p[f"up_{tag}"], ref.conv1[0].packed(), p[f"spx1_{tag}"]) and \
+                    shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed(), d):
+                c = run_conv(ctx, spx[0].packed(), [d, feats[cat_i]], tag=getattr(spx[0], "_esm_name", "spx.0"))
+                pre = p[f"spx1_{tag}"]
+            else:
+                c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c
             if i == 0:
                 x = run_conv(ctx, p["to_feat"], [x], tag=f"{me}.to_feat")
@@ -267,9 +278,12 @@ class _ESMUpsampler(nn.Module):
                     x = blk.emit(ctx, x)
             # upsampling (1x1 -> PixelShuffle -> SiLU) + tail (3x3 -> 1): one launch, with the refinement
             # hourglass's first conv fused behind it where the kernel has the shape
-            ref = getattr(self, f"ref{tag}")
             c10 = None
-            if shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed(), x):
+            if pre is not None:
+                c10 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(), pre=pre,
+                                       tag=f"{me}.spx_{tag}.1+upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1.0")
+                x = None
+            elif shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed(), x):
                 c10 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(),
                                        tag=f"{me}.upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1.0")
                 x = None

@@ -626,9 +626,14 @@ struct Sc4Geo {
     static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = OW_TB + 1,
                          OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, WN = OW_SH + C;
     static constexpr int XN = NF * LH * LW;
+    // the pre-conv (PRE): its input window (16 channels x (LH + 2) x (LW + 2), channel stride 240 = 16 mod 32
+    // banks), its weights as the MFMA A image [tap][ci 16][co 16] and BN (8 + 8)
+    static constexpr int PCH = 16, PR = LH + 2, PW = LW + 2, PCS = PR * PW, PXN = PCH * PCS;
+    static constexpr int PWN = 9 * 16 * 16, PBN = 2 * NF;
+    static constexpr int PNT = (LH * LW + 15) / 16;  // pre-conv N tiles (16 window pixels each)
 };
 
-template <int L>
+template <int L, bool PRE>
 __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle_conv_desc d) {
     using G = Sc4Geo<L>;
     constexpr int NF = G::NF, C = G::C, SR = G::SR, SC = G::SC, LH = G::LH, LW = G::LW, WN = G::WN, XN = G::XN;
@@ -638,6 +643,8 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
     __shared__ float lr[NF][LH][LW];
     __shared__ __attribute__((aligned(16))) float sh[NF][SR][SC];
     __shared__ __attribute__((aligned(16))) float xs[G::XR][G::XC];
+    __shared__ float pxs[PRE ? G::PXN : 1];
+    __shared__ float pws[PRE ? G::PWN + G::PBN : 1];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, g = lane >> 4, n = lane & 15;
@@ -647,7 +654,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
     const int b = bk_.z;
     const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
     const int Y0 = 4 * ly0, X0 = 4 * lx0;
-    const float* xb = a.x + b * a.xb;
+    const float* xb = PRE ? nullptr : a.x + b * a.xb;
 
     // ---- stage (one round trip): every weight (head, tail, conv, BN) and the low-res window
     constexpr int WRN = (WN + NT - 1) / NT, XRN = (XN + NT - 1) / NT;
@@ -668,22 +675,97 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         const float v = (ok ? p : a.up_w)[ok ? off : 0];
         rw[k] = ok ? v : (i >= G::OW_SC && i < G::OW_SH ? 1.f : 0.f);
     }
+    if constexpr (!PRE) {
 #pragma unroll
-    for (int k = 0; k < XRN; ++k) {
-        const int i = tid + k * NT;
-        const int c = i / (LH * LW), rem = i - c * (LH * LW);
-        const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
-        const bool ok = i < XN && yy >= 0 && yy < H && xx >= 0 && xx < W;
-        const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
-        rx[k] = ok ? v : 0.f;
+        for (int k = 0; k < XRN; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / (LH * LW), rem = i - c * (LH * LW);
+            const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
+            const bool ok = i < XN && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+            rx[k] = ok ? v : 0.f;
+        }
+    }
+    // PRE: the pre-conv's input window (rows ly0 - 2 .., cols lx0 - 2 ..; zero outside the image: the
+    // conv's padding), weights and BN
+    constexpr int PXR = PRE ? (G::PXN + NT - 1) / NT : 1, PWR = PRE ? (G::PWN + G::PBN + NT - 1) / NT : 1;
+    float rp[PXR], rq[PWR];
+    if constexpr (PRE) {
+        const float* pb = d.pre_x + b * d.pb;
+#pragma unroll
+        for (int k = 0; k < PXR; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / G::PCS, rem = i - c * G::PCS;
+            const int yy = ly0 - 2 + rem / G::PW, xx = lx0 - 2 + rem % G::PW;
+            const bool ok = i < G::PXN && c < d.pre_cin && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = pb[ok ? c * d.pc + yy * d.ph + xx : 0];
+            rp[k] = ok ? v : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < PWR; ++k) {
+            const int i = tid + k * NT;
+            float v = 0.f;
+            if (i < G::PWN) {  // [tap][ci][co] <- packed [tap][cin_pad][cout_pad]
+                const int co = i & 15, ci = (i >> 4) & 15, tap = i >> 8;
+                const bool ok = ci < d.pre_cin && co < NF;
+                const float u = d.pre_w[ok ? (tap * d.pre_cin_pad + ci) * d.pre_cout_pad + co : 0];
+                v = ok ? u : 0.f;
+            } else if (i < G::PWN + G::PBN) {
+                const int j = i - G::PWN;
+                const float* q = j < NF ? d.pre_scale : d.pre_shift;
+                const float u = (q ? q : d.pre_w)[q ? (j & (NF - 1)) : 0];
+                v = q ? u : (j < NF ? 1.f : 0.f);
+            }
+            rq[k] = v;
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < WRN; ++k)
         if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
+    if constexpr (!PRE) {
 #pragma unroll
-    for (int k = 0; k < XRN; ++k)
-        if (tid + k * NT < XN) (&lr[0][0][0])[tid + k * NT] = rx[k];
+        for (int k = 0; k < XRN; ++k)
+            if (tid + k * NT < XN) (&lr[0][0][0])[tid + k * NT] = rx[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < PXR; ++k)
+            if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
+#pragma unroll
+        for (int k = 0; k < PWR; ++k)
+            if (tid + k * NT < G::PWN + G::PBN) pws[tid + k * NT] = rq[k];
+        __syncthreads();
+        // x = GELU(BN(conv3x3(pre_x))) on the low-res window (MFMA: M = the nf couts (rows 8..15 zero weights),
+        // N = 16 window pixels, K = 16 channels x 9 taps), zero outside the image (the head's window padding)
+        for (int nt = wave; nt < G::PNT; nt += NT / 64) {
+            const int p = nt * 16 + n;
+            const int pp = p < LH * LW ? p : 0;
+            const int py = pp / LW, px = pp - (pp / LW) * LW;
+            // two accumulation chains (even / odd channel groups): a dependent MFMA waits for its predecessor
+            conv::floatx4 acc2[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int ci = 4 * ks + g;
+                    acc2[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        pws[(tap * 16 + ci) * 16 + n], pxs[ci * G::PCS + (py + dy) * G::PW + px + dx], acc2[ks & 1], 0, 0, 0);
+                }
+            }
+            const conv::floatx4 acc = acc2[0] + acc2[1];
+            const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
+            const bool in = p < LH * LW && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            if (g < 2 && p < LH * LW) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g + j;
+                    const float v = gelu_erf(acc[j] * pws[G::PWN + co] + pws[G::PWN + NF + co]);
+                    lr[co][py][px] = in ? v : 0.f;
+                }
+            }
+        }
+    }
     __syncthreads();
 
     // ---- shuffled interior (MFMA, as shuffle_tail4_kernel), rows 2 .. TR + 1
@@ -814,7 +896,10 @@ template <int L>
 int launch_sc4(const esm_shuffle_conv_desc& a, hipStream_t s) {
     const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
-    hipLaunchKernelGGL((shuffle_conv4_kernel<L>), grid, dim3(64 * L), 0, s, a);
+    if (a.pre_x)
+        hipLaunchKernelGGL((shuffle_conv4_kernel<L, true>), grid, dim3(64 * L), 0, s, a);
+    else
+        hipLaunchKernelGGL((shuffle_conv4_kernel<L, false>), grid, dim3(64 * L), 0, s, a);
     return check_launch("shuffle_conv");
 }
 
@@ -856,9 +941,17 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
     if (!d) return arg_error("shuffle_conv: null descriptor");
     const esm_shuffle_conv_desc& a = *d;
     const esm_shuffle_tail_desc& t = a.st;
-    if (!t.x || !t.up_w || !t.up_b || !t.tail_w || !a.w || !a.out) return arg_error("shuffle_conv: null pointer");
+    if (!(a.pre_x ? !t.x : t.x != nullptr) || !t.up_w || !t.up_b || !t.tail_w || !a.w || !a.out)
+        return arg_error("shuffle_conv: null pointer (or both st.x and pre_x set)");
+    if (a.pre_x) {
+        if (!(t.nf == 8 && t.r == 4 && a.C == 16) || (t.flags >> 1 & 3) == 1)
+            return arg_error("shuffle_conv: the pre-conv needs nf 8, r 4, C 16 and the row form");
+        if (!a.pre_w || a.pre_cin < 1 || a.pre_cin > 16 || a.pre_cin_pad < a.pre_cin || a.pre_cout_pad < t.nf)
+            return arg_error("shuffle_conv: bad pre-conv weights / channels");
+        if (a.ph < t.W || a.pc < static_cast<long long>(t.H) * a.ph) return arg_error("shuffle_conv: pre_x strides");
+    }
     if (t.B <= 0 || t.H <= 0 || t.W <= 0) return arg_error("shuffle_conv: bad size");
-    if (t.xh < t.W || t.xc < static_cast<long long>(t.H) * t.xh) return arg_error("shuffle_conv: strides inconsistent");
+    if (t.x && (t.xh < t.W || t.xc < static_cast<long long>(t.H) * t.xh)) return arg_error("shuffle_conv: strides inconsistent");
     if (a.cin_pad < 1 || a.cout_pad < a.C) return arg_error("shuffle_conv: bad conv weight padding");
     const long long Ho2 = (static_cast<long long>(t.H) * t.r + 1) / 2, Wo2 = (static_cast<long long>(t.W) * t.r + 1) / 2;
     if (a.oh < Wo2 || a.oc < Ho2 * a.oh || a.ob < a.C * a.oc) return arg_error("shuffle_conv: output strides");
@@ -868,7 +961,7 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
         const int form = (t.flags >> 1) & 3;
         const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
-        if (form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
+        if (a.pre_x || form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
         return launch_sc<8, 4, 16>(a, s);
     }
     if (t.nf == 8 && t.r == 2 && a.C == 16) return launch_sc<8, 2, 16>(a, s);

@@ -861,15 +861,36 @@ def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[t
         conv.act == ACT_GELU
 
 
+# the upsampler stage's spx_<t>[1] computed inside the row-form shuffle_conv launch (ESM_SHUFFLE_PRE=0: its own
+# launch, A/B measurements)
+SHUFFLE_PRE_ENABLED = os.environ.get("ESM_SHUFFLE_PRE", "1") != "0"
+
+
+def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: PackedConv) -> bool:
+    """Whether ``pre`` (BasicConv(Cp <= 16, nf, 3, 1, 1), BN + GELU) can run inside the row-form launch."""
+    return SHUFFLE_PRE_ENABLED and shuffle_conv_supported(p, conv) and (p.nf, p.r, conv.cout) == (8, 4, 16) and \
+        pre.nd == 2 and not pre.transposed and (pre.k, pre.stride, pre.pad) == (3, 1, 1) and pre.cin <= 16 and \
+        pre.cout == p.nf and pre.act == ACT_GELU
+
+
 def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: PackedConv,
-                     tag: str = "shuffle_conv", form: int = 0) -> torch.Tensor:
+                     tag: str = "shuffle_conv", form: int = 0, pre: Optional[PackedConv] = None) -> torch.Tensor:
     """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
     3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
     stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)].  ``form`` (nf 8, r 4, C 16): 0
-    automatic, 1 the window form, 2 the row form."""
+    automatic, 1 the window form, 2 the row form.  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
+    ``pre`` (the stage's spx_<t>[1], BasicConv(Cp, nf, 3, 1, 1)), computed inside the launch as well."""
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
+    if pre is not None:
+        if not shuffle_conv_pre_supported(p, conv, pre):
+            raise ValueError("shuffle_conv: unsupported pre-conv")
+        if nf != pre.cin:
+            raise RuntimeError(f"shuffle_conv: pre-conv input has {nf} channels, layer expects {pre.cin}")
+        if x.stride(3) != 1:
+            raise ValueError("shuffle_conv: pre-conv input rows must be contiguous")
+        nf = p.nf
     if nf != p.nf:
         raise RuntimeError(f"shuffle_conv: input has {nf} channels, layer expects {p.nf}")
     if not shuffle_conv_supported(p, conv):  # (size policy is the caller's: blocks.py)
@@ -879,8 +900,21 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     require_on(x.device, "shuffle_conv", x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
     d = EsmShuffleConvDesc()
     t = d.st
-    t.x = x.data_ptr()
-    t.xb, t.xc, t.xh = x.stride(0), x.stride(1), x.stride(2)
+    if pre is None:
+        t.x = x.data_ptr()
+        t.xb, t.xc, t.xh = x.stride(0), x.stride(1), x.stride(2)
+    else:
+        t.x = None
+        t.xb, t.xc, t.xh = nf * H * W, H * W, W  # the virtual head input (never read)
+        d.pre_x = x.data_ptr()
+        d.pb, d.pc, d.ph = x.stride(0), x.stride(1), x.stride(2)
+        d.pre_w = pre.w.data_ptr()
+        d.pre_scale = pre.scale.data_ptr() if pre.scale is not None else None
+        d.pre_shift = pre.shift.data_ptr() if pre.shift is not None else None
+        d.pre_cin, d.pre_cin_pad, d.pre_cout_pad = pre.cin, pre.cin_pad, pre.cout_pad
+        require_on(x.device, "shuffle_conv pre-conv", pre.w, pre.scale, pre.shift)
+        ctx.hold(pre.w, pre.scale, pre.shift)
+        form = 2
     t.up_w, t.up_b, t.tail_w = p.up_w.data_ptr(), p.up_b.data_ptr(), p.tail_w.data_ptr()
     t.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
     t.out = None
@@ -895,9 +929,15 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
     npix = B * H * W * r * r
     flops = 2 * npix * nf * (nf + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9  # head as shuffle_tail + the 1 -> C 3x3
+    cin_read = nf
+    if pre is not None:  # + the 3x3 Cp -> nf pre-conv on the low-resolution map, whose weights are read too
+        flops += 2 * B * H * W * nf * pre.cin * 9
+        cin_read = pre.cin
     ctx.meta.append(dict(name=tag, kind="shuffle_conv", flops=flops,
-                         bytes=4 * (B * nf * H * W + B * conv.cout * Ho2 * Wo2),
-                         shape=f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}",
+                         bytes=4 * (B * cin_read * H * W + B * conv.cout * Ho2 * Wo2) +
+                         (4 * 9 * pre.cin * nf if pre is not None else 0),
+                         shape=(f"pre {pre.cin}->{nf} k3 " if pre is not None else "") +
+                         f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}",
                          reads=_spans(x), writes=_spans(out)))
     ctx.shuffle_conv(d)
     return out

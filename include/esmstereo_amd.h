@@ -233,6 +233,17 @@ typedef struct {
     float* out;
     int64_t ob, oc, oh;
     int32_t C, cin_pad, cout_pad, reserved;
+    /* Optional pre-conv (nf 8, r 4, C 16 row form only): with pre_x set, the head's input x is not read from
+     * st.x (which must be NULL) but computed in the launch as GELU(BN(Conv2d(pre_cin, nf, 3, 1, 1)(pre_x)))
+     * -- the upsampler stage's spx_<t>[1] (models/ESMStereo.py:247-259) -- from pre_x [B, pre_cin, H, W]
+     * (strides pb, pc, ph; pre_cin <= 16), packed weights pre_w [9][pre_cin_pad][pre_cout_pad] and the
+     * folded BN pre_scale / pre_shift (pre_scale NULL = 1). */
+    const float* pre_x;
+    int64_t pb, pc, ph;
+    const float* pre_w;
+    const float* pre_scale;
+    const float* pre_shift;
+    int32_t pre_cin, pre_cin_pad, pre_cout_pad, pre_reserved;
 } esm_shuffle_conv_desc;
 
 const char* esm_last_error(void);

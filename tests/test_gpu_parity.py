@@ -694,6 +694,32 @@ def test_shuffle_conv_fused(nf, r, C, H, W):
         assert rel(y, two) < 1e-5, form
 
 
+@pytest.mark.parametrize("cp,H,W", [(16, 96, 312), (16, 21, 37), (12, 9, 40), (16, 7, 13)])
+def test_shuffle_conv_pre(cp, H, W):
+    """The row-form head + ref conv launch with the stage's spx_<t>[1] (BasicConv(cp, 8, 3, 1, 1)) computed
+    inside it from its input (esm_shuffle_conv_desc.pre_x) vs fp64 torch of the four reference layers and vs
+    the separate launches (relative 1e-5), batch 2, ragged extents."""
+    from esmstereo_amd.engine import pack_shuffle_tail, run_shuffle_conv
+    torch.manual_seed(cp * 100 + H)
+    up = torch.nn.Conv2d(8, 128, 1, 1, 0)
+    tail = torch.nn.Conv2d(8, 1, 3, 1, 1)
+    pconv, pbn = _mk(2, cp, 8, 3, 1, 1, seed=H + 1)
+    conv, bn = _mk(2, 1, 16, 3, 2, 1, seed=H)
+    c = torch.randn(2, cp, H, W)
+    x = _ref_conv([c], pconv, pbn, ACT_GELU)
+    t = F.conv2d(F.silu(F.pixel_shuffle(F.conv2d(x.double(), up.weight.double(), up.bias.double()), 4)),
+                 tail.weight.double(), tail.bias.double(), 1, 1)
+    ref = _ref_conv([t], conv, bn, ACT_GELU)
+    p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), 4)
+    pc, pp = pk(conv, bn, ACT_GELU), pk(pconv, pbn, ACT_GELU)
+    ctx = Ctx(DEV)
+    y = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-5
+    two = run_shuffle_conv(ctx, run_conv(ctx, pp, [c.to(DEV)]), p, pc, form=2)
+    assert rel(y, two) < 1e-5
+
+
 PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones
     ((1,), 5, 1, 1, 3, 1, 16, 24, 78),           # dm<t>.0 -> dm<t>.1
     ((16,), 3, 1, 1, 1, 1, 16, 22, 76),          # dm<t>.2 -> dm<t>.3 (k1 p1: the GELU(shift) ring)

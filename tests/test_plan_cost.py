@@ -124,8 +124,14 @@ def test_plan_per_op_cost(case):
             else:
                 g2 = re.search(r"C(\d+) (\d+)x(\d+)$", shape)
                 c, ho, wo = (int(v) for v in g2.groups())
-                assert op["flops"] == head + 2 * B * ho * wo * c * 9, name
-                assert op["bytes"] == 4 * (B * nf * hi * wi + B * c * ho * wo), name
+                gp = re.match(r"pre (\d+)->(\d+) k3 ", shape)  # the stage's spx_<t>[1] inside the launch
+                cp = int(gp.group(1)) if gp else 0
+                if gp:
+                    spx1 = _layer(m, name.split("+")[0])
+                    assert tuple(spx1.weight.shape) == (nf, cp, 3, 3), name
+                pre_f = 2 * B * hi * wi * nf * cp * 9
+                assert op["flops"] == head + 2 * B * ho * wo * c * 9 + pre_f, name
+                assert op["bytes"] == 4 * (B * (cp or nf) * hi * wi + B * c * ho * wo) + 4 * 9 * cp * nf, name
         elif kind == "fmnet":
             g = re.search(r"C(\d+) (\d+)x(\d+) dw(\d+)", shape)
             C, hh, ww, k = (int(v) for v in g.groups())
@@ -148,11 +154,12 @@ def test_shuffle_head_flops_s_k():
     """upsampling4 + tail4x at S-K is 2 * 384 * 1248 * 8 * (8 + 9) = 130.35 MFLOP; fused with
     ref4x.conv1[0] (the row-form shuffle_conv, round 4) plus the 1 -> 16 3x3 stride-2 conv on 192 x 624."""
     _, _, meta, _ = _plan("S-K")
-    op = next(x for x in meta if x["name"].startswith("upsample_module.upsampling4+tail4x"))
+    op = next(x for x in meta if "upsampling4+tail4x" in x["name"])
     head = 2 * 384 * 1248 * 8 * 17
     assert head == 130_351_104
+    pre = 2 * 96 * 312 * 8 * 16 * 9 if op["name"].startswith("upsample_module.spx_4x.1+") else 0  # spx_4x[1] inside
     if op["name"].endswith("+ref4x.conv1.0"):
         assert op["kind"] == "shuffle_conv"
-        assert op["flops"] == head + 2 * 192 * 624 * 16 * 9
+        assert op["flops"] == head + 2 * 192 * 624 * 16 * 9 + pre
     else:
         assert op["flops"] == head
