@@ -680,6 +680,7 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     }
     if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
     if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);
+    if (rsel == 3 && (a.hint & (1 << 28))) return launch_t3_mt<1, 3, 8, 4>(a, s);  // bit 28: 8 rows per wave
     return launch_t3_mt<1, 3, 4, 4>(a, s);
 }
 

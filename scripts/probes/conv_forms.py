@@ -13,6 +13,7 @@ T3 = 1 << 23
 NOTILE = 1 << 19  # conv.hip kHintNoTile: the automatic rules without the tiled forms
 CASES = [  # name, nd, cins, cout, k, s, p, spatial, B
     ("L group_stem B4", 3, (32,), 8, 3, 1, 1, (48, 96, 312), 4),
+    ("L conv1.1 B4", 3, (24,), 24, 3, 1, 1, (24, 48, 156), 4),
     ("L agg B4", 3, (8,), 8, 3, 1, 1, (48, 96, 312), 4),
     ("S ref4x.conv1.1", 2, (16,), 16, 3, 1, 1, (192, 624), 1),
     ("S ref4x.agg_1.0", 2, (16, 16, 24), 16, 1, 1, 0, (192, 624), 1),
@@ -61,6 +62,8 @@ for name, nd, cins, cout, k, s, p, sp, B in CASES:
     res = {}
     forms = [("auto", 0), ("no tile", NOTILE), ("tile r1", T3 | 1 << 26), ("tile r2", T3 | 2 << 26),
              ("tile r4", T3 | 3 << 26)]
+    if nd == 3 and k == 3 and s == 1 and cout > 8:
+        forms.append(("tile r8", T3 | 3 << 26 | 1 << 28))
     if len(sys.argv) > 1 and not any(f in name for f in sys.argv[1:]):
         continue
     for label, hint in forms:
