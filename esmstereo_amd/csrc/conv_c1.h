@@ -102,6 +102,47 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
     const int qz = D3 ? (oz & 1) : 0;
     const int iz0 = D3 ? (oz >> 1) + qz - 1 : 0;  // input plane of plane tap t = 1 (t = 0: iz0 + 1)
     const int iy0 = Y0 / 2 - 1, ix0 = X0 / 2 - 1;  // input row / column of tile index 0
+    // the thread's outputs (row oy, columns ox0 ..): their epilogue operands -- BN scale / shift and the
+    // 4 bilinear taps of `up` per column (the refinement's conv1_up adds the upsampled previous
+    // disparity) -- are loaded with the staging batch below, not after the FMAs (one round trip less)
+    const int oy = Y0 + 2 * (((tid >> 6) >> 1) * 4 + (tid & 63) / 16) + ((tid >> 6) & 1);
+    const int ox0 = X0 + QW * ((tid & 63) % 16);
+    const float ep_s = a.scale ? a.scale[0] : 1.f, ep_h = a.shift ? a.shift[0] : 0.f;
+    constexpr int NU = D3 ? 1 : QW;
+    float upv[NU][4], ulx[NU], uly = 0.f;
+    if (!D3 && a.up) {
+        const float* img = a.up + b * a.ub;
+        const float sc = 1.0f / static_cast<float>(a.up_f);
+        const int y = oy < Ho ? oy : Ho - 1;
+        float sy = sc * (static_cast<float>(y) + 0.5f) - 0.5f;
+        sy = sy < 0.f ? 0.f : sy;
+        const int y0 = static_cast<int>(sy), y1 = y0 + (y0 < a.up_h - 1 ? 1 : 0);
+        uly = sy - static_cast<float>(y0);
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const int x = ox0 + j < Wo ? ox0 + j : Wo - 1;
+            float sx = sc * (static_cast<float>(x) + 0.5f) - 0.5f;
+            sx = sx < 0.f ? 0.f : sx;
+            const int x0 = static_cast<int>(sx), x1 = x0 + (x0 < a.up_w - 1 ? 1 : 0);
+            ulx[j] = sx - static_cast<float>(x0);
+            upv[j][0] = img[y0 * a.uh + x0];
+            upv[j][1] = img[y0 * a.uh + x1];
+            upv[j][2] = img[y1 * a.uh + x0];
+            upv[j][3] = img[y1 * a.uh + x1];
+        }
+    }
+    // conv_finish with the prefetched operands (bilinear_at's arithmetic, common.h)
+    auto finish = [&](float v, int j) __attribute__((always_inline)) {
+        v = a.scale ? v * ep_s + ep_h : v + ep_h;
+        v = apply_act(v, a.act);
+        if (a.mul) v = v * a.mul[b * a.mb + oy * a.mh + ox0 + j];
+        if (a.res) v = v + a.res[b * a.rb + oz * a.rd + oy * a.rh + ox0 + j];
+        if (!D3 && a.up) {
+            const float ly1 = uly, ly0 = 1.0f - ly1, lx1 = ulx[j], lx0 = 1.0f - lx1;
+            v = ly0 * (lx0 * upv[j][0] + lx1 * upv[j][1]) + ly1 * (lx0 * upv[j][2] + lx1 * upv[j][3]) + v;
+        }
+        return v;
+    };
     // ---- stage: every load of the thread in flight together, then the LDS stores
     const C1Stage<XR, XN, NP, CP, IR, IC, ICP> stg(a, tid, iz0, iy0, ix0);
     float rx[XR], rw[WR];
@@ -137,7 +178,6 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
     const int qy = wave & 1;
     const int g = lane % 16;
     const int r = 2 * ((wave >> 1) * 4 + lane / 16) + qy;
-    const int oy = Y0 + r;
     const int lr = r / 2 + 1 + qy;  // tile row of input m + q (row tap t = 0); t = 1 is lr - 1
     const int lc = QW / 2 * g;      // first tile column the thread reads (QW = 1: see below)
     constexpr int NV = QW / 2 + 2;  // tile columns per row the thread reads
@@ -167,23 +207,22 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
         }
     }
     if (oy >= Ho) return;
-    const int ox0 = X0 + QW * g;
     const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;
     if constexpr (QW == 4) {
         const bool plain = !a.mul && !a.res && !a.out2;
         if (plain && ox0 + 3 < Wo && ((o | a.oh) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0) {
             floatx4 v4;
-            v4.x = conv_finish(a, acc[0], b, 0, oz, oy, ox0 + 0) * a.post_scale;
-            v4.y = conv_finish(a, acc[1], b, 0, oz, oy, ox0 + 1) * a.post_scale;
-            v4.z = conv_finish(a, acc[2], b, 0, oz, oy, ox0 + 2) * a.post_scale;
-            v4.w = conv_finish(a, acc[3], b, 0, oz, oy, ox0 + 3) * a.post_scale;
+            v4.x = finish(acc[0], 0) * a.post_scale;
+            v4.y = finish(acc[1], 1) * a.post_scale;
+            v4.z = finish(acc[2], 2) * a.post_scale;
+            v4.w = finish(acc[3], 3) * a.post_scale;
             *reinterpret_cast<floatx4*>(a.out + o) = v4;
             return;
         }
     }
 #pragma unroll
     for (int j = 0; j < QW; ++j)
-        if (ox0 + j < Wo) conv_put(a, conv_finish(a, acc[j], b, 0, oz, oy, ox0 + j), b, 0, oz, oy, ox0 + j);
+        if (ox0 + j < Wo) conv_put(a, finish(acc[j], j), b, 0, oz, oy, ox0 + j);
 }
 
 // 3-D: channel chunks of CC, the next chunk's loads in flight during the current one's FMAs.

@@ -680,7 +680,9 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     }
     if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
     if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);
-    if (rsel == 3 && (a.hint & (1 << 28))) return launch_t3_mt<1, 3, 8, 4>(a, s);  // bit 28: 8 rows per wave
+    // 8 rows per wave on the largest volumes (L-K B = 4 aggregation_out.conv1.1, 24 -> 24 on 24x48x156: 277 vs 301
+    // us for 4 rows, r04 probe); hint bit 28 with rows 4 asks for it explicitly
+    if ((rsel == 3 && (a.hint & (1 << 28))) || rsel == 0) return launch_t3_mt<1, 3, 8, 4>(a, s);
     return launch_t3_mt<1, 3, 4, 4>(a, s);
 }
 
