@@ -228,145 +228,6 @@ int launch_p2_k(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     return small ? launch_p2<KA, SA, KB, 2, 48>(a, b, s) : launch_p2<KA, SA, KB, 4, 48>(a, b, s);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The refinement hourglass's agg_N pair on large maps (models/ESMStereo.py:226-236: agg_N[0] = BasicConv
-// 1x1 over cat(up, conv, feature), 56 channels at S -> 16, then agg_N[1] = BasicConv 3x3 16 -> 16): the
-// 1x1's output never reaches memory.  A workgroup of 8 waves owns RB output rows x 64 columns:
-//   phase 1: the 1x1 + BN + GELU on the (RB + 2) x 66 window the 3x3 needs (zero outside the map: the
-//            3x3's padding), as MFMA units of 16 mid channels x 16 window columns x K = Cin (A = the 1x1
-//            weights in VGPRs, B = one buffer load per k-step and lane, straight from the sources), into
-//            LDS [16][RB + 2][68] (channel stride = 16 mod 32 banks);
-//   phase 2: wave w takes columns 16 (w & 3) .. + 15 and half of the rows; the 3x3's weights live in VGPRs
-//            (36 per lane), each LDS window row is read once per (group, dx) and feeds the up to 3 output
-//            rows it reaches (the wide form's row streaming, with LDS in place of global loads);
-//   epilogue: BN + GELU, write-through stores.
-// The 1x1 is recomputed on the 2-row / 2-column halo (1.29x at RB = 8) instead of a 7.7 MB write + read and
-// a launch.  Per output the sums run in the same (k-step, tap) order as the two single launches.
-constexpr int kKpRB = 8, kKpUW = 68;
-constexpr int kKpCS = ((kKpRB + 2) * kKpUW + 15) / 32 * 32 + 16;  // = 16 mod 32
-
-template <int NK1>
-__global__ void __launch_bounds__(512) kpair_kernel(const esm_conv_desc a, const esm_conv_desc bd) {
-    constexpr int RB = kKpRB, UW = kKpUW, CS = kKpCS, NU = (RB + 2) * 5;
-    __shared__ __attribute__((aligned(16))) float u[16 * CS];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, n = lane & 15;
-    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
-    const int b = bk_.z, Y0 = bk_.y * RB, X0 = bk_.x * 64;
-    const int H = a.Ho, W = a.Wo;  // the 1x1 keeps the extent; the 3x3 (s1 p1) too
-
-    // sources (4-channel aligned): a k-step's source is wave-uniform
-    const int ns = a.nsrc;
-    const int lo1 = a.src[0].C, lo2 = a.src[0].C + (ns > 1 ? a.src[1].C : 0);
-    auto src_rsrc = [&](const esm_src& q) __attribute__((always_inline)) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.ptr + b * q.sb), static_cast<short>(0),
-                                                 4 * ((q.C - 1) * static_cast<int>(q.sc) + (a.Hi - 1) * static_cast<int>(q.sh) + a.Wi),
-                                                 0x00020000);
-    };
-    const __amdgpu_buffer_rsrc_t rs0 = src_rsrc(a.src[0]);
-    const __amdgpu_buffer_rsrc_t rs1 = ns > 1 ? src_rsrc(a.src[1]) : rs0;
-    const __amdgpu_buffer_rsrc_t rs2 = ns > 2 ? src_rsrc(a.src[2]) : rs0;
-    const int sc0 = static_cast<int>(a.src[0].sc), sh0 = static_cast<int>(a.src[0].sh);
-    const int sc1 = ns > 1 ? static_cast<int>(a.src[1].sc) : sc0, sh1 = ns > 1 ? static_cast<int>(a.src[1].sh) : sh0;
-    const int sc2 = ns > 2 ? static_cast<int>(a.src[2].sc) : sc0, sh2 = ns > 2 ? static_cast<int>(a.src[2].sh) : sh0;
-
-    // weights: the 1x1 as A operands (lane (g, n): W1[co n][ci 4 ks + g]), the 3x3 likewise per (tap, group)
-    float w1[NK1], w3[9][4];
-#pragma unroll
-    for (int ks = 0; ks < NK1; ++ks) {
-        const int ci = 4 * ks + g;
-        const bool ok = ci < a.Cin;
-        const float v = a.w[ok ? ci * a.cout_pad + n : 0];
-        w1[ks] = ok ? v : 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int G = 0; G < 4; ++G) w3[t][G] = bd.w[(t * bd.cin_pad + 4 * G + g) * bd.cout_pad + n];
-    float s1[4], h1[4], s2[4], h2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = 4 * g + j;
-        s1[j] = a.scale ? a.scale[c] : 1.f;
-        h1[j] = a.shift ? a.shift[c] : 0.f;
-        s2[j] = bd.scale ? bd.scale[c] : 1.f;
-        h2[j] = bd.shift ? bd.shift[c] : 0.f;
-    }
-
-    // ---- phase 1: unit = (window row ur, 16-column tile nt); window (ur, wc) = map (Y0 - 1 + ur, X0 - 1 + wc)
-    for (int un = wave; un < NU; un += 8) {
-        const int ur = un / 5, nt = un - (un / 5) * 5;
-        const int wc = 16 * nt + n;
-        const int yy = Y0 - 1 + ur, xx = X0 - 1 + wc;
-        const bool in = wc < 66 && yy >= 0 && yy < H && xx >= 0 && xx < W;
-        float v[NK1];
-#pragma unroll
-        for (int ks = 0; ks < NK1; ++ks) {
-            const int c0 = 4 * ks;
-            const int sq = c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2);
-            const int cl = c0 + g - (sq == 0 ? 0 : (sq == 1 ? lo1 : lo2));
-            const int sc = sq == 0 ? sc0 : (sq == 1 ? sc1 : sc2), sh = sq == 0 ? sh0 : (sq == 1 ? sh1 : sh2);
-            const unsigned off = (in && c0 < a.Cin) ? 4u * static_cast<unsigned>(cl * sc + yy * sh + xx) : kOOB;
-            v[ks] = buf_load_s(sq == 0 ? rs0 : (sq == 1 ? rs1 : rs2), off, 0);
-        }
-        floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int ks = 0; ks < NK1; ++ks) acc[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[ks], v[ks], acc[ks & 1], 0, 0, 0);
-        if (wc < 66) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float r = act_t<ESM_ACT_GELU>((acc[0][j] + acc[1][j]) * s1[j] + h1[j], 0);
-                u[(4 * g + j) * CS + ur * UW + wc] = in ? r : 0.f;
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- phase 2: wave w -> columns 16 s .. (s = w & 3), output rows r0 .. r0 + RB / 2 - 1 (r0 = (w >> 2) RB / 2)
-    constexpr int RH = RB / 2;
-    const int st = wave & 3, r0 = (wave >> 2) * RH;
-    floatx4 acc[RH];
-#pragma unroll
-    for (int r = 0; r < RH; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* ub = u + g * CS + 16 * st + n;
-#pragma unroll
-    for (int ir = 0; ir < RH + 2; ++ir) {  // window row r0 + ir feeds output rows r0 + ir - dy
-        float bv[4][3];
-#pragma unroll
-        for (int G = 0; G < 4; ++G)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) bv[G][dx] = ub[4 * G * CS + (r0 + ir) * UW + dx];
-#pragma unroll
-        for (int G = 0; G < 4; ++G)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int dy = 0; dy < 3; ++dy) {
-                    const int r = ir - dy;
-                    if (r < 0 || r >= RH) continue;
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[dy * 3 + dx][G], bv[G][dx], acc[r], 0, 0, 0);
-                }
-    }
-    const int x = X0 + 16 * st + n;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        bd.out + b * bd.ob, static_cast<short>(0),
-        4 * ((bd.Cout - 1) * static_cast<int>(bd.oc) + (bd.Ho - 1) * static_cast<int>(bd.oh) + bd.Wo), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < RH; ++r) {
-        const int y = Y0 + r0 + r;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = 4 * g + j;
-            const float v = act_t<ESM_ACT_GELU>(acc[r][j] * s2[j] + h2[j], 0);
-            const unsigned o = (y < bd.Ho && x < bd.Wo && co < bd.Cout)
-                                   ? 4u * static_cast<unsigned>(co * static_cast<int>(bd.oc) + y * static_cast<int>(bd.oh) + x)
-                                   : kOOB;
-            store_b32(__float_as_uint(v), ro, static_cast<int>(o), 0);
-        }
-    }
-}
-
 }  // namespace
 
 // convA: 2-D, not transposed, k 1/3/5 (stride 1) or 3 (stride 2), <= 48 input channels (64 for k 1; 1..3 sources),
@@ -391,25 +252,8 @@ bool pair2_ok(const esm_conv_desc& a, const esm_conv_desc& b) {
     return 4 * last < static_cast<long long>(kOOB) && b.oc < (1 << 28) && b.oh < (1 << 28);
 }
 
-// the k1 -> k3 form (kpair_kernel): 2-D 1x1 s1 p0 over <= 64 channels (1..3 sources, 4-channel splits) -> 16,
-// then 3x3 s1 p1 16 -> 16, both BN + GELU with plain epilogues; taken when the first conv's hint has bit 23
-// (the host asks for it on maps of >= engine.KPAIR_MIN_PIX output pixels)
-bool kpair_ok(const esm_conv_desc& a, const esm_conv_desc& b) {
-    if (!pair2_ok(a, b)) return false;
-    return a.kh == 1 && a.ph == 0 && a.Cout == 16 && a.Cin <= 64 && b.kh == 3 && b.ph == 1 && b.Cout == 16 &&
-           b.Cin == 16 && a.cout_pad >= 16 && b.cout_pad >= 16 && b.cin_pad >= 16;
-}
-
-int launch_kpair(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
-    const dim3 grid(ceil_div(b.Wo, 64), ceil_div(b.Ho, kKpRB), a.B);
-    if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv pair: grid too large");
-    hipLaunchKernelGGL((kpair_kernel<16>), grid, dim3(512), 0, s, a, b);  // pair2_ok: <= 64 input channels
-    return check_launch("conv pair (k1 -> k3)");
-}
-
 int launch_pair2(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     if (!pair2_ok(a, b)) return arg_error("conv pair: unsupported pair");
-    if (kpair_ok(a, b) && (a.hint & (1 << 23))) return launch_kpair(a, b, s);
     if (a.kh == 5) return b.kh == 3 ? launch_p2_k<5, 1, 3>(a, b, s) : launch_p2_k<5, 1, 1>(a, b, s);
     if (a.kh == 1) return b.kh == 3 ? launch_p2_k<1, 1, 3>(a, b, s) : launch_p2_k<1, 1, 1>(a, b, s);
     if (a.stride == 2) return b.kh == 3 ? launch_p2_k<3, 2, 3>(a, b, s) : launch_p2_k<3, 2, 1>(a, b, s);

@@ -628,9 +628,6 @@ def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]
     return len(srcs) == 1 or all(int(t.shape[1]) % 4 == 0 for t in srcs)
 
 
-# ESM_KPAIR=0: the agg_N 1x1 -> 3x3 pairs on large maps as two launches (A/B measurements)
-KPAIR_ENABLED = os.environ.get("ESM_KPAIR", "1") != "0"
-KPAIR_MIN_PIX = int(os.environ.get("ESM_KPAIR_MIN_PIX", "16384"))
 # every supported pair on maps of at most this many output pixels (A/B knob; 0 = the rules below only)
 PAIR2_SMALL_MAXPIX = int(os.environ.get("ESM_PAIR2_SMALL_MAXPIX", "0"))
 
@@ -651,22 +648,17 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     light = pa.cin * pa.k * pa.k
     if B * Ho * Wo <= PAIR2_SMALL_MAXPIX:
         return True
-    # the refinement's agg_N 1x1 -> 3x3 pair on large maps: the k1 -> k3 row form (conv_pair2.hip kpair_kernel)
-    kpair = KPAIR_ENABLED and pa.k == 1 and pb.k == 3 and pa.cout == 16 and pb.cout == 16 and B * Ho * Wo >= KPAIR_MIN_PIX
-    return kpair or pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
+    return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 
 def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
-              tags: Tuple[str, str] = ("convA", "convB"), force: bool = False, kpair: bool = False) -> torch.Tensor:
+              tags: Tuple[str, str] = ("convA", "convB"), force: bool = False) -> torch.Tensor:
     """``pb(pa(cat(srcs)))`` (two BasicConvs, BN + GELU each) as one launch where ``pair2_auto`` takes it
-    (``force``: wherever supported), else two launches.  ``kpair``: ask for the 1x1 -> 3x3 row form on any
-    map size (conv_pair2.hip kpair_kernel; tests)."""
+    (``force``: wherever supported), else two launches."""
     if not (pair2_supported(pa, pb, srcs) if force else pair2_auto(pa, pb, srcs)):
         return run_conv(ctx, pb, [run_conv(ctx, pa, srcs, tag=tags[0])], tag=tags[1])
     da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
     B = int(srcs[0].shape[0])
-    if kpair or (KPAIR_ENABLED and pa.k == 1 and pb.k == 3 and B * int(da.Ho) * int(da.Wo) >= KPAIR_MIN_PIX):
-        da.hint |= 1 << 23  # the k1 -> k3 row form where conv_pair2.hip can take it
     virt = srcs[0].as_strided((B, pa.cout, int(da.Ho), int(da.Wo)), (0, 0, 0, 1))  # geometry only, never read
     db, out, mb = _conv_desc(ctx, pb, [virt], tag=tags[1])
     mid = 4 * B * pa.cout * int(da.Ho) * int(da.Wo)

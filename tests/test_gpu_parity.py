@@ -753,27 +753,6 @@ def test_conv_pair2(cins, ka, sa, pa, kb, pb, coutb, H, W):
     assert rel(y, two) < 1e-5
 
 
-@pytest.mark.parametrize("cins,H,W,B", [((16, 16, 24), 192, 624, 1), ((16, 16, 24), 37, 101, 2), ((16, 16, 24), 9, 70, 1),
-                                        ((32, 16), 20, 130, 1), ((12,), 17, 64, 2)])
-def test_conv_kpair(cins, H, W, B):
-    """The agg_N 1x1 -> 3x3 pair as one row-form launch (conv_pair2.hip kpair_kernel: the 1x1 recomputed on the
-    3x3's halo, intermediate in LDS) vs fp64 torch and vs the two single launches (relative 1e-5); ragged
-    extents, batch 2, 1..3 sources; 192x624 takes the form automatically."""
-    from esmstereo_amd.engine import run_pair2
-    ca, ba = _mk(2, sum(cins), 16, 1, 1, 0, seed=41 + H)
-    cb, bb = _mk(2, 16, 16, 3, 1, 1, seed=42 + W)
-    xs = [torch.randn(B, c, H, W) for c in cins]
-    ref = _ref_conv([_ref_conv(xs, ca, ba, ACT_GELU)], cb, bb, ACT_GELU)
-    pa_, pb_ = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
-    xd = [x.to(DEV) for x in xs]
-    ctx = Ctx(DEV)
-    y = run_pair2(ctx, pa_, xd, pb_, force=True, kpair=True)
-    assert y.shape == ref.shape
-    assert rel(y, ref) < 1e-5
-    two = run_conv(ctx, pb_, [run_conv(ctx, pa_, xd)])
-    assert rel(y, two) < 1e-5
-
-
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)
