@@ -62,7 +62,7 @@ for name, nd, cins, cout, k, s, p, sp, B in CASES:
     res = {}
     forms = [("auto", 0), ("no tile", NOTILE), ("tile r1", T3 | 1 << 26), ("tile r2", T3 | 2 << 26),
              ("tile r4", T3 | 3 << 26)]
-    if nd == 3 and k == 3 and s == 1 and cout > 8:
+    if nd == 3 and k == 3 and s == 1:
         forms.append(("tile r8", T3 | 3 << 26 | 1 << 28))
     if len(sys.argv) > 1 and not any(f in name for f in sys.argv[1:]):
         continue
