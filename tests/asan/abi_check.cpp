@@ -223,6 +223,31 @@ esm_shuffle_conv_desc sconv_base() {
     return d;
 }
 
+// the S 4x stage: spx_4x[1] computed inside the row-form launch (pre_x; st.x NULL)
+esm_shuffle_conv_desc sconv_pre_base() {
+    esm_shuffle_conv_desc d = sconv_base();
+    d.st.x = nullptr;
+    d.st.r = 4;
+    d.st.H = 96;
+    d.st.W = 312;
+    d.st.xb = 8 * 96 * 312;
+    d.st.xc = 96 * 312;
+    d.st.xh = 312;
+    d.st.ob = 384 * 1248;
+    d.st.oh = 1248;
+    d.ob = 16 * 192 * 624;
+    d.oc = 192 * 624;
+    d.oh = 624;
+    d.pre_x = d.pre_w = d.pre_scale = d.pre_shift = P;
+    d.pb = 16 * 96 * 312;
+    d.pc = 96 * 312;
+    d.ph = 312;
+    d.pre_cin = 16;
+    d.pre_cin_pad = 16;
+    d.pre_cout_pad = 32;
+    return d;
+}
+
 void fuzz_conv(int iters) {
     const auto ptrs = conv_ptrs();
     for (const esm_conv_desc& base : {conv3d_base(), conv2d_base()}) {
@@ -324,6 +349,22 @@ void plans(int iters) {
             check(esm_plan_set_repeat(p, idx, pick_int()) >= 0 ? 0 : ESM_ERR_ARG, "set_repeat");
         }
         check(esm_plan_run_op(p, static_cast<int>(rng() % (nops + 2)) - 1, pick_int(), nullptr), "run_op");
+        {  // zero-copy rebinding: random ranges around the dummy pointer, moved to other dummies and back
+            const int nb = static_cast<int>(rng() % 4);
+            const void* olds[3];
+            const void* news[3];
+            uint64_t bytes[3];
+            for (int k = 0; k < 3; ++k) {
+                olds[k] = g_dummy + (rng() % 8);
+                news[k] = g_dummy + (rng() % 8);
+                bytes[k] = (rng() % 3 == 0) ? 0 : 4 * (1 + rng() % 64);
+            }
+            const int rc = esm_plan_rebind(p, nb, nb ? olds : nullptr, nb ? bytes : nullptr, nb ? news : nullptr);
+            check(rc >= 0 ? 0 : rc, "rebind");
+            check(esm_plan_rebind(p, nb, nb ? news : nullptr, nb ? bytes : nullptr, nb ? olds : nullptr) >= 0 ? 0 : ESM_ERR_ARG,
+                  "rebind back");
+        }
+        expect_err(esm_plan_rebind(p, 1, nullptr, nullptr, nullptr), "rebind null arrays");
         if (it % 16 == 0) {
             // no device here: these reach the runtime and must fail cleanly (stream / graph / events)
             check(esm_plan_run(p, nullptr), "plan run");
@@ -361,7 +402,8 @@ int main(int argc, char** argv) {
                                          offsetof(esm_fmnet_desc, dw_w), offsetof(esm_fmnet_desc, dw_w) + 8,
                                          offsetof(esm_fmnet_desc, dw_b), offsetof(esm_fmnet_desc, dw_b) + 8,
                                          offsetof(esm_fmnet_desc, conv0_w), offsetof(esm_fmnet_desc, conv0_b),
-                                         offsetof(esm_fmnet_desc, conv2_w), offsetof(esm_fmnet_desc, conv2_b)};
+                                         offsetof(esm_fmnet_desc, conv2_w), offsetof(esm_fmnet_desc, conv2_b),
+                                         offsetof(esm_fmnet_desc, work)};
     std::vector<size_t> fm_all = fm_ptrs;
     for (int s = 0; s < 4; ++s)
         for (int j = 0; j < 5; ++j) fm_all.push_back(offsetof(esm_fmnet_desc, stage) + s * sizeof(esm_smix_stage) + 8 * j);
@@ -380,6 +422,10 @@ int main(int argc, char** argv) {
                      offsetof(esm_shuffle_conv_desc, shift), offsetof(esm_shuffle_conv_desc, out)})
         sc_ptrs.push_back(o);
     fuzz_desc<esm_shuffle_conv_desc>(sconv_base(), esm_shuffle_conv_f32, sc_ptrs, "shuffle_conv", iters);
+    for (size_t o : {offsetof(esm_shuffle_conv_desc, pre_x), offsetof(esm_shuffle_conv_desc, pre_w),
+                     offsetof(esm_shuffle_conv_desc, pre_scale), offsetof(esm_shuffle_conv_desc, pre_shift)})
+        sc_ptrs.push_back(o);
+    fuzz_desc<esm_shuffle_conv_desc>(sconv_pre_base(), esm_shuffle_conv_f32, sc_ptrs, "shuffle_conv pre", iters);
     fuzz_flat(iters);
     plans(iters / 20 + 1);
     std::printf("abi_check: %d calls checked, %d failures\n", g_checked, g_fail);
