@@ -28,6 +28,7 @@ namespace esm {
 namespace conv {
 
 constexpr int kC1Threads = 256;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kC1TH = 16;  // output rows per tile
 
 // Per-thread staging plan of an input tile [NP planes][CC channels][IR rows][IC columns] (element i of
@@ -181,9 +182,9 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
     const int lr = r / 2 + 1 + qy;  // tile row of input m + q (row tap t = 0); t = 1 is lr - 1
     const int lc = QW / 2 * g;      // first tile column the thread reads (QW = 1: see below)
     constexpr int NV = QW / 2 + 2;  // tile columns per row the thread reads
-    float acc[QW];
+    f32x2 acc2[QW / 2];
 #pragma unroll
-    for (int j = 0; j < QW; ++j) acc[j] = 0.f;
+    for (int j = 0; j < QW / 2; ++j) acc2[j] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int tz = 0; tz < NP; ++tz) {
         const int p = D3 ? 1 - tz : 0;  // plane tap t = tz sits at tile plane 1 - t
@@ -194,18 +195,24 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_batch_kernel(const esm_co
             for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
                 for (int j = 0; j < NV; ++j) v[ty][j] = xs[p][c][lr - ty][lc + j];
+            // output columns j = 2 jp (qx = 0) and 2 jp + 1 (qx = 1) as one packed pair (v_pk_fma_f32): per
+            // element the same product and sum order as one column at a time.  Input m + qx - tx of output
+            // column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
 #pragma unroll
-            for (int j = 0; j < QW; ++j) {
-                const int qx = j & 1;
-                // input m + qx - tx of output column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
+            for (int jp = 0; jp < QW / 2; ++jp)
 #pragma unroll
                 for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
-                    for (int tx = 0; tx < 2; ++tx)
-                        acc[j] += ws[qz][qy][c][qx][tz][ty * 2 + tx] * v[ty][1 + (j >> 1) + qx - tx];
-            }
+                    for (int tx = 0; tx < 2; ++tx) {
+                        const f32x2 w2 = {ws[qz][qy][c][0][tz][ty * 2 + tx], ws[qz][qy][c][1][tz][ty * 2 + tx]};
+                        const f32x2 v2 = {v[ty][1 + jp - tx], v[ty][2 + jp - tx]};
+                        acc2[jp] = __builtin_elementwise_fma(w2, v2, acc2[jp]);
+                    }
         }
     }
+    float acc[QW];
+#pragma unroll
+    for (int j = 0; j < QW; ++j) acc[j] = acc2[j >> 1][j & 1];
     if (oy >= Ho) return;
     const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;
     if constexpr (QW == 4) {
@@ -294,9 +301,9 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
     const int lr = r / 2 + 1 + qy;  // tile row of input m + q (row tap t = 0); t = 1 is lr - 1
     const int lc = QW / 2 * g;      // first tile column the thread reads (QW = 1: see below)
     constexpr int NV = QW / 2 + 2;  // tile columns per row the thread reads
-    float acc[QW];
+    f32x2 acc2[QW / 2];
 #pragma unroll
-    for (int j = 0; j < QW; ++j) acc[j] = 0.f;
+    for (int j = 0; j < QW / 2; ++j) acc2[j] = f32x2{0.f, 0.f};
     for (int ch = 0; ch < nch; ++ch) {
         if (ch) __syncthreads();  // the previous chunk's reads of xs are done
         stg.store(&xs[0][0][0][0], rx);
@@ -313,19 +320,23 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
                 for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
                     for (int j = 0; j < NV; ++j) v[ty][j] = xs[p][c][lr - ty][lc + j];
+                // the packed column pairs of convt_c1_batch_kernel
 #pragma unroll
-                for (int j = 0; j < QW; ++j) {
-                    const int qx = j & 1;
-                    // input m + qx - tx of output column QW*g + j sits at tile column lc + 1 + (j >> 1) + qx - tx
+                for (int jp = 0; jp < QW / 2; ++jp)
 #pragma unroll
                     for (int ty = 0; ty < 2; ++ty)
 #pragma unroll
-                        for (int tx = 0; tx < 2; ++tx)
-                            acc[j] += ws[qz][qy][cw][qx][tz][ty * 2 + tx] * v[ty][1 + (j >> 1) + qx - tx];
-                }
+                        for (int tx = 0; tx < 2; ++tx) {
+                            const f32x2 w2 = {ws[qz][qy][cw][0][tz][ty * 2 + tx], ws[qz][qy][cw][1][tz][ty * 2 + tx]};
+                            const f32x2 v2 = {v[ty][1 + jp - tx], v[ty][2 + jp - tx]};
+                            acc2[jp] = __builtin_elementwise_fma(w2, v2, acc2[jp]);
+                        }
             }
         }
     }
+    float acc[QW];
+#pragma unroll
+    for (int j = 0; j < QW; ++j) acc[j] = acc2[j >> 1][j & 1];
     if (oy >= Ho) return;
     const int ox0 = X0 + QW * g;
     const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;

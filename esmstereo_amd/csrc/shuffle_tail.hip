@@ -13,6 +13,8 @@
 // bias + sum over (channel, ky, kx) of w*v.
 #include "conv_direct.h"
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 namespace esm {
 namespace {
 
@@ -365,8 +367,14 @@ __global__ void __launch_bounds__(64 * L) shuffle_tail4_kernel(const esm_shuffle
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
                 const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                // output pairs (0, 1), (2, 3) as packed FMAs (v_pk_fma_f32), per output the same order
+                const f2v w2 = {w, w};
+                const f2v lo = __builtin_elementwise_fma(w2, f2v{v[kx], v[1 + kx]}, f2v{acc[0], acc[1]});
+                const f2v hi = __builtin_elementwise_fma(w2, f2v{v[2 + kx], v[3 + kx]}, f2v{acc[2], acc[3]});
+                acc[0] = lo[0];
+                acc[1] = lo[1];
+                acc[2] = hi[0];
+                acc[3] = hi[1];
             }
         }
     }
@@ -841,8 +849,13 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
                     const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j] += w * v[j + kx];
+                    const f2v w2 = {w, w};  // packed output pairs, as shuffle_tail4_kernel
+                    const f2v lo = __builtin_elementwise_fma(w2, f2v{v[kx], v[1 + kx]}, f2v{acc[0], acc[1]});
+                    const f2v hi = __builtin_elementwise_fma(w2, f2v{v[2 + kx], v[3 + kx]}, f2v{acc[2], acc[3]});
+                    acc[0] = lo[0];
+                    acc[1] = lo[1];
+                    acc[2] = hi[0];
+                    acc[3] = hi[1];
                 }
             }
         }

@@ -11,6 +11,8 @@
 // per-pixel LN/MLP chain then runs on one thread per pixel with its C channels in registers.
 #include "common.h"
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 namespace esm {
 namespace {
 
@@ -280,9 +282,12 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
         const float bias = lb[c];
         for (int it = lane; it < ITEMS; it += 64) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
-            float acc[SEG];
+            // output pairs (j, j + 1) as packed FMAs (v_pk_fma_f32): per output the same products summed in
+            // the same (ky, kx) order
+            static_assert(SEG % 2 == 0, "packed output pairs");
+            f2v acc[SEG / 2];
 #pragma unroll
-            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
+            for (int j = 0; j < SEG / 2; ++j) acc[j] = f2v{0.f, 0.f};
 #pragma unroll
             for (int ky = 0; ky < K; ++ky) {
                 float row[SEG + K - 1];
@@ -290,13 +295,16 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
 #pragma unroll
                 for (int j = 0; j < SEG + K - 1; ++j) row[j] = sr[j];
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx)
+                for (int kx = 0; kx < K; ++kx) {
+                    const f2v w2 = {w[ky * K + kx], w[ky * K + kx]};
 #pragma unroll
-                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * K + kx] * row[j + kx];
+                    for (int j = 0; j < SEG / 2; ++j)
+                        acc[j] = __builtin_elementwise_fma(w2, f2v{row[2 * j + kx], row[2 * j + 1 + kx]}, acc[j]);
+                }
             }
 #pragma unroll
             for (int j = 0; j < SEG; ++j)
-                if (px0 + j < OW) dst[c * OH * OW + py * OW + px0 + j] = acc[j] + bias;
+                if (px0 + j < OW) dst[c * OH * OW + py * OW + px0 + j] = acc[j >> 1][j & 1] + bias;
         }
     }
 }
@@ -609,9 +617,9 @@ __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float*
         const float bias = lb[c];
         for (int it = lane; it < ITEMS; it += 64) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
-            float acc[SEG];
+            f2v acc[SEG / 2];  // packed output pairs, as dw_region
 #pragma unroll
-            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
+            for (int j = 0; j < SEG / 2; ++j) acc[j] = f2v{0.f, 0.f};
 #pragma unroll
             for (int ky = 0; ky < 7; ++ky) {
                 float row[SEG + 6];
@@ -619,13 +627,16 @@ __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float*
 #pragma unroll
                 for (int j = 0; j < SEG + 6; ++j) row[j] = sr[j];
 #pragma unroll
-                for (int kx = 0; kx < 7; ++kx)
+                for (int kx = 0; kx < 7; ++kx) {
+                    const f2v w2 = {w[ky * 7 + kx], w[ky * 7 + kx]};
 #pragma unroll
-                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * 7 + kx] * row[j + kx];
+                    for (int j = 0; j < SEG / 2; ++j)
+                        acc[j] = __builtin_elementwise_fma(w2, f2v{row[2 * j + kx], row[2 * j + 1 + kx]}, acc[j]);
+                }
             }
 #pragma unroll
             for (int j = 0; j < SEG; ++j)
-                if (px0 + j < OW) dst[(c * OH + py) * DWS + px0 + j] = acc[j] + bias;
+                if (px0 + j < OW) dst[(c * OH + py) * DWS + px0 + j] = acc[j >> 1][j & 1] + bias;
         }
     }
 }
