@@ -12,6 +12,8 @@ dev = torch.device("cuda")
 T3 = 1 << 23
 NOTILE = 1 << 19  # conv.hip kHintNoTile: the automatic rules without the tiled forms
 CASES = [  # name, nd, cins, cout, k, s, p, spatial, B
+    ("S group_stem", 3, (32,), 8, 3, 1, 1, (12, 24, 78), 1),
+    ("S agg", 3, (8,), 8, 3, 1, 1, (12, 24, 78), 1),
     ("L group_stem B4", 3, (32,), 8, 3, 1, 1, (48, 96, 312), 4),
     ("L conv1.1 B4", 3, (24,), 24, 3, 1, 1, (24, 48, 156), 4),
     ("L agg B4", 3, (8,), 8, 3, 1, 1, (48, 96, 312), 4),
