@@ -54,21 +54,24 @@ __device__ __forceinline__ void mix_stage_w(float (&t)[C], const float* __restri
     float n[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) * inv * ln_w[c];
+    // output pairs (j, j + 1) as packed FMAs (v_pk_fma_f32); per output the same sum order
     float h[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-        float s = fc0_b[j];
+    for (int j = 0; j < C; j += 2) {
+        f2v s = {fc0_b[j], fc0_b[j + 1]};
 #pragma unroll
-        for (int i = 0; i < H2; ++i) s += fc0_w[j * H2 + i] * n[i];
-        h[j] = silu_fast(s);
+        for (int i = 0; i < H2; ++i) s = __builtin_elementwise_fma(f2v{fc0_w[j * H2 + i], fc0_w[(j + 1) * H2 + i]}, f2v{n[i], n[i]}, s);
+        h[j] = silu_fast(s[0]);
+        h[j + 1] = silu_fast(s[1]);
     }
     float cat[C];
 #pragma unroll
-    for (int i = 0; i < H2; ++i) {
-        float s = fc2_b[i];
+    for (int i = 0; i < H2; i += 2) {
+        f2v s = {fc2_b[i], fc2_b[i + 1]};
 #pragma unroll
-        for (int j = 0; j < C; ++j) s += fc2_w[i * C + j] * h[j];
-        cat[i] = s;
+        for (int j = 0; j < C; ++j) s = __builtin_elementwise_fma(f2v{fc2_w[i * C + j], fc2_w[(i + 1) * C + j]}, f2v{h[j], h[j]}, s);
+        cat[i] = s[0];
+        cat[i + 1] = s[1];
     }
 #pragma unroll
     for (int i = H2; i < C; ++i) cat[i] = n[i];
