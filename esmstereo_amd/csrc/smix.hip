@@ -11,8 +11,6 @@
 // per-pixel LN/MLP chain then runs on one thread per pixel with its C channels in registers.
 #include "common.h"
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
 namespace esm {
 namespace {
 
@@ -54,24 +52,21 @@ __device__ __forceinline__ void mix_stage_w(float (&t)[C], const float* __restri
     float n[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) n[c] = (t[c] - mu) * inv * ln_w[c];
-    // output pairs (j, j + 1) as packed FMAs (v_pk_fma_f32); per output the same sum order
     float h[C];
 #pragma unroll
-    for (int j = 0; j < C; j += 2) {
-        f2v s = {fc0_b[j], fc0_b[j + 1]};
+    for (int j = 0; j < C; ++j) {
+        float s = fc0_b[j];
 #pragma unroll
-        for (int i = 0; i < H2; ++i) s = __builtin_elementwise_fma(f2v{fc0_w[j * H2 + i], fc0_w[(j + 1) * H2 + i]}, f2v{n[i], n[i]}, s);
-        h[j] = silu_fast(s[0]);
-        h[j + 1] = silu_fast(s[1]);
+        for (int i = 0; i < H2; ++i) s += fc0_w[j * H2 + i] * n[i];
+        h[j] = silu_fast(s);
     }
     float cat[C];
 #pragma unroll
-    for (int i = 0; i < H2; i += 2) {
-        f2v s = {fc2_b[i], fc2_b[i + 1]};
+    for (int i = 0; i < H2; ++i) {
+        float s = fc2_b[i];
 #pragma unroll
-        for (int j = 0; j < C; ++j) s = __builtin_elementwise_fma(f2v{fc2_w[i * C + j], fc2_w[(i + 1) * C + j]}, f2v{h[j], h[j]}, s);
-        cat[i] = s[0];
-        cat[i + 1] = s[1];
+        for (int j = 0; j < C; ++j) s += fc2_w[i * C + j] * h[j];
+        cat[i] = s;
     }
 #pragma unroll
     for (int i = H2; i < C; ++i) cat[i] = n[i];
@@ -285,12 +280,9 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
         const float bias = lb[c];
         for (int it = lane; it < ITEMS; it += 64) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
-            // output pairs (j, j + 1) as packed FMAs (v_pk_fma_f32): per output the same products summed in
-            // the same (ky, kx) order
-            static_assert(SEG % 2 == 0, "packed output pairs");
-            f2v acc[SEG / 2];
+            float acc[SEG];
 #pragma unroll
-            for (int j = 0; j < SEG / 2; ++j) acc[j] = f2v{0.f, 0.f};
+            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky) {
                 float row[SEG + K - 1];
@@ -298,16 +290,13 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
 #pragma unroll
                 for (int j = 0; j < SEG + K - 1; ++j) row[j] = sr[j];
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) {
-                    const f2v w2 = {w[ky * K + kx], w[ky * K + kx]};
+                for (int kx = 0; kx < K; ++kx)
 #pragma unroll
-                    for (int j = 0; j < SEG / 2; ++j)
-                        acc[j] = __builtin_elementwise_fma(w2, f2v{row[2 * j + kx], row[2 * j + 1 + kx]}, acc[j]);
-                }
+                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * K + kx] * row[j + kx];
             }
 #pragma unroll
             for (int j = 0; j < SEG; ++j)
-                if (px0 + j < OW) dst[c * OH * OW + py * OW + px0 + j] = acc[j >> 1][j & 1] + bias;
+                if (px0 + j < OW) dst[c * OH * OW + py * OW + px0 + j] = acc[j] + bias;
         }
     }
 }
@@ -620,9 +609,9 @@ __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float*
         const float bias = lb[c];
         for (int it = lane; it < ITEMS; it += 64) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
-            f2v acc[SEG / 2];  // packed output pairs, as dw_region
+            float acc[SEG];
 #pragma unroll
-            for (int j = 0; j < SEG / 2; ++j) acc[j] = f2v{0.f, 0.f};
+            for (int j = 0; j < SEG; ++j) acc[j] = 0.f;
 #pragma unroll
             for (int ky = 0; ky < 7; ++ky) {
                 float row[SEG + 6];
@@ -630,16 +619,13 @@ __device__ __forceinline__ void f2_dw(const float* src, float* dst, const float*
 #pragma unroll
                 for (int j = 0; j < SEG + 6; ++j) row[j] = sr[j];
 #pragma unroll
-                for (int kx = 0; kx < 7; ++kx) {
-                    const f2v w2 = {w[ky * 7 + kx], w[ky * 7 + kx]};
+                for (int kx = 0; kx < 7; ++kx)
 #pragma unroll
-                    for (int j = 0; j < SEG / 2; ++j)
-                        acc[j] = __builtin_elementwise_fma(w2, f2v{row[2 * j + kx], row[2 * j + 1 + kx]}, acc[j]);
-                }
+                    for (int j = 0; j < SEG; ++j) acc[j] += w[ky * 7 + kx] * row[j + kx];
             }
 #pragma unroll
             for (int j = 0; j < SEG; ++j)
-                if (px0 + j < OW) dst[(c * OH + py) * DWS + px0 + j] = acc[j >> 1][j & 1] + bias;
+                if (px0 + j < OW) dst[(c * OH + py) * DWS + px0 + j] = acc[j] + bias;
         }
     }
 }
