@@ -448,7 +448,7 @@ XCD_SLAB_MIN_VOX_WIDE = int(os.environ.get("ESM_XCD_SLAB_MIN_VOX_WIDE", "16384")
 XCD_SLAB_OPS = tuple(t for t in os.environ.get("ESM_XCD_SLAB_OPS", "").split(",") if t)
 
 # shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
-_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
+_TUNED_PATH = os.environ.get("ESM_TUNED") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
 TUNED_HINTS: Dict[str, int] = {}
 if os.path.exists(_TUNED_PATH) and not os.environ.get("ESM_NO_TUNED"):
     with open(_TUNED_PATH) as _f:
