@@ -266,19 +266,22 @@ constexpr int kFConvTallMinTiles = 512;  // 3-row tiles at or above this many (2
 // consecutive outputs of a row, so each source value read from LDS feeds up to K outputs.  Per output
 // the products are summed over ky, then kx, as in smix_kernel.  Lanes of the last segment of a row
 // compute (and drop) up to SEG - 1 outputs past OW: src needs SEG + K - 2 floats of slack at its end.
-template <int C, int K, int OH, int OW, int SH, int SWP, int SEG>
+// NTH threads: with more waves than channels, WPC waves share a channel's items
+template <int C, int K, int OH, int OW, int SH, int SWP, int SEG, int NTH = kFThreads>
 __device__ __forceinline__ void dw_region(const float* src, float* dst, const float* lw, const float* lb, int wave,
                                           int lane) {
     constexpr int NSEG = (OW + SEG - 1) / SEG;
     constexpr int ITEMS = OH * NSEG;
-    constexpr int NWAVES = kFThreads / 64;
-    for (int c = wave; c < C; c += NWAVES) {
+    constexpr int NWAVES = NTH / 64;
+    constexpr int WPC = NWAVES > C ? NWAVES / C : 1;
+    for (int cw = wave; cw < C * WPC; cw += NWAVES) {
+        const int c = cw % C, part = cw / C;
         // the channel's K*K weights from the workgroup's LDS copy into registers (broadcast reads)
         float w[K * K];
 #pragma unroll
         for (int i = 0; i < K * K; ++i) w[i] = lw[c * K * K + i];
         const float bias = lb[c];
-        for (int it = lane; it < ITEMS; it += 64) {
+        for (int it = part * 64 + lane; it < ITEMS; it += 64 * WPC) {
             const int py = it / NSEG, px0 = (it - py * NSEG) * SEG;
             float acc[SEG];
 #pragma unroll
@@ -301,8 +304,10 @@ __device__ __forceinline__ void dw_region(const float* src, float* dst, const fl
     }
 }
 
-template <int C, int K, bool CONV, int HID, int CTH = 1>
-__global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a) {
+// NTH: threads per workgroup (1024 for the S-K map, 24 x 78 at C = 8: 120 workgroups on 256 CUs, so a
+// workgroup can take a whole CU and halve the per-thread depthwise work)
+template <int C, int K, bool CONV, int HID, int CTH = 1, int NTH = kFThreads>
+__global__ void __launch_bounds__(NTH) fmnet_kernel(const esm_fmnet_desc a) {
     constexpr int R = K / 2;
     constexpr int TH = CONV ? CTH : 4, TW = CONV ? kFConvTW : kFTW;                        // output tile
     constexpr int HC = CONV ? 1 : 0;                                    // t3 ring for conv0
@@ -310,12 +315,12 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int BH = CH + 2 * R, BW = CW + 2 * R, BP = BH * BW;      // t2 region
     constexpr int AH = CH + 4 * R, AW = CW + 4 * R, AP = AH * AW;      // t1 region
     constexpr int AWP = AW + 1, BWP = BW + 1;
-    constexpr int SEG = 4;
+    constexpr int SEG = NTH >= 1024 ? 2 : 4;  // 1024 threads: two waves per channel in the depthwise phases
     constexpr int SLACK = SEG + K;                                      // dw_region's over-read
-    constexpr int NWAVES = kFThreads / 64;
+    constexpr int NWAVES = NTH / 64;
     constexpr int NPX = TH * TW;
-    static_assert(AP <= kFThreads, "one t1 pixel per thread");
-    static_assert(!CONV || (NPX <= 64 && HID % NWAVES == 0), "conv0 / conv2: one pixel per lane");
+    static_assert(AP <= NTH, "one t1 pixel per thread");
+    static_assert(!CONV || (NPX <= 64 && (C == 8 || HID % NWAVES == 0)), "conv0 / conv2: one pixel per lane");
     // Every weight is staged in LDS once (below) and read there as a wave-uniform broadcast; the LDS
     // otherwise carries the activations of the three regions
     __shared__ float s1[C * AH * AWP + SLACK];  // t1 image, then t2 image ([C][BH][BWP])
@@ -337,7 +342,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     constexpr int CV0 = DW1 + C * K * K + C;
     constexpr int CV2 = CV0 + (CONV ? HID * C * 9 + HID : 0);
     constexpr int NW = CV2 + (CONV ? C * HID + C : 0);
-    constexpr int NWR = (NW + kFThreads - 1) / kFThreads;
+    constexpr int NWR = (NW + NTH - 1) / NTH;
     // every weight goes to LDS (the warm-up loads below fetch each one once, all in flight together with
     // the t1 pixel loads) and every phase reads its weights there as LDS broadcasts: as scalar loads they
     // were a chain of L2 (or, in the replayed step, memory) round trips per phase -- dw0 1.6, dw1 1.5,
@@ -346,11 +351,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     // form (two workgroups per CU on L-K's 96 x 312 maps), so there the weights stay scalar loads
     constexpr bool LW = C == 8;
     __shared__ float sw[LW ? NW : 1];
-    __shared__ float wsink[LW ? 1 : kFThreads];
+    __shared__ float wsink[LW ? 1 : NTH];
     float rw[NWR];
 #pragma unroll
     for (int k = 0; k < NWR; ++k) {
-        const int i = tid + k * kFThreads;
+        const int i = tid + k * NTH;
         const float* p = nullptr;
         int off = 0;
         if (i < DW0) {
@@ -405,7 +410,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     if constexpr (LW) {  // the warm-up values -> LDS weights, read from the next phase on
 #pragma unroll
         for (int k = 0; k < NWR; ++k) {
-            const int i = tid + k * kFThreads;
+            const int i = tid + k * NTH;
             if (i < NW) sw[i] = rw[k];
         }
     } else {  // scalar weights: the vector loads above only warm L2 for them
@@ -417,11 +422,11 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     __syncthreads();
     FM_STAMP(1);
     // dw0 (t1) on region B
-    dw_region<C, K, BH, BW, AH, AWP, SEG>(s1, s2, w_dw0, b_dw0, wave, lane);
+    dw_region<C, K, BH, BW, AH, AWP, SEG, NTH>(s1, s2, w_dw0, b_dw0, wave, lane);
     __syncthreads();
     FM_STAMP(2);
     // t2 = SMLayer1.mlp1 (SMLayer0.mlp2 (dw0)) on region B, into s1
-    for (int p = tid; p < BP; p += kFThreads) {
+    for (int p = tid; p < BP; p += NTH) {
         const int py = p / BW, px = p - (p / BW) * BW;
         const int gy = y0 - HC - R + py, gx = x0 - HC - R + px;
         const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
@@ -443,7 +448,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
     __syncthreads();
     FM_STAMP(3);
     // dw1 (t2) on region C
-    dw_region<C, K, CH, CW, BH, BWP, SEG>(s1, s2, w_dw1, b_dw1, wave, lane);
+    dw_region<C, K, CH, CW, BH, BWP, SEG, NTH>(s1, s2, w_dw1, b_dw1, wave, lane);
     __syncthreads();
     FM_STAMP(4);
     // t3 = SMLayer1.mlp2 (dw1) + x on region C
@@ -486,7 +491,7 @@ __global__ void __launch_bounds__(kFThreads) fmnet_kernel(const esm_fmnet_desc a
             // every lane works (a wave owning HID / 8 channels of the tile's 16 pixels left 3/4 of its lanes
             // idle: 1.6 us of the S-K block); weights as LDS reads, per output the products summed over c, ky,
             // kx as before
-            for (int e = tid; e < HID * NPX; e += kFThreads) {
+            for (int e = tid; e < HID * NPX; e += NTH) {
                 const int hc = e / NPX, pp = e - (e / NPX) * NPX;
                 const int py = pp / TW, px = pp - (pp / TW) * TW;
                 const float* w0 = lw_cv0 + hc * C * 9;
@@ -953,7 +958,7 @@ int launch_fmnet(const esm_fmnet_desc* d, hipStream_t s) {
     const dim3 grid(ceil_div(a.W, conv ? kFConvTW : kFTW), ceil_div(a.H, th), a.B);
     if (a.C == 8) {
         if (tall) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24, 3>), grid, dim3(kFThreads), 0, s, a);
-        else if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24>), grid, dim3(kFThreads), 0, s, a);
+        else if (conv) hipLaunchKernelGGL((fmnet_kernel<8, 7, true, 24, 1, 1024>), grid, dim3(1024), 0, s, a);
         else hipLaunchKernelGGL((fmnet_kernel<8, 7, false, 1>), grid, dim3(kFThreads), 0, s, a);
     } else if (a.C == 16) {
         if (tall) hipLaunchKernelGGL((fmnet_kernel<16, 7, true, 32, 3>), grid, dim3(kFThreads), 0, s, a);
