@@ -445,7 +445,7 @@ def test_conv_wide_form(cin, cout, k, p, shape):
                                                   ((16, 16, 32), 16, 1, 0, (47, 157)), ((8, 8), 24, 3, 1, (19, 40))])
 def test_conv_wide_form_multisource(cins, cout, k, p, shape):
     """Wide form over a channel concat (spx_Nx.0, agg_N.0), one descriptor per source: the sources carved
-    out of one allocation (as a launch list's arena carves them), then allocated apart with 1.5 GiB
+    out of one allocation (as a launch list's arena carves them), then allocated apart with 3 GiB
     between them, in both address orders; vs fp64 torch (1e-5 relative), and the two placements bitwise
     equal."""
     conv, bn = _mk(2, sum(cins), cout, k, 1, p, seed=10)
@@ -1084,7 +1084,7 @@ def test_hot_path_reads_inputs_in_place(graph):
                 up2 = [u + 0.01 * it for u in up]
                 out = model.hot_path(ml2, mr2, att, up2)[0]
                 assert torch.equal(out, expect(ml2, mr2, att, up2)), (name, it)
-            spacer = torch.empty(3 << 28, device=DEV)  # 1.5 GiB allocated between the plan's arena and the features
+            spacer = torch.empty(3 << 28, device=DEV)  # 3 GiB allocated between the plan's arena and the features
             upf = [u + 0.02 for u in up]
             out = model.hot_path(ml2, mr2, att, upf)[0]
             assert torch.equal(out, expect(ml2, mr2, att, upf)), name
