@@ -101,14 +101,16 @@ def _up(cin: int, cout: int, is_3d: bool, last: bool = False) -> BasicConv:
 
 
 def _pair(ctx: Ctx, first: BasicConv, srcs: Sequence[torch.Tensor], second, second_packed: Optional[PackedConv] = None,
-          **kw) -> torch.Tensor:
+          regress: Optional[torch.Tensor] = None, **kw) -> torch.Tensor:
     """``second(first(cat(srcs)))``: one launch with the intermediate in LDS where conv_pair2.hip has the
-    shape (2-D, plain BN + GELU epilogues), else two launches."""
+    shape (2-D, plain BN + GELU epilogues), else two launches.  ``regress``: see engine.run_pair2."""
     n0 = getattr(first, "_esm_name", "BasicConv")
     n1 = getattr(second, "_esm_name", "conv") if second is not None else "conv"
     pb = second_packed if second_packed is not None else second.packed()
     if not kw:
-        return run_pair2(ctx, first.packed(), srcs, pb, tags=(n0, n1))
+        return run_pair2(ctx, first.packed(), srcs, pb, tags=(n0, n1), regress=regress)
+    if regress is not None:
+        raise ValueError("_pair: regress with an epilogue")
     mid = run_conv(ctx, first.packed(), srcs, tag=n0)
     return run_conv(ctx, pb, [mid], tag=n1, **kw)
 
@@ -246,10 +248,11 @@ class _ESMUpsampler(nn.Module):
         return self._esm[1]
 
     def emit(self, ctx: Ctx, feats: Sequence[torch.Tensor], init_disp: torch.Tensor, final_scale: float = 1.0,
-             scaled_copies: Optional[float] = None) -> List[torch.Tensor]:
+             scaled_copies: Optional[float] = None, init_cost: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
         """Returns [finest, ..., coarsest] like the reference forward.  ``final_scale`` scales the
         finest output in its store; with ``scaled_copies`` every coarser output also gets a
-        scaled second copy (returned second): ([outputs], [scaled copies])."""
+        scaled second copy (returned second): ([outputs], [scaled copies]).  ``init_cost``: ``init_disp`` is
+        still to be computed as disparity_regression of this [B, D, H, W] cost (by the first pair)."""
         p = self._packed()
         me = getattr(self, "_esm_name", "upsample")
         prev = init_disp
@@ -257,7 +260,7 @@ class _ESMUpsampler(nn.Module):
         n = len(self.STAGES)
         for i, (tag, C, catc, spx_out, r, cf1, cf2, cat_i, ra, rb) in enumerate(self.STAGES):
             dm = getattr(self, f"dm{tag}")
-            d = _pair(ctx, dm[0], [prev], dm[1])
+            d = _pair(ctx, dm[0], [prev], dm[1], regress=init_cost if i == 0 else None)
             d = _pair(ctx, dm[2], [d], dm[3])
             spx = getattr(self, f"spx_{tag}")
             ref = getattr(self, f"ref{tag}")

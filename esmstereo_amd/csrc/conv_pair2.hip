@@ -22,6 +22,25 @@ namespace conv {
 namespace {
 
 constexpr int kP2Threads = 256;
+// a.hint bit 29 on convA: its single input channel is disparity_regression of the cost volume in src[0]
+// (src[0].C = D planes), also stored to a.out (see pair2_ok)
+constexpr int kHintPairReg = 1 << 29;
+
+// disparity_regression at one pixel, as regression.hip dispreg_kernel: products rounded, then summed in
+// d order (torch.sum(x * arange)): the same bits as the separate launch
+__device__ __forceinline__ float regress_px(const float* __restrict__ cp, int D, int sc) {
+#pragma clang fp contract(off)
+    float acc = 0.f;
+    for (int d0 = 0; d0 < D; d0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = d0 + k < D ? cp[(d0 + k) * sc] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (d0 + k < D) acc = acc + v[k] * static_cast<float>(d0 + k);
+    }
+    return acc;
+}
 
 template <int KA, int SA, int KB, int TH>
 struct P2Geo {
@@ -36,7 +55,7 @@ struct P2Geo {
     static constexpr int ACS = ACS0 + ((16 - ACS0 % 64) + 64) % 64;
 };
 
-template <int KA, int SA, int KB, int TH, int CINMAX>
+template <int KA, int SA, int KB, int TH, int CINMAX, bool REG>
 __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a, const esm_conv_desc bd) {
     using G = P2Geo<KA, SA, KB, TH>;
     constexpr int NA = G::NA, IR = G::IR, IC = G::IC, ICP = G::ICP, ICS = G::ICS, AR = G::AR, ACS = G::ACS;
@@ -75,6 +94,9 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
     constexpr int NIN = CINMAX * IR * IC;
     constexpr int PI = (NIN + kP2Threads - 1) / kP2Threads;
     float vi[PI];
+    // (REG: issued after the weight loads -- the regression's adds and the map's store wait for the cost
+    // planes, the weights' loads need not)
+    auto stage_in = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
         const int e = i * kP2Threads + tid;
@@ -85,9 +107,24 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         const int cl = c - (s2 ? c01 : (s1 ? c0 : 0));
         const int scs = s2 ? sc2 : (s1 ? sc1 : sc0), shs = s2 ? sh2 : (s1 ? sh1 : sh0);
         const bool ok = e < NIN && c < cin && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-        const float v = base[ok ? cl * scs + yi * shs + xi : 0];
-        vi[i] = ok ? v : 0.f;
+        if constexpr (REG) {
+            // the regressed map, written once per pixel by the tile that owns it: rows [yb0, yb0 + TH) and
+            // columns [xb0, xb0 + VB), the edge tiles extended to the map's edges (windows cover them: pair2_ok)
+            vi[i] = 0.f;
+            if (ok) {
+                const float v = regress_px(sp0 + yi * sh0 + xi, a.src[0].C, sc0);
+                vi[i] = v;
+                const bool own_y = (bk_.y == 0 || yi >= yb0) && (bk_.y == static_cast<int>(gridDim.y) - 1 || yi < yb0 + TH);
+                const bool own_x = (bk_.x == 0 || xi >= xb0) && (bk_.x == static_cast<int>(gridDim.x) - 1 || xi < xb0 + VB);
+                if (own_y && own_x) a.out[b * a.ob + yi * a.oh + xi] = v;
+            }
+        } else {
+            const float v = base[ok ? cl * scs + yi * shs + xi : 0];
+            vi[i] = ok ? v : 0.f;
+        }
     }
+    };
+    if constexpr (!REG) stage_in();
     constexpr int NWA = TA * CINMAX * 16;
     constexpr int PWA = (NWA + kP2Threads - 1) / kP2Threads;
     float vwa[PWA];
@@ -119,6 +156,7 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         const float v = (ok ? p : a.w)[ok ? c : 0];
         vep = ok ? v : ((k & 1) ? 0.f : 1.f);
     }
+    if constexpr (REG) stage_in();
     __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
@@ -202,7 +240,7 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
     }
 }
 
-template <int KA, int SA, int KB, int TH, int CINMAX>
+template <int KA, int SA, int KB, int TH, int CINMAX, bool REG = false>
 int launch_p2(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     using G = P2Geo<KA, SA, KB, TH>;
     const size_t lds = sizeof(float) * (static_cast<size_t>(CINMAX) * G::ICS + KA * KA * CINMAX * 16 + KB * KB * 256 +
@@ -210,7 +248,14 @@ int launch_p2(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     constexpr int VB = 16 - KB + 1;
     const dim3 grid(ceil_div(b.Wo, VB), ceil_div(b.Ho, TH), a.B);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv pair: grid too large");
-    hipLaunchKernelGGL((pair2_kernel<KA, SA, KB, TH, CINMAX>), grid, dim3(kP2Threads), lds, s, a, b);
+    if constexpr (REG) {
+        // every pixel of the regressed map inside the window of the tile that stores it
+        const int pr = b.ph + a.ph, pc = b.pw + a.pw;
+        if (pr < 0 || pc < 0 || TH > G::IR - pr || VB > G::IC - pc ||
+            (static_cast<int>(grid.y) - 1) * TH - pr + G::IR < a.Hi || (static_cast<int>(grid.x) - 1) * VB - pc + G::IC < a.Wi)
+            return arg_error("conv pair: regressed map not covered by the tiles");
+    }
+    hipLaunchKernelGGL((pair2_kernel<KA, SA, KB, TH, CINMAX, REG>), grid, dim3(kP2Threads), lds, s, a, b);
     return check_launch("conv pair");
 }
 
@@ -219,6 +264,10 @@ int launch_p2_k(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     // 2-row tiles on small maps (more workgroups), 4-row tiles where that still gives >= 256
     const long long tiles4 = static_cast<long long>(ceil_div(b.Wo, 16 - KB + 1)) * ceil_div(b.Ho, 4) * a.B;
     const bool small = tiles4 < 256;
+    if constexpr (KA == 5 && KB == 3) {
+        if (a.hint & kHintPairReg)
+            return small ? launch_p2<KA, SA, KB, 2, 4, true>(a, b, s) : launch_p2<KA, SA, KB, 4, 4, true>(a, b, s);
+    }
     if (a.Cin <= 4) return small ? launch_p2<KA, SA, KB, 2, 4>(a, b, s) : launch_p2<KA, SA, KB, 4, 4>(a, b, s);
     if (a.Cin <= 16) return small ? launch_p2<KA, SA, KB, 2, 16>(a, b, s) : launch_p2<KA, SA, KB, 4, 16>(a, b, s);
     if (a.Cin <= 32) return small ? launch_p2<KA, SA, KB, 2, 32>(a, b, s) : launch_p2<KA, SA, KB, 4, 32>(a, b, s);
@@ -232,7 +281,11 @@ int launch_p2_k(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
 
 // convA: 2-D, not transposed, k 1/3/5 (stride 1) or 3 (stride 2), <= 48 input channels (64 for k 1; 1..3 sources),
 // 16 outputs, BN + GELU, plain output (only convB's output is stored); convB: 2-D k1/k3 stride 1 over
-// convA's 16 channels, <= 16 outputs, BN + GELU, plain epilogue.
+// convA's 16 channels, <= 16 outputs, BN + GELU, plain epilogue.  With hint bit 29 on convA (5x5, one
+// input channel, convB 3x3): src[0] is a [B, D, H, W] cost volume (C = D) and convA's input map is its
+// disparity_regression (models/submodule.py:211-216), computed per staged pixel and stored once to
+// a.out ([B, 1, H, W], strides ob / oh) -- the regression launch of the hot path folded into the
+// upsampler's first pair.
 bool pair2_ok(const esm_conv_desc& a, const esm_conv_desc& b) {
     const bool a3 = a.kd > 1 || a.Di > 1 || a.Do > 1, b3 = b.kd > 1 || b.Di > 1 || b.Do > 1;
     if (a3 || b3 || a.transposed || b.transposed || a.shuffle > 1 || b.shuffle > 1) return false;
@@ -248,6 +301,11 @@ bool pair2_ok(const esm_conv_desc& a, const esm_conv_desc& b) {
     if (a.nsrc > 1)
         for (int i = 0; i < a.nsrc; ++i)
             if (a.src[i].C % 4) return false;
+    if (a.hint & kHintPairReg) {  // convA 5x5 1 -> 16 over the regressed map, convB 3x3 (the dm<t>.0 + .1 head)
+        if (a.kh != 5 || b.kh != 3 || a.Cin != 1 || a.nsrc != 1 || a.src[0].C < 1 || !a.out || a.out == b.out)
+            return false;
+        if (static_cast<long long>(a.src[0].C) * a.src[0].sc >= (1LL << 31) || a.src[0].sh >= (1 << 28)) return false;
+    }
     const long long last = (b.Cout - 1) * b.oc + (b.Ho - 1) * b.oh + b.Wo;
     return 4 * last < static_cast<long long>(kOOB) && b.oc < (1 << 28) && b.oh < (1 << 28);
 }

@@ -651,20 +651,57 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 
+# the hot path's disparity_regression folded into the upsampler's first pair (conv_pair2.hip hint bit 29):
+# one launch less on the S / M chains; ESM_PAIR_REGRESS=0 keeps the separate launch (A/B)
+PAIR_REGRESS_ENABLED = os.environ.get("ESM_PAIR_REGRESS", "1") != "0"
+HINT_PAIR_REGRESS = 1 << 29
+
+
 def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv,
-              tags: Tuple[str, str] = ("convA", "convB"), force: bool = False) -> torch.Tensor:
+              tags: Tuple[str, str] = ("convA", "convB"), force: bool = False,
+              regress: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``pb(pa(cat(srcs)))`` (two BasicConvs, BN + GELU each) as one launch where ``pair2_auto`` takes it
-    (``force``: wherever supported), else two launches."""
-    if not (pair2_supported(pa, pb, srcs) if force else pair2_auto(pa, pb, srcs)):
+    (``force``: wherever supported), else two launches.
+
+    ``regress``: a [B, D, H, W] cost volume whose disparity_regression (models/submodule.py:211-216) is
+    ``srcs[0]``, still to be computed: the pair computes it per staged pixel and stores it to ``srcs[0]``
+    where the kernel has the shape (5x5 1 -> 16 head, 3x3 convB), else the regression runs first as its
+    own launch."""
+    take = pair2_supported(pa, pb, srcs) if force else pair2_auto(pa, pb, srcs)
+    if regress is not None:
+        B_, D_, H_, W_ = (int(v) for v in regress.shape)
+        init = srcs[0]
+        fuse = (take and PAIR_REGRESS_ENABLED and len(srcs) == 1 and pa.k == 5 and pb.k == 3 and pa.cin == 1
+                and regress.stride(3) == 1 and tuple(init.shape) == (B_, 1, H_, W_) and init.stride(3) == 1)
+        if not fuse:
+            ctx.regression(0, regress, init, B_, D_, H_, W_)
+            regress = None
+    if not take:
         return run_conv(ctx, pb, [run_conv(ctx, pa, srcs, tag=tags[0])], tag=tags[1])
     da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
+    da.hint &= ~HINT_PAIR_REGRESS
     B = int(srcs[0].shape[0])
     virt = srcs[0].as_strided((B, pa.cout, int(da.Ho), int(da.Wo)), (0, 0, 0, 1))  # geometry only, never read
     db, out, mb = _conv_desc(ctx, pb, [virt], tag=tags[1])
     mid = 4 * B * pa.cout * int(da.Ho) * int(da.Wo)
-    ctx.meta.append(dict(name=f"{tags[0]}+{tags[1].rsplit('.', 1)[-1]}", kind="conv_pair", flops=ma["flops"] + mb["flops"],
-                         bytes=ma["bytes"] - mid + mb["bytes"] - mid, shape=f"pair {ma['shape']} + {mb['shape']}",
-                         reads=ma["reads"], writes=mb["writes"], key=ma["key"] + " | " + mb["key"], hint=0))
+    name = f"{tags[0]}+{tags[1].rsplit('.', 1)[-1]}"
+    flops, byts, reads, writes = ma["flops"] + mb["flops"], ma["bytes"] - mid + mb["bytes"] - mid, ma["reads"], mb["writes"]
+    if regress is not None:
+        # convA reads the D cost planes instead of the map, and the map is stored once
+        require_on(init.device, "pair regression", regress)
+        st = regress.stride()
+        da.src[0].ptr, da.src[0].C = regress.data_ptr(), D_
+        da.src[0].sb, da.src[0].sc, da.src[0].sh = st[0], st[1], st[2]
+        da.out = init.data_ptr()
+        da.ob, da.oc, da.oh = init.stride(0), init.stride(1), init.stride(2)
+        da.hint |= HINT_PAIR_REGRESS
+        ctx.hold(regress, init)
+        name = "disparity_regression+" + name
+        flops += 2 * B_ * D_ * H_ * W_
+        byts += 4 * B_ * D_ * H_ * W_
+        reads, writes = _spans(regress), writes + _spans(init)
+    ctx.meta.append(dict(name=name, kind="conv_pair", flops=flops, bytes=byts, shape=f"pair {ma['shape']} + {mb['shape']}",
+                         reads=reads, writes=writes, key=ma["key"] + " | " + mb["key"], hint=0))
     ctx.pair2(da, db)
     return out
 

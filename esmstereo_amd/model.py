@@ -438,9 +438,13 @@ class ESMStereo(nn.Module):
             raise RuntimeError(f"The size of tensor a ({Dc}) must match the size of tensor b ({D}) at non-singleton "
                                f"dimension 1 (maxdisp // cv_scale must be even, SURVEY.md §0.4)")
         init = ctx.empty(B, 1, h, w)
-        ctx.regression(1 if vs == 4 else 0, cost.view(B, D, h, w), init, B, D, h, w)
+        reg_cost = None
+        if vs == 4:
+            ctx.regression(1, cost.view(B, D, h, w), init, B, D, h, w)
+        else:  # disparity_regression: inside the upsampler's first pair where it fits, else its own launch there
+            reg_cost = cost.view(B, D, h, w)
         outs = self.upsample_module.emit(ctx, up, init, final_scale=4.0,
-                                         scaled_copies=4.0 if train_status else None)
+                                         scaled_copies=4.0 if train_status else None, init_cost=reg_cost)
         extra = self._emit_extra(ctx, cost.view(B, D, h, w), init, ml, up)
         if extra:
             return [outs[0].view(B, outs[0].shape[-2], outs[0].shape[-1])] + extra

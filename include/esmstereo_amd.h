@@ -133,7 +133,8 @@ typedef struct {
                      Bits 26-27 with WIDE / WIDET: rows per wave (1 / 2 / 3 = 2 / 4 / 8 rows, WIDET 1 / 2
                      sub-grid rows); 0 = the automatic choice.  Bit 28 with WIDE: each strip's channel groups
                      split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
-                     8 waves per workgroup splitting K (layers with more than 4 channel groups).
+                     8 waves per workgroup splitting K (layers with more than 4 channel groups); bit 29 on
+                     the first desc of esm_conv_pair2_f32: regression source (see there).
                      Bit 30 (any value of the other bits, including 0 = automatic): XCD-slab tile order for
                      the small / wide / wide3 / wideT / pair / single-output ConvT forms: each XCD runs a
                      contiguous band of tiles, so halo rows are fetched once per band instead of once per
@@ -279,6 +280,11 @@ int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
  * 16 outputs, <= 48 input channels (64 for k 1) over 1..3 sources (4-channel multiples when several);
  * a->out is not written.  b: k 1 or 3, stride 1, 16 inputs (its src[] is ignored: the input is a's
  * output), <= 16 outputs, plain epilogue.  ESM_ERR_ARG for a pair outside that set.
+ * Regression source (a->hint bit 29; a: 5x5, Cin 1, one source; b: 3x3): a->src[0] is a [B, D, H, W]
+ * cost volume (src[0].C = D, H x W = a's input extent) and a's input map is its disparity_regression
+ * sum_d cost[d] * d (models/submodule.py:211-216, the bits of esm_disp_regression_f32), which is also
+ * stored to a->out ([B, 1, H, W], strides ob / oh): the regression launch folded into the upsampler's
+ * first pair (models/ESMStereo.py:735-745).
  * (models/ESMStereo.py:185-259: the refinement hourglasses' conv2 / conv3 pairs and the upsampler
  * stages' dm<t> / spx_<t> pairs.) */
 int esm_conv_pair2_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);

@@ -753,6 +753,31 @@ def test_conv_pair2(cins, ka, sa, pa, kb, pb, coutb, H, W):
     assert rel(y, two) < 1e-5
 
 
+@pytest.mark.parametrize("B,D,H,W", [(1, 12, 24, 78), (1, 24, 48, 156), (1, 12, 96, 312), (2, 5, 7, 9), (2, 12, 25, 79)])
+def test_conv_pair2_regress(B, D, H, W):
+    """disparity_regression folded into the dm<t>.0 -> dm<t>.1 pair (conv_pair2.hip hint bit 29): the map it
+    stores is bitwise the separate regression launch's, and the pair's output bitwise the pair run on that
+    map (S-K 24x78 D12, M-K 48x156 D24, the 4-row-tile form at 96x312, ragged extents, batch 2)."""
+    from esmstereo_amd.engine import run_pair2
+    ca, ba = _mk(2, 1, 16, 5, 1, 1, seed=41 + W)
+    cb, bb = _mk(2, 16, 16, 3, 1, 1, seed=42 + H)
+    pa_, pb_ = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
+    cost = torch.randn(B, D, H, W)
+    costd = cost.to(DEV)
+    ctx = Ctx(DEV)
+    init = torch.full((B, 1, H, W), float("nan"), device=DEV)
+    n0 = len(ctx.meta)
+    y = run_pair2(ctx, pa_, [init], pb_, force=True, regress=costd)
+    assert [m["name"] for m in ctx.meta[n0:]] == ["disparity_regression+convA+convB"]
+    ref_init = torch.empty(B, 1, H, W, device=DEV)
+    ctx.regression(0, costd, ref_init, B, D, H, W)
+    assert torch.equal(init, ref_init)
+    two = run_pair2(ctx, pa_, [ref_init], pb_, force=True)
+    assert torch.equal(y, two)
+    ref = (cost * torch.arange(D, dtype=torch.float32).view(1, D, 1, 1)).sum(1, keepdim=True)
+    assert rel(init, ref) < 1e-6
+
+
 def test_conv_multisource_crop_and_epilogues():
     # agg_0-style: crop of a larger tensor + two more sources, 1x1 then residual/mul/up epilogues
     conv, bn = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=3)

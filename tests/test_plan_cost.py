@@ -55,7 +55,10 @@ def test_plan_flops_equal_flop_counter_on_oracle(case):
         O.hot_path({k: v.to("meta") for k, v in sd.items()}, cvs, md, True, M(B, 64, h, w), M(B, 64, h, w),
                    M(B, 32, h, w) if cvs == 16 else None, [M(*u) for u in ups])
     counted = fc.get_total_flops()
-    ours = sum(x["flops"] for x in meta if x["kind"] in CONV_KINDS)
+    # the flop counter sees convolutions only: take out disparity_regression's 2·B·D·h·w where the first pair
+    # of the upsampler computes it (the `disparity_regression+` pair)
+    reg = sum(2 * B * (md // cvs) * h * w for x in meta if x["name"].startswith("disparity_regression+"))
+    ours = sum(x["flops"] for x in meta if x["kind"] in CONV_KINDS) - reg
     assert ours == counted, (case, ours, counted, ours - counted)
 
 
@@ -107,11 +110,16 @@ def test_plan_per_op_cost(case):
             assert op["bytes"] == b, (name, op["bytes"], b)
         elif kind == "conv_pair":
             sa, sb = shape[len("pair "):].split(" + ")
-            na, nb = name.split("+")
+            reg = name.startswith("disparity_regression+")  # convA's 1-channel input regressed from the cost
+            na, nb = name.split("+")[-2:]
             nb = na.rsplit(".", 1)[0] + "." + nb
             ga, gb = re.search(r"in (\S+) out (\S+)", sa), re.search(r"in (\S+) out (\S+)", sb)
             fa, ba, wa, mid = _conv_cost(_layer(m, na), B, _ext(ga.group(1)), _ext(ga.group(2)))
             fb, bb, wb, _ = _conv_cost(_layer(m, nb), B, _ext(gb.group(1)), _ext(gb.group(2)))
+            if reg:
+                assert cvs != 4 and _ext(ga.group(1)) == (1, h, w), name
+                fa += 2 * B * D * h * w
+                ba += 4 * B * D * h * w  # the D cost planes read; the map is written instead of read
             assert op["flops"] == fa + fb, name
             assert op["bytes"] == ba + bb - 2 * 4 * mid, name  # the intermediate map never reaches HBM
         elif kind in ("shuffle_tail", "shuffle_conv"):
