@@ -8,7 +8,9 @@ library's interface is ``include/esmstereo_amd.h``.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -51,13 +53,49 @@ def _stale(obj: str, src: str) -> bool:
 NO_CONTRACT = {"volumes.hip", "regression.hip"}
 
 
+# Kernels allowed to use scratch (private) memory, bytes per lane: the direct conv's 2-D 5x5 forms and a few
+# of its 3-D forms (measured with them; none is on the S-K chain's hot forms).  Any other kernel that spills
+# or keeps a dynamically indexed array in scratch fails the build: the round-4 conv pair did, at 650-980
+# bytes per lane, through a lambda over the staging array, and lost ~25 % of the S-K step before it was seen.
+SCRATCH_OK = {
+    "_ZN3esm4conv12dconv_kernelILb0ELi5ELi1ELb0ELi2ELi2ELi1ELi4ELb1EEEv13esm_conv_desc": 204,
+    "_ZN3esm4conv12dconv_kernelILb0ELi5ELi1ELb0ELi2ELi2ELi1ELi4ELb0EEEv13esm_conv_desc": 200,
+    "_ZN3esm4conv12dconv_kernelILb1ELi1ELi1ELb0ELi2ELi2ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb1ELi3ELi1ELb0ELi1ELi1ELi4ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb1ELi3ELi1ELb0ELi1ELi2ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb1ELi3ELi2ELb0ELi1ELi1ELi4ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb1ELi3ELi2ELb0ELi1ELi1ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
+}
+
+
+def kernel_resources(stderr: str) -> dict:
+    """{mangled kernel: {"vgpr": n, "scratch": bytes per lane}} from hipcc's kernel-resource-usage remarks."""
+    out, cur = {}, None
+    for line in stderr.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+(VGPRs|ScratchSize \[bytes/lane\]): (\d+)", line)
+        if m and cur is not None:
+            cur["vgpr" if m.group(1) == "VGPRs" else "scratch"] = int(m.group(2))
+    return out
+
+
 def _compile(src: str, obj: str, defines=()) -> str:
     extra = ["-ffp-contract=off"] if os.path.basename(src) in NO_CONTRACT else []
     extra += [f"-D{d}" for d in defines]
-    cmd = [_hipcc()] + CXXFLAGS + extra + ["-c", src, "-o", obj]
+    cmd = [_hipcc()] + CXXFLAGS + extra + ["-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")
+    res = kernel_resources(r.stderr)
+    with open(obj + ".res.json", "w") as f:
+        json.dump(res, f, indent=0, sort_keys=True)
+    bad = {k: v["scratch"] for k, v in res.items() if v.get("scratch", 0) > SCRATCH_OK.get(k, 0)}
+    if bad and not defines:  # (the diagnostic build's stamps may spill)
+        os.remove(obj)  # rebuilt (and re-checked) next time
+        raise RuntimeError(f"{os.path.basename(src)}: kernels using scratch memory (bytes per lane): {bad}")
     return obj
 
 

@@ -94,37 +94,21 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
     constexpr int NIN = CINMAX * IR * IC;
     constexpr int PI = (NIN + kP2Threads - 1) / kP2Threads;
     float vi[PI];
-    // (REG: issued after the weight loads -- the regression's adds and the map's store wait for the cost
-    // planes, the weights' loads need not)
-    auto stage_in = [&]() __attribute__((always_inline)) {
+    if constexpr (!REG) {
 #pragma unroll
-    for (int i = 0; i < PI; ++i) {
-        const int e = i * kP2Threads + tid;
-        const int q = e % IC, r = (e / IC) % IR, c = e / (IC * IR);
-        const int yi = yi0 + r, xi = xi0 + q;
-        const bool s1 = c >= c0, s2 = c >= c01;
-        const float* base = s2 ? sp2 : (s1 ? sp1 : sp0);
-        const int cl = c - (s2 ? c01 : (s1 ? c0 : 0));
-        const int scs = s2 ? sc2 : (s1 ? sc1 : sc0), shs = s2 ? sh2 : (s1 ? sh1 : sh0);
-        const bool ok = e < NIN && c < cin && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-        if constexpr (REG) {
-            // the regressed map, written once per pixel by the tile that owns it: rows [yb0, yb0 + TH) and
-            // columns [xb0, xb0 + VB), the edge tiles extended to the map's edges (windows cover them: pair2_ok)
-            vi[i] = 0.f;
-            if (ok) {
-                const float v = regress_px(sp0 + yi * sh0 + xi, a.src[0].C, sc0);
-                vi[i] = v;
-                const bool own_y = (bk_.y == 0 || yi >= yb0) && (bk_.y == static_cast<int>(gridDim.y) - 1 || yi < yb0 + TH);
-                const bool own_x = (bk_.x == 0 || xi >= xb0) && (bk_.x == static_cast<int>(gridDim.x) - 1 || xi < xb0 + VB);
-                if (own_y && own_x) a.out[b * a.ob + yi * a.oh + xi] = v;
-            }
-        } else {
+        for (int i = 0; i < PI; ++i) {
+            const int e = i * kP2Threads + tid;
+            const int q = e % IC, r = (e / IC) % IR, c = e / (IC * IR);
+            const int yi = yi0 + r, xi = xi0 + q;
+            const bool s1 = c >= c0, s2 = c >= c01;
+            const float* base = s2 ? sp2 : (s1 ? sp1 : sp0);
+            const int cl = c - (s2 ? c01 : (s1 ? c0 : 0));
+            const int scs = s2 ? sc2 : (s1 ? sc1 : sc0), shs = s2 ? sh2 : (s1 ? sh1 : sh0);
+            const bool ok = e < NIN && c < cin && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
             const float v = base[ok ? cl * scs + yi * shs + xi : 0];
             vi[i] = ok ? v : 0.f;
         }
     }
-    };
-    if constexpr (!REG) stage_in();
     constexpr int NWA = TA * CINMAX * 16;
     constexpr int PWA = (NWA + kP2Threads - 1) / kP2Threads;
     float vwa[PWA];
@@ -156,7 +140,26 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         const float v = (ok ? p : a.w)[ok ? c : 0];
         vep = ok ? v : ((k & 1) ? 0.f : 1.f);
     }
-    if constexpr (REG) stage_in();
+    if constexpr (REG) {
+        // after the weight loads (the regression's adds and the map's store wait for the cost planes, the
+        // weights' loads need not); channel 0 only (Cin 1), the other staged channels zero.  The map is
+        // written once per pixel by the tile that owns it: rows [yb0, yb0 + TH) and columns [xb0, xb0 + VB),
+        // the edge tiles extended to the map's edges (their windows cover them: launch_p2)
+#pragma unroll
+        for (int i = 0; i < PI; ++i) {
+            const int e = i * kP2Threads + tid;
+            const int q = e % IC, r = (e / IC) % IR, c = e / (IC * IR);
+            const int yi = yi0 + r, xi = xi0 + q;
+            vi[i] = 0.f;
+            if (e < NIN && c == 0 && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi) {
+                const float v = regress_px(sp0 + yi * sh0 + xi, a.src[0].C, sc0);
+                vi[i] = v;
+                const bool own_y = (bk_.y == 0 || yi >= yb0) && (bk_.y == static_cast<int>(gridDim.y) - 1 || yi < yb0 + TH);
+                const bool own_x = (bk_.x == 0 || xi >= xb0) && (bk_.x == static_cast<int>(gridDim.x) - 1 || xi < xb0 + VB);
+                if (own_y && own_x) a.out[b * a.ob + yi * a.oh + xi] = v;
+            }
+        }
+    }
     __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
@@ -182,13 +185,28 @@ __global__ void __launch_bounds__(kP2Threads) pair2_kernel(const esm_conv_desc a
         // accumulator indices stay compile-time (a runtime index turns every MFMA into a select chain
         // over the accumulators): two chains alternate by tap, or by channel group for 1x1 convA
         if constexpr (TA > 1) {
-            for (int kc = 0; kc < kca; ++kc) {
+            if (cin == 1) {
+                // one input channel (the dm<t>.0 heads): the taps fill k, 4 per MFMA (7 MFMAs per row for 5x5,
+                // not 25 with 3 zero channels each); lane group kq takes tap 4 kc + kq
+                const float* ib0 = in + i * SA * ICP + n * SA;
 #pragma unroll
-                for (int t = 0; t < TA; ++t) {
-                    const int ky = t / KA, kx = t % KA;
-                    const float bv = ib[4 * kc * ICS + ky * ICP + kx];
-                    const float av = wp[(t * CINMAX + 4 * kc) * 16];
-                    acc[t & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t & 1], 0, 0, 0);
+                for (int kc = 0; kc < (TA + 3) / 4; ++kc) {
+                    const int t = 4 * kc + kq;
+                    const bool tv = t < TA;
+                    const int tt = tv ? t : 0;
+                    const float bv = ib0[(tt / KA) * ICP + tt % KA];
+                    const float av = wa[tt * CINMAX * 16 + n];
+                    acc[kc & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv ? av : 0.f, tv ? bv : 0.f, acc[kc & 1], 0, 0, 0);
+                }
+            } else {
+                for (int kc = 0; kc < kca; ++kc) {
+#pragma unroll
+                    for (int t = 0; t < TA; ++t) {
+                        const int ky = t / KA, kx = t % KA;
+                        const float bv = ib[4 * kc * ICS + ky * ICP + kx];
+                        const float av = wp[(t * CINMAX + 4 * kc) * 16];
+                        acc[t & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t & 1], 0, 0, 0);
+                    }
                 }
             }
         } else {
