@@ -281,11 +281,17 @@ template <int KA, int SA, int KB>
 int launch_p2_k(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     // 2-row tiles on small maps (more workgroups), 4-row tiles where that still gives >= 256
     const long long tiles4 = static_cast<long long>(ceil_div(b.Wo, 16 - KB + 1)) * ceil_div(b.Ho, 4) * a.B;
-    const bool small = tiles4 < 256;
+    // b.hint bits 26-27: tile rows 2 / 4 / 8 (8: <= 16 input channels), 0 automatic
+    const int thsel = (b.hint >> 26) & 3;
+    const bool small = thsel ? thsel == 1 : tiles4 < 256;
+    const bool tall = thsel == 3 && a.Cin <= 16;
     if constexpr (KA == 5 && KB == 3) {
-        if (a.hint & kHintPairReg)
+        if (a.hint & kHintPairReg) {
+            if (tall) return launch_p2<KA, SA, KB, 8, 4, true>(a, b, s);
             return small ? launch_p2<KA, SA, KB, 2, 4, true>(a, b, s) : launch_p2<KA, SA, KB, 4, 4, true>(a, b, s);
+        }
     }
+    if (tall) return a.Cin <= 4 ? launch_p2<KA, SA, KB, 8, 4>(a, b, s) : launch_p2<KA, SA, KB, 8, 16>(a, b, s);
     if (a.Cin <= 4) return small ? launch_p2<KA, SA, KB, 2, 4>(a, b, s) : launch_p2<KA, SA, KB, 4, 4>(a, b, s);
     if (a.Cin <= 16) return small ? launch_p2<KA, SA, KB, 2, 16>(a, b, s) : launch_p2<KA, SA, KB, 4, 16>(a, b, s);
     if (a.Cin <= 32) return small ? launch_p2<KA, SA, KB, 2, 32>(a, b, s) : launch_p2<KA, SA, KB, 4, 32>(a, b, s);

@@ -654,6 +654,10 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
 # the hot path's disparity_regression folded into the upsampler's first pair (conv_pair2.hip hint bit 29):
 # one launch less on the S / M chains; ESM_PAIR_REGRESS=0 keeps the separate launch (A/B)
 PAIR_REGRESS_ENABLED = os.environ.get("ESM_PAIR_REGRESS", "1") != "0"
+# tile rows of the pairs whose first conv's name contains one of the comma-separated substrings (A/B knobs;
+# conv_pair2.hip: 2 / 4 / 8 rows, 8 only up to 16 input channels; default: the launcher's choice)
+PAIR2_TH = {sel: tuple(x for x in os.environ.get(f"ESM_PAIR2_TH{n}", "").split(",") if x)
+            for sel, n in ((1, 2), (2, 4), (3, 8))}
 HINT_PAIR_REGRESS = 1 << 29
 
 
@@ -683,6 +687,10 @@ def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: Packed
     B = int(srcs[0].shape[0])
     virt = srcs[0].as_strided((B, pa.cout, int(da.Ho), int(da.Wo)), (0, 0, 0, 1))  # geometry only, never read
     db, out, mb = _conv_desc(ctx, pb, [virt], tag=tags[1])
+    db.hint &= ~(3 << 26)  # convB's bits 26-27 pick the pair's tile rows (a standalone conv's tuned hint does not)
+    for sel, subs in PAIR2_TH.items():
+        if any(x in tags[0] for x in subs):
+            db.hint |= sel << 26
     mid = 4 * B * pa.cout * int(da.Ho) * int(da.Wo)
     name = f"{tags[0]}+{tags[1].rsplit('.', 1)[-1]}"
     flops, byts, reads, writes = ma["flops"] + mb["flops"], ma["bytes"] - mid + mb["bytes"] - mid, ma["reads"], mb["writes"]

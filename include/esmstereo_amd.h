@@ -284,7 +284,8 @@ int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
  * cost volume (src[0].C = D, H x W = a's input extent) and a's input map is its disparity_regression
  * sum_d cost[d] * d (models/submodule.py:211-216, the bits of esm_disp_regression_f32), which is also
  * stored to a->out ([B, 1, H, W], strides ob / oh): the regression launch folded into the upsampler's
- * first pair (models/ESMStereo.py:735-745).
+ * first pair (models/ESMStereo.py:735-745).  b->hint bits 26-27: tile rows 2 / 4 / 8 (8 only with <= 16
+ * input channels; other bits of b->hint are ignored), 0 = automatic (4 rows where that gives >= 256 tiles).
  * (models/ESMStereo.py:185-259: the refinement hourglasses' conv2 / conv3 pairs and the upsampler
  * stages' dm<t> / spx_<t> pairs.) */
 int esm_conv_pair2_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
