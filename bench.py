@@ -545,6 +545,8 @@ def main() -> None:
     ap.add_argument("--streams", type=int, default=2,
                     help="side measurement: independent B-pair instances on this many concurrent streams")
     ap.add_argument("--cpu-standin", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
+    ap.add_argument("--dist", action="store_true", help="initialise the RCCL process group and gather through the "
+                    "collective even at one rank (tests/test_gpu_dist.py: the N > 1 code path on a one-GPU box)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
@@ -569,7 +571,13 @@ def main() -> None:
         return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        if world == 1:  # a one-rank group without a launcher: a local rendezvous
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ["WORLD_SIZE"] = "1"
         torch.distributed.init_process_group("nccl", device_id=dev)
     world, rank = D.world_info()
     if args.global_batch is not None:
@@ -621,7 +629,7 @@ def main() -> None:
                        "trailing_dispatches": meta[dom].get("launches", 1) * (3 + args.steps) + (23 if has_stem else 0)}, f)
 
     # the timed region: the plain plan (one hipGraph per step) + the per-step disparity all-gather
-    gather = D.DisparityGather(hp.outputs[0]) if world > 1 and not args.no_gather else None
+    gather = D.DisparityGather(hp.outputs[0], collective=use_dist) if use_dist and not args.no_gather else None
 
     def step():
         hp.launch()
@@ -670,6 +678,9 @@ def main() -> None:
             "roofline": roof,
             "roofline_step": step_roofline(meta, ms_step, args.batch),
         }
+        if use_dist:
+            line["collective"] = (f"{torch.distributed.get_backend()} all_gather_into_tensor of the [{args.batch}, "
+                                  f"{args.height}, {args.width}] disparities per step" if gather is not None else None)
         mf = [i for i, m in enumerate(meta) if m["name"] == "group_stem"]
         if mf and marg is not None:
             r = kernel_roofline(meta[mf[0]], marg[mf[0]] * 1e-3)
@@ -702,7 +713,7 @@ def main() -> None:
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         torch.distributed.destroy_process_group()
 
 

@@ -131,6 +131,7 @@ SIGNATURES = {
     "esm_plan_graph_build": (c_int, [c_void_p, c_void_p]),
     "esm_plan_graph_launch": (c_int, [c_void_p, c_void_p]),
     "esm_plan_rebind": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(ctypes.c_uint64), POINTER(c_void_p)]),
+    "esm_plan_busy": (c_int, [c_void_p]),
     "esm_plan_set_probe": (c_int, [c_void_p, c_int, c_int]),
     "esm_plan_probe_read": (c_int, [c_void_p, POINTER(c_float), c_int]),
 }

@@ -304,12 +304,14 @@ __global__ void __launch_bounds__(64 * KSW) wconv3r_kernel(const esm_conv_desc a
     }
 }
 
-// output rows per workgroup of the row-streaming variant (A/B: ESM_W3_ROWS=1 disables it).  Measured at S-K
+// output rows per workgroup of the row-streaming variant (A/B: ESM_W3_ROWS=1 disables it, read only with
+// ESM_AB=1 so that a caller's environment never selects an untested form).  Measured at S-K
 // (scripts/gpu_r03_w3rows.sh, two rotations): RB 1 / 2 / 3 / 4 -> group_stem in the replayed step 13.6 /
 // 13.4 / 10.1 / 11.5-12.2 us.  Neither two accumulators per row nor the same form for the 8 -> 8 `agg`
 // (2 waves) measured faster; both were removed.
 static const int kW3Rows = [] {
-    const char* e = getenv("ESM_W3_ROWS");
+    const char* ab = getenv("ESM_AB");
+    const char* e = ab && ab[0] == '1' && ab[1] == 0 ? getenv("ESM_W3_ROWS") : nullptr;
     return e ? atoi(e) : 3;
 }();
 template <int KSW, int RB>

@@ -594,6 +594,8 @@ int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const ui
     for (int k = 0; k < n; ++k) {
         const uintptr_t lo = reinterpret_cast<uintptr_t>(old_base[k]);
         if (!old_base[k] || !new_base[k]) return esm::arg_error("plan: rebind of a null buffer");
+        for (const Rebase::Range& g : rb.r)
+            if (lo < g.hi && g.lo < lo + bytes[k]) return esm::arg_error("plan: rebind ranges overlap");
         rb.r.push_back({lo, lo + bytes[k], reinterpret_cast<intptr_t>(new_base[k]) - static_cast<intptr_t>(lo)});
     }
     std::vector<char> dirty(plan->ops.size(), 0);
@@ -607,6 +609,7 @@ int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const ui
     // the instantiated graph's kernel arguments are about to change: the previous replay must have
     // finished reading them
     if (plan->launched && hipEventSynchronize(plan->last_launch) != hipSuccess) {
+        plan->clear_graph();  // the ops moved but the nodes did not: rebuild from the ops at the next launch
         esm::set_error("plan: hipEventSynchronize failed");
         return ESM_ERR_RUNTIME;
     }
@@ -617,6 +620,16 @@ int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const ui
         }
     }
     return moved;
+}
+
+int esm_plan_busy(esm_plan* plan) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (!plan->launched) return 0;
+    const hipError_t e = hipEventQuery(plan->last_launch);
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorNotReady) return 1;
+    esm::set_error("plan: hipEventQuery failed");
+    return ESM_ERR_RUNTIME;
 }
 
 int esm_plan_set_probe(esm_plan* plan, int index, int ring) {

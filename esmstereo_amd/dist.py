@@ -111,14 +111,19 @@ class DisparityGather:
     buffer: ``all_gather_into_tensor`` over RCCL, the list form over gloo.  Every rank holds the
     same number of pairs (``local_batch`` enforces it), so no padding is needed on the hot loop."""
 
-    def __init__(self, local: torch.Tensor, group=None):
+    def __init__(self, local: torch.Tensor, group=None, collective: Optional[bool] = None):
+        """``collective``: exchange through the process group even at world size 1 (default: only
+        when there is more than one rank; the single-GPU RCCL test forces it)."""
         self.group = group
         self.world, _ = world_info(group)
         self.buf = local.new_empty((self.world,) + tuple(local.shape))
-        self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        if self.collective and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("DisparityGather: collective exchange needs an initialised process group")
+        self.nccl = self.collective and dist.get_backend(group) == "nccl"
 
     def __call__(self, local: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if not self.collective:
             self.buf[0].copy_(local)
         elif self.nccl:
             dist.all_gather_into_tensor(self.buf, local, group=self.group)

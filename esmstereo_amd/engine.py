@@ -16,6 +16,7 @@ import ctypes
 import json
 import math
 import os
+import threading
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -35,15 +36,21 @@ def _rup(x: int, m: int) -> int:
 
 # Dry emission (Ctx(dry=True)): the launch list is walked with shape-only ``meta`` tensors, nothing is
 # submitted and no device memory is touched.  It sizes a plan's arena before the real emission and
-# lets CPU tests read every op's algorithmic cost (ctx.meta).  While one is active, meta tensors pass
-# the device checks below; they can never reach a kernel, because a dry Ctx submits nothing.
-_DRY_DEPTH = 0
+# lets CPU tests read every op's algorithmic cost (ctx.meta).  While one is active IN THIS THREAD, meta
+# tensors pass the device checks below; they can never reach a kernel, because a dry Ctx submits nothing.
+# The depth is thread-local: a dry emission in one thread never relaxes another thread's eager checks
+# (ADVICE r4).
+_DRY = threading.local()
+
+
+def _dry_depth() -> int:
+    return getattr(_DRY, "depth", 0)
 
 
 def require_device(t: torch.Tensor, what: str) -> None:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{what}: expected a torch.Tensor")
-    if _DRY_DEPTH and t.device.type == "meta":
+    if t.device.type == "meta" and _dry_depth():
         return
     if t.device.type != "cuda":
         raise RuntimeError(f"{what}: esmstereo_amd runs on ROCm devices only (got a {t.device.type} tensor); "
@@ -57,11 +64,12 @@ def require_device(t: torch.Tensor, what: str) -> None:
 def require_on(dev: torch.device, what: str, *ts: Optional[torch.Tensor]) -> None:
     """Every pointer a kernel dereferences must live on the launch device (a host or
     other-device pointer would fault the GPU, so this is checked on the host first)."""
-    if _DRY_DEPTH:  # a dry emission submits nothing (its buffers are shape-only)
-        return
+    dry = _dry_depth()
     for t in ts:
         if t is None:
             continue
+        if dry and (t.device.type == "meta" or torch.device(dev).type == "meta"):
+            continue  # a dry emission submits nothing (its buffers are shape-only)
         if t.device != dev or t.dtype != torch.float32:
             raise RuntimeError(f"{what}: tensor on {t.device} ({t.dtype}); expected float32 on {dev} "
                                "(move the module to the input's device)")
@@ -201,20 +209,18 @@ class Ctx:
         self.num_ops = 0       # ops submitted (or, dry, recorded)
 
     def __enter__(self) -> "Ctx":
-        global _DRY_DEPTH
         if self.dry:
-            _DRY_DEPTH += 1
+            _DRY.depth = _dry_depth() + 1
         return self
 
     def __exit__(self, *exc) -> None:
-        global _DRY_DEPTH
         if self.dry:
-            _DRY_DEPTH -= 1
+            _DRY.depth = _dry_depth() - 1
 
     def _submit(self) -> bool:
         """Count one op; True when it is to be handed to the library (not a dry emission)."""
         self.num_ops += 1
-        if self.dry and not _DRY_DEPTH:
+        if self.dry and not _dry_depth():
             raise RuntimeError("a dry Ctx must be used as a context manager")
         return not self.dry
 
@@ -429,6 +435,16 @@ def eager_emit(device: torch.device, fn, *args, **kw):
 # ----------------------------------------------------------------------------- ops
 
 
+# A/B switches.  The kernel-selection knobs below are read from the environment only when ESM_AB=1 (the
+# measurement scripts set it); otherwise every knob takes its measured default, so a caller's environment
+# can never select a combination of forms the GPU suite did not run.
+AB = os.environ.get("ESM_AB") == "1"
+
+
+def _ab(name: str, default: str) -> str:
+    return os.environ.get(name, default) if AB else default
+
+
 # Measured tile choices (scripts/autotune.py on MI355X, in the hot path's own launch sequence):
 # XCD-slab tile order (esm_conv_desc.hint bit 30, esm_shuffle_tail_desc.flags bit 0; common.h xcd_block)
 # for launches whose input or output map (B x D x H x W) has at least this many pixels: there it takes
@@ -436,21 +452,21 @@ def eager_emit(device: torch.device, fn, *args, **kw):
 # cost in step time, while on the hourglasses' small maps it measured 0.1-1 us slower per launch
 # (round 3, S-K, rocprofv3 op maps; every launch remapped: +10 us on the S-K step).
 HINT_XCD_SLAB = 1 << 30
-XCD_SLAB_MIN_PIX = int(os.environ.get("ESM_XCD_SLAB_MIN_PIX", "65536"))
+XCD_SLAB_MIN_PIX = int(_ab("ESM_XCD_SLAB_MIN_PIX", "65536"))
 # the same order on 3-D volumes (B x D x H x W output or input voxels over the threshold); ESM_XCD_SLAB_3D=0
 # leaves every 3-D launch in the default order (A/B measurements)
-XCD_SLAB_3D = os.environ.get("ESM_XCD_SLAB_3D", "1") != "0"
+XCD_SLAB_3D = _ab("ESM_XCD_SLAB_3D", "1") != "0"
 # 3-D launches with >= 32 input channels from this many output voxels: the S / M `group_stem` (12x24x78),
 # whose 32-channel input each workgroup re-reads with its halo: 15.8 -> 7.8 MB per launch, step time
 # unchanged (round 4, two alternations, profiles/r04_xcd_group_stem_SK.txt)
-XCD_SLAB_MIN_VOX_WIDE = int(os.environ.get("ESM_XCD_SLAB_MIN_VOX_WIDE", "16384"))
+XCD_SLAB_MIN_VOX_WIDE = int(_ab("ESM_XCD_SLAB_MIN_VOX_WIDE", "16384"))
 # launches (by name, comma-separated) given the slab order whatever their size (A/B measurements)
-XCD_SLAB_OPS = tuple(t for t in os.environ.get("ESM_XCD_SLAB_OPS", "").split(",") if t)
+XCD_SLAB_OPS = tuple(t for t in _ab("ESM_XCD_SLAB_OPS", "").split(",") if t)
 
 # shape key -> esm_conv_desc.hint.  Layers not in the table take the library's automatic rules.
-_TUNED_PATH = os.environ.get("ESM_TUNED") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
+_TUNED_PATH = _ab("ESM_TUNED", "") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_hints.json")
 TUNED_HINTS: Dict[str, int] = {}
-if os.path.exists(_TUNED_PATH) and not os.environ.get("ESM_NO_TUNED"):
+if os.path.exists(_TUNED_PATH) and not _ab("ESM_NO_TUNED", ""):
     with open(_TUNED_PATH) as _f:
         TUNED_HINTS = {k: int(v) for k, v in json.load(_f).get("hints", {}).items()}
 
@@ -612,7 +628,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
 
 # Two consecutive 2-D BasicConvs as one launch (esm_conv_pair2_f32, conv_pair2.hip); ESM_PAIR2=0
 # runs every pair as two launches (A/B measurements)
-PAIR2_ENABLED = os.environ.get("ESM_PAIR2", "1") != "0"
+PAIR2_ENABLED = _ab("ESM_PAIR2", "1") != "0"
 
 
 def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
@@ -626,10 +642,6 @@ def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]
     if pb.stride != 1 or pb.k not in (1, 3) or pa.act != ACT_GELU or pb.act != ACT_GELU:
         return False
     return len(srcs) == 1 or all(int(t.shape[1]) % 4 == 0 for t in srcs)
-
-
-# every supported pair on maps of at most this many output pixels (A/B knob; 0 = the rules below only)
-PAIR2_SMALL_MAXPIX = int(os.environ.get("ESM_PAIR2_SMALL_MAXPIX", "0"))
 
 
 def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
@@ -646,17 +658,15 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     Ho = (int(srcs[0].shape[2]) + 2 * pa.pad - pa.k) // pa.stride + 1
     Wo = (int(srcs[0].shape[3]) + 2 * pa.pad - pa.k) // pa.stride + 1
     light = pa.cin * pa.k * pa.k
-    if B * Ho * Wo <= PAIR2_SMALL_MAXPIX:
-        return True
     return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 
 # the hot path's disparity_regression folded into the upsampler's first pair (conv_pair2.hip hint bit 29):
 # one launch less on the S / M chains; ESM_PAIR_REGRESS=0 keeps the separate launch (A/B)
-PAIR_REGRESS_ENABLED = os.environ.get("ESM_PAIR_REGRESS", "1") != "0"
+PAIR_REGRESS_ENABLED = _ab("ESM_PAIR_REGRESS", "1") != "0"
 # tile rows of the pairs whose first conv's name contains one of the comma-separated substrings (A/B knobs;
 # conv_pair2.hip: 2 / 4 / 8 rows, 8 only up to 16 input channels; default: the launcher's choice)
-PAIR2_TH = {sel: tuple(x for x in os.environ.get(f"ESM_PAIR2_TH{n}", "").split(",") if x)
+PAIR2_TH = {sel: tuple(x for x in _ab(f"ESM_PAIR2_TH{n}", "").split(",") if x)
             for sel, n in ((1, 2), (2, 4), (3, 8))}
 HINT_PAIR_REGRESS = 1 << 29
 
@@ -764,7 +774,7 @@ def run_smix(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], *, dw: Opti
 # The whole FMBlock as two launches (esm_fmnet_desc.work, smix.hip fm2a / fm2b) on maps of at least this
 # many pixels (B x H x W); smaller maps keep the one-launch form, whose halo recompute is cheap there and
 # whose single launch boundary matters (S-K: 24 x 78)
-FM2_MIN_PIX = int(os.environ.get("ESM_FM2_MIN_PIX", "16384"))
+FM2_MIN_PIX = int(_ab("ESM_FM2_MIN_PIX", "16384"))
 
 
 def run_fmnet(ctx: Ctx, x: torch.Tensor, stages: Sequence[SmixStage], dw0: Tuple[torch.Tensor, torch.Tensor],
@@ -891,15 +901,18 @@ def run_shuffle_tail(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, out: Optio
 
 # tail(upsampling(x)) and the refinement's first conv in one launch (esm_shuffle_conv_f32);
 # ESM_SHUFFLE_CONV=0 runs them as two launches (A/B measurements)
-SHUFFLE_CONV_ENABLED = os.environ.get("ESM_SHUFFLE_CONV", "1") != "0"
-# largest low-resolution input (B * H * W) it is used on.  Round 3: faster than the two launches at S-K's
-# 2x stage (24x78 in: 8.4 vs 10.5 us), slower at the 4x stage (96x312 in: 23.2 vs 20.8 us) with the
-# window form; round 4 adds the row form there (shuffle_conv4_kernel)
-SHUFFLE_CONV_MAX_PIX = int(os.environ.get("ESM_SHUFFLE_CONV_MAXPIX", str(1 << 30)))
+SHUFFLE_CONV_ENABLED = _ab("ESM_SHUFFLE_CONV", "1") != "0"
+# largest low-resolution input (B * H * W) the window form is used on.  Round 3: faster than the two launches
+# at S-K's 2x stage (24x78 in: 8.4 vs 10.5 us), slower at the 4x stage (96x312 in: 23.2 vs 20.8 us).  The
+# row form (shuffle_conv4_kernel, nf 8, r 4, C 16 only; round 4) has no cap: it won at the 4x stage.  Heads
+# without a row form (L's nf 16) keep the cap (at L-K B=4 the fused window form took 145.8 us
+# against 116.3 + 26.8 us as two launches).
+SHUFFLE_CONV_MAX_PIX = int(_ab("ESM_SHUFFLE_CONV_MAXPIX", "8192"))
 
 
 def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[torch.Tensor] = None) -> bool:
-    if x is not None and int(x.shape[0]) * int(x.shape[2]) * int(x.shape[3]) > SHUFFLE_CONV_MAX_PIX:
+    row_form = (p.nf, p.r, conv.cout) == (8, 4, 16)
+    if x is not None and not row_form and int(x.shape[0]) * int(x.shape[2]) * int(x.shape[3]) > SHUFFLE_CONV_MAX_PIX:
         return False
     return SHUFFLE_CONV_ENABLED and (p.nf, p.r, conv.cout) in ((8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)) and \
         conv.nd == 2 and not conv.transposed and (conv.k, conv.stride, conv.pad, conv.cin) == (3, 2, 1, 1) and \
@@ -908,7 +921,7 @@ def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[t
 
 # the upsampler stage's spx_<t>[1] computed inside the row-form shuffle_conv launch (ESM_SHUFFLE_PRE=0: its own
 # launch, A/B measurements)
-SHUFFLE_PRE_ENABLED = os.environ.get("ESM_SHUFFLE_PRE", "1") != "0"
+SHUFFLE_PRE_ENABLED = _ab("ESM_SHUFFLE_PRE", "1") != "0"
 
 
 def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: PackedConv) -> bool:

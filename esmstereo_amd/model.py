@@ -148,6 +148,9 @@ class HotPath:
         self._arena_span = (arena.data_ptr(), arena.data_ptr() + arena.numel())
         self._own = [self.ml, self.mr, self.att] + list(self.up)    # the plan's own input buffers
         self._bound = [None if t is None else t.data_ptr() for t in self._own]  # what the plan reads now
+        # slots whose caller pointer changed while the previous replay was still running: they are copied
+        # into the plan's own buffer from then on (stream-ordered, no host wait)
+        self._copy_mode = [False] * len(self._own)
 
     def _emit(self, ctx: Ctx, model, B, h, w, att_ch, up_shapes, train_status, channels) -> None:
         e = ctx.empty
@@ -209,17 +212,19 @@ class HotPath:
         return not (lo < a_hi and a_lo < hi)
 
     def _rebind(self, ptrs: Sequence[Optional[int]]) -> None:
-        olds, sizes, news = [], [], []
+        olds, sizes, news, idx = [], [], [], []
         for i, p in enumerate(ptrs):
             if p is not None and p != self._bound[i]:
                 olds.append(self._bound[i])
                 sizes.append(4 * self._own[i].numel())
                 news.append(p)
-                self._bound[i] = p
+                idx.append(i)
         if olds:
             n = len(olds)
             check(lib.esm_plan_rebind(self.ctx.plan, n, (_lib.c_void_p * n)(*olds), (ctypes.c_uint64 * n)(*sizes),
                                       (_lib.c_void_p * n)(*news)), "plan_rebind")
+            for i, p in zip(idx, news):  # only once the native side has moved them
+                self._bound[i] = p
 
     def bind(self, ml, mr, att, up) -> None:
         """Point the plan at the caller's tensors (zero-copy; models/ESMStereo.py:700-745 reads its
@@ -228,8 +233,16 @@ class HotPath:
         plan's own buffer instead.  The plan keeps no reference: the caller keeps the tensors alive
         until the launch that reads them has run (stream order, as for any PyTorch op).  When the
         pointers are the ones already bound (a serving loop whose allocator hands back the same
-        blocks), nothing happens; otherwise the graph's affected nodes are updated in place."""
-        ptrs = []
+        blocks), nothing happens; otherwise the graph's affected nodes are updated in place.
+
+        Two slots never read overlapping memory through a binding: a tensor that overlaps another
+        slot's tensor of the same call (``hot_path(x, x, ...)``) is copied into its slot's own buffer,
+        so every bound range belongs to exactly one slot and a later rebind moves each pointer to the
+        right tensor.  A slot whose pointer changes while the previous replay is still
+        running (a caller handing over fresh tensors every step) switches to copies for good: a rebind
+        would make the host wait for the device."""
+        busy = None
+        ptrs, spans = [], []
         for i, (t, own) in enumerate(zip(self._slots(ml, mr, att, up), self._own)):
             if own is None:
                 ptrs.append(None)
@@ -237,10 +250,20 @@ class HotPath:
             require_device(t, "hot-path input")
             if tuple(t.shape) != tuple(own.shape):
                 raise ValueError(f"hot path input {i}: shape {tuple(t.shape)}, plan built for {tuple(own.shape)}")
-            if not self._in_place_ok(i, t):
+            copy = self._copy_mode[i] or not self._in_place_ok(i, t)
+            if not copy:
+                lo, hi = t.data_ptr(), t.data_ptr() + 4 * t.numel()
+                copy = any(lo < b and a < hi for a, b in spans)  # aliases an earlier slot of this call
+            if not copy and t.data_ptr() != self._bound[i]:
+                if busy is None:
+                    busy = check(lib.esm_plan_busy(self.ctx.plan), "plan_busy") > 0
+                if busy:
+                    self._copy_mode[i] = copy = True
+            if copy and t.data_ptr() != own.data_ptr():
                 own.copy_(t)
                 t = own
             ptrs.append(t.data_ptr())
+            spans.append((t.data_ptr(), t.data_ptr() + 4 * t.numel()))
         self._rebind(ptrs)
 
     def load_inputs(self, ml, mr, att, up) -> None:
@@ -319,7 +342,8 @@ class ESMStereo(nn.Module):
         for name, mod in self.named_modules():  # launch names for profiles / the bench probe
             object.__setattr__(mod, "_esm_name", name)
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
-        self.use_graph = os.environ.get("ESM_GRAPH", "1") != "0"
+        # ESM_GRAPH=0 replays the plan eagerly (A/B measurements; read only with ESM_AB=1)
+        self.use_graph = not (os.environ.get("ESM_AB") == "1" and os.environ.get("ESM_GRAPH", "1") == "0")
 
     # ------------------------------------------------------------------ plan cache
     def invalidate_plans(self) -> None:

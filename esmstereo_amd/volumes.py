@@ -80,6 +80,25 @@ def disparity_regression(x: torch.Tensor, maxdisp: int) -> torch.Tensor:
     return out
 
 
+def _gather_samples(s: torch.Tensor, B: int, D: int, H: int, W: int) -> torch.Tensor:
+    """The block of ``disparity_samples`` the reference's ``torch.gather(disparity_samples, 1, pool_ind)``
+    (submodule.py:223) reads, with gather's failure class: no broadcasting (a 4-D tensor at least
+    [B, ., H, W] in the non-gathered dims, else ``RuntimeError: Size does not match at dimension ...``),
+    and every selected index must lie inside dim 1 (an index past it raises ``index ... is out of bounds``;
+    here whenever dim 1 is shorter than D, since any of the D planes may be selected)."""
+    require_device(s, "disparity_samples")
+    if s.dim() != 4:
+        raise RuntimeError("Index tensor must have the same number of dimensions as input tensor "
+                           f"(disparity_samples {tuple(s.shape)}, index [B, k, H, W])")
+    for d, n in ((0, B), (2, H), (3, W)):
+        if int(s.shape[d]) < n:
+            raise RuntimeError(f"Size does not match at dimension {d} expected index [{B}, k, {H}, {W}] to be "
+                               f"smaller than self {list(s.shape)} apart from dimension 1")
+    if int(s.shape[1]) < D:
+        raise RuntimeError(f"index {D - 1} is out of bounds for dimension 1 with size {int(s.shape[1])}")
+    return s[:B, :D, :H, :W].contiguous()
+
+
 def regression_topk(cost: torch.Tensor, disparity_samples: torch.Tensor, k: int) -> torch.Tensor:
     """``regression_topk`` (submodule.py:218-225) -> [B, 1, H, W]: the top-k costs over D (value
     descending; ties -> lowest index, NaN first), softmax over them, the probability-weighted sum of
@@ -97,7 +116,6 @@ def regression_topk(cost: torch.Tensor, disparity_samples: torch.Tensor, k: int)
     cost = cost.contiguous()
     samples = None
     if disparity_samples is not None:
-        require_device(disparity_samples, "disparity_samples")
-        samples = disparity_samples.expand(B, D, H, W).contiguous()
+        samples = _gather_samples(disparity_samples, B, D, H, W)
     Ctx(cost.device).regression(1, cost, out, B, D, H, W, samples=samples, k=ke)
     return out

@@ -376,9 +376,15 @@ int esm_plan_graph_launch(esm_plan* plan, void* stream);
  * reference forward's behaviour, models/ESMStereo.py:700-745).  With a built graph, the nodes of the
  * ops that changed are updated in place (after the previous replay has finished); when an op's
  * kernel choice changes with its pointers, the graph is dropped and rebuilt by the next launch.
- * Returns the number of pointer fields moved, or an error. */
+ * Returns the number of pointer fields moved, or an error: ESM_ERR_ARG when two old ranges overlap
+ * (which range a pointer belongs to would be ambiguous; bind aliased inputs through copies).  When
+ * waiting for the previous replay fails, the ops are already moved and the graph is dropped (rebuilt
+ * from the moved ops by the next launch). */
 int esm_plan_rebind(esm_plan* plan, int n, const void* const* old_base, const uint64_t* bytes,
                     const void* const* new_base);
+/* 1 while the last graph replay of the plan may still be running on the device (a rebind would then
+ * wait for it), 0 when it has finished or the plan was never launched as a graph; < 0 on error. */
+int esm_plan_busy(esm_plan* plan);
 /* Probe: record a hipEvent pair around op `index` on every run/replay (ring of `ring`
  * pairs, ring <= 4096).  esm_plan_probe_read returns the elapsed ms of the completed
  * runs since the last read (caller synchronises first); returns the count written. */

@@ -93,7 +93,7 @@ def regression_topk(cost: torch.Tensor, disparity_samples, k: int) -> torch.Tens
     if disparity_samples is None:
         samples = idx.to(cost.dtype)
     else:
-        samples = torch.gather(disparity_samples.expand_as(cost), 1, idx)
+        samples = torch.gather(disparity_samples, 1, idx)  # no broadcasting: gather's own failure class
     prob = F.softmax(torch.gather(cost, 1, idx), 1)
     return torch.sum(samples * prob, dim=1, keepdim=True)
 

@@ -18,6 +18,7 @@ import os
 import sys
 import time
 
+os.environ.setdefault("ESM_AB", "1")  # the package reads A/B knobs only with ESM_AB=1
 os.environ.setdefault("ESM_NO_TUNED", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)

@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
+os.environ.setdefault("ESM_AB", "1")  # the package reads A/B knobs only with ESM_AB=1
 import torch  # noqa: E402
 
 import bench  # noqa: E402

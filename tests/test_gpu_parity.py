@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from helpers import GOLDEN_DIR, feature_pair, load_golden, load_spec, seeded_state, stereo_pair
-from parity import check_fullsize, flip_masked, fullsize_case, fullsize_manifest, top2_sets
+from parity import check_fullsize, flip_masked, fullsize_case, fullsize_manifest, record_report, top2_sets
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a ROCm GPU")]
 
@@ -140,10 +140,22 @@ def test_regressions_vs_oracle():
     cost[0, 5, 0, :4] = cost[0, 9, 0, :4] = 10.0  # exact ties -> lowest index first
     out = E.disparity_regression(cost.to(DEV), 48)
     assert rel(out, O.disparity_regression(cost, 48)) < 1e-6
-    t = E.regression_topk(cost.to(DEV), torch.arange(48, dtype=torch.float32, device=DEV).view(1, 48, 1, 1), 2)
+    full = torch.arange(48, dtype=torch.float32).view(1, 48, 1, 1).repeat(2, 1, 17, 33)  # as ESMStereo.py:719-720
+    t = E.regression_topk(cost.to(DEV), full.to(DEV), 2)
     assert rel(t, O.regression_topk2(cost)) < 1e-6
+    assert rel(t, O.regression_topk(cost, full, 2)) < 1e-6
+    big = torch.rand(3, 50, 18, 35, generator=g) * 48  # larger than the index: gather reads its corner block
+    t = E.regression_topk(cost.to(DEV), big.to(DEV), 2)
+    assert rel(t, O.regression_topk(cost, big, 2)) < 1e-6
     with pytest.raises(RuntimeError):
         E.disparity_regression(cost.to(DEV), 47)
+    # the reference's torch.gather(disparity_samples, 1, pool_ind) does not broadcast (submodule.py:223):
+    # a [1, D, 1, 1] sample vector raises there, and here
+    for bad in (full[:, :, :1, :1], full[:1], full[0], full[:, :40]):
+        with pytest.raises(RuntimeError):
+            O.regression_topk(cost, bad, 2)
+        with pytest.raises(RuntimeError):
+            E.regression_topk(cost.to(DEV), bad.contiguous().to(DEV), 2)
 
 
 # ----------------------------------------------------------------------------- convs
@@ -1031,6 +1043,8 @@ def test_hot_path_fullsize_vs_reference(name):
         d_ref_init = E.engine.eager_emit(DEV, model.upsample_module.emit, up, cu(g["init_pred"]), final_scale=4.0)[0]
     rep = check_fullsize(name, m, g, cost, init.view(m["B"], 1, *cost.shape[-2:]), disp0,
                          disp0_from_ref_init=d_ref_init[:, 0])
+    record_report(name, dict(rep, workload=f"ESMStereo-{m['variant']} {m['cv']} B{m['B']} "
+                                           f"{m.get('H', '')}x{m.get('W', '')} md{m['maxdisp']}"))
     print(name, rep)
 
 
@@ -1121,6 +1135,13 @@ def test_hot_path_reads_inputs_in_place(graph):
             assert torch.equal(out, expect(ml2, mr2, att, up2)), name
             out = model.hot_path(mr2, ml2, att, up2)[0]  # swapped
             assert torch.equal(out, expect(mr2, ml2, att, up2)), name
+            out = model.hot_path(ml2, ml2, att, up2)[0]  # aliased: one tensor in two slots
+            assert torch.equal(out, expect(ml2, ml2, att, up2)), name
+            out = model.hot_path(ml2, mr2, att, up2)[0]  # distinct again: each slot reads its own tensor
+            assert torch.equal(out, expect(ml2, mr2, att, up2)), name
+            ml3 = ml2 * 0.75
+            out = model.hot_path(ml3, mr2, att, up2)[0]  # only ml moves after the aliased call
+            assert torch.equal(out, expect(ml3, mr2, att, up2)), name
             u0 = up2[0]
             wide = torch.zeros((u0.shape[0], 2 * u0.shape[1]) + tuple(u0.shape[2:]), device=DEV)
             wide[:, 1::2] = u0
@@ -1130,6 +1151,37 @@ def test_hot_path_reads_inputs_in_place(graph):
             out = model.hot_path(ml, mr, att, up)[0]  # and back in place
             assert torch.equal(out, first), name
         ref_hp.close()
+
+
+def test_hot_path_rebind_while_replay_runs():
+    """A slot whose caller pointer changes while the previous replay is still running switches to
+    copies into the plan's own buffer (no host wait for the device), and stays correct:
+    fresh tensors, then the same tensor edited in place."""
+    model, sd, m = _model_from_manifest("hot_S_gwc.npz")
+    g = load_golden("hot_S_gwc.npz")
+    ml, mr, att = cu(g["match_left"]), cu(g["match_right"]), cu(g["att"])
+    up = [cu(g[f"up_{i}"]) for i in range(4)]
+    B, C, h, w = ml.shape
+    ref_hp = E.HotPath(model, B, h, w, int(att.shape[1]), [tuple(u.shape) for u in up], DEV, graph=False)
+
+    def expect(a, b, at, u):
+        ref_hp.load_inputs(a, b, at, u)
+        ref_hp.launch()
+        return ref_hp.outputs[0].clone()
+
+    with torch.no_grad():
+        model.hot_path(ml, mr, att, up)
+        hp = list(model._plans.values())[-1]
+        for _ in range(300):  # a queue of replays: the next bind finds the plan busy
+            hp.launch()
+        ml3 = ml * 1.25
+        out = model.hot_path(ml3, mr, att, up)[0]
+        assert hp._copy_mode[0] and hp._bound[0] == hp._own[0].data_ptr()
+        assert torch.equal(out, expect(ml3, mr, att, up))
+        ml3.mul_(0.5)
+        out = model.hot_path(ml3, mr, att, up)[0]
+        assert torch.equal(out, expect(ml3, mr, att, up))
+    ref_hp.close()
 
 
 def test_expected_raises():

@@ -49,6 +49,25 @@ def test_error_path_without_gpu():
     assert _lib.lib.esm_conv_f32(ctypes.byref(d), None) == -1
 
 
+def test_plan_rebind_rejects_overlapping_ranges_without_gpu():
+    """two old ranges that overlap would make the owner of a pointer ambiguous; the native
+    rebind refuses them before touching any op (no device call: an empty plan)."""
+    lib = _lib.lib
+    plan = lib.esm_plan_create()
+    try:
+        n = 2
+        olds = (_lib.c_void_p * n)(0x10000, 0x10100)
+        sizes = (ctypes.c_uint64 * n)(0x200, 0x200)
+        news = (_lib.c_void_p * n)(0x90000, 0xa0000)
+        assert lib.esm_plan_rebind(plan, n, olds, sizes, news) == -1
+        assert b"overlap" in lib.esm_last_error()
+        olds = (_lib.c_void_p * n)(0x10000, 0x10200)  # adjacent, disjoint: accepted (nothing to move)
+        assert lib.esm_plan_rebind(plan, n, olds, sizes, news) == 0
+        assert lib.esm_plan_busy(plan) == 0  # never launched
+    finally:
+        lib.esm_plan_destroy(plan)
+
+
 def _emulate_packed(x, P, transposed, k, s, p):
     """Reference-free emulation of the kernel's K-loop indexing on the CPU (3-D, float64)."""
     B, Cin, Di, Hi, Wi = x.shape
