@@ -1,14 +1,17 @@
 #!/bin/bash
-# Round-4 closing evidence on the final tree: every GPU test, smoke(), the default bench line, the S-K
+# Closing evidence on the final tree: every GPU test, smoke(), the default bench line, the S-K
 # op map + PMC traffic, the configs[2] / [3] / [4] bench lines, the L-K B = 4 op map + PMC traffic.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash scripts/gpu_r04.sh all || exit 1
+bash scripts/gpu_round.sh all || exit 1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
-for c in 3 2 4; do
-  timeout -k 10 600 python -u bench.py --config $c --steps 10 --warmup 3 --no-extra --no-cpu-baseline \
+# configs[2] / [4] with the side measurements (EPE vs the reference fixtures) and a bounded CPU baseline;
+# configs[3] (32 pairs on one GPU, the 8-rank job's global batch) without them
+for c in 2 4 3; do
+  extra=""; [ $c = 3 ] && extra="--no-extra --no-cpu-baseline"
+  timeout -k 10 600 python -u bench.py --config $c --steps 10 --warmup 3 $extra \
       > gpurun_out/bench_c$c.log 2>&1 || { tail -20 gpurun_out/bench_c$c.log; exit 1; }
   tail -1 gpurun_out/bench_c$c.log | cut -c1-160
 done

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 evidence on the current tree: every GPU test, the default bench line (all side
+# Evidence on the current tree: every GPU test, the default bench line (all side
 # measurements), then rocprofv3 kernel stats + op map + PMC traffic of the S-K step.
-# Usage: bash scripts/gpu_r04.sh [tests|bench|prof|all]  (default all)
+# Usage: bash scripts/gpu_round.sh [tests|bench|prof|all]  (default all)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
