@@ -441,6 +441,16 @@ def forward_e2e(model, args, dev, iters: int = 10) -> dict:
             model(left, right, False)
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / iters
+        model.capture_forward = False  # the backbone side eagerly (each launch from the host), for comparison
+        for _ in range(2):
+            model(left, right, False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model(left, right, False)
+        torch.cuda.synchronize()
+        el_eager = (time.perf_counter() - t0) / iters
+        model.capture_forward = True
         ml, mr, att, up = model.prefix(left, right)
         model.hot_path(ml, mr, att, up)
         torch.cuda.synchronize()
@@ -452,8 +462,11 @@ def forward_e2e(model, args, dev, iters: int = 10) -> dict:
         torch.cuda.synchronize()
         hp_ms = (time.perf_counter() - t0) / hp_iters * 1e3
     return {"value": round(args.batch / el, 2), "unit": "pairs/s", "ms_per_forward": round(el * 1e3, 3),
+            "ms_per_forward_eager_backbone": round(el_eager * 1e3, 3),
             "hot_path_call_ms": round(hp_ms, 4), "hot_path_host_us": round(t_host / hp_iters * 1e6, 1),
-            "what": f"model(left, right, False) with the random-init backbone; hot_path_call_ms = one "
+            "what": f"model(left, right, False) with the random-init backbone, replayed from the captured "
+                    f"whole-forward graphs (model.ForwardGraph; ms_per_forward_eager_backbone: the backbone side "
+                    f"launched eagerly instead); hot_path_call_ms = one "
                     f"model.hot_path() call on resident features ({hp_iters} back to back), host work included "
                     f"(plan key, binding, graph launch, output clone); hot_path_host_us = its host time alone"}
 

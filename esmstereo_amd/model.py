@@ -83,21 +83,23 @@ class FeatUp(nn.Module):
                 m.weight.data.fill_(1)
                 m.bias.data.zero_()
 
+    def one(self, feats):
+        """The neck on one feature list (both images at once when the pyramid is batched [left; right]:
+        every op is per sample, so this equals the reference's two passes)."""
+        x2, x4, x8, x16, x32 = feats
+        x16 = self.deconv32_16(x32, x16)
+        if self.v == 16:
+            x16 = self.conv16(x16)
+        if self.v in (8, 4):
+            x8 = self.deconv16_8(x16, x8)
+        if self.v == 8:
+            x8 = self.conv8(x8)
+        if self.v == 4:
+            x4 = self.conv4(self.deconv8_4(x8, x4))
+        return [x4, x8, x16, x32]
+
     def forward(self, featL, featR):
-        outs = []
-        for feats in (featL, featR):
-            x2, x4, x8, x16, x32 = feats
-            x16 = self.deconv32_16(x32, x16)
-            if self.v == 16:
-                x16 = self.conv16(x16)
-            if self.v in (8, 4):
-                x8 = self.deconv16_8(x16, x8)
-            if self.v == 8:
-                x8 = self.conv8(x8)
-            if self.v == 4:
-                x4 = self.conv4(self.deconv8_4(x8, x4))
-            outs.append([x4, x8, x16, x32])
-        return outs[0], outs[1]
+        return self.one(featL), self.one(featR)
 
 
 def _stem(cin: int, c: int) -> nn.Sequential:
@@ -282,6 +284,53 @@ class HotPath:
         self.ctx.close()
 
 
+class ForwardGraph:
+    """The whole eval forward (reference ``models/ESMStereo.py:638-745``) for one input shape, replayed
+    without host work per launch:
+
+    * the backbone side (:meth:`ESMStereo.prefix`: the timm-layout feature pyramid on MIOpen, the neck, the
+      stems and the matching descriptor, whose ``BasicConv``s run the HIP conv kernels) is captured once
+      into a torch CUDA graph (hipGraph) over static image buffers; its outputs then live at fixed
+      addresses in the graph's memory pool;
+    * the hot path's own plan (:class:`HotPath`) is bound zero-copy to those outputs and replayed as its
+      hipGraph right behind it, on the same stream.
+
+    ``run(left, right)`` copies the images into the static buffers, replays both graphs and returns fresh
+    output tensors (the reference returns new tensors).  Captured after two eager warm-up passes on a side
+    stream (MIOpen's algorithm choice and every lazily packed weight settle there, as torch's capture rules
+    require)."""
+
+    def __init__(self, model: "ESMStereo", left: torch.Tensor, right: torch.Tensor, train_status: bool):
+        self.device = left.device
+        self.left, self.right = left.clone(), right.clone()
+        cur = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                ml, mr, att, up = model.prefix(self.left, self.right)
+        cur.wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.ml, self.mr, self.att, self.up = model.prefix(self.left, self.right)
+        self.hp = HotPath(model, int(self.ml.shape[0]), int(self.ml.shape[2]), int(self.ml.shape[3]),
+                          0 if self.att is None else int(self.att.shape[1]), [tuple(u.shape) for u in self.up],
+                          self.device, train_status, graph=True, channels=int(self.ml.shape[1]))
+        self.hp.bind(self.ml, self.mr, self.att, self.up)
+
+    def run(self, left: torch.Tensor, right: torch.Tensor) -> List[torch.Tensor]:
+        self.left.copy_(left)
+        self.right.copy_(right)
+        self.graph.replay()
+        self.hp.launch()
+        return [o.clone() for o in self.hp.outputs]
+
+    def close(self) -> None:
+        self.hp.close()
+        self.graph.reset()
+
+
 def plan_ops(model: "ESMStereo", B: int, h: int, w: int, att_ch: int, up_shapes: Sequence[Tuple[int, ...]],
              train_status: bool = False, channels: int = 64) -> List[dict]:
     """The launch list the hot path compiles to for these input shapes, one dict per launch (name,
@@ -344,6 +393,9 @@ class ESMStereo(nn.Module):
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
         # ESM_GRAPH=0 replays the plan eagerly (A/B measurements; read only with ESM_AB=1)
         self.use_graph = not (os.environ.get("ESM_AB") == "1" and os.environ.get("ESM_GRAPH", "1") == "0")
+        # the whole eval forward (backbone side + hot path) replayed from captured graphs (ForwardGraph);
+        # False runs the backbone side eagerly and only the hot path from its plan's graph
+        self.capture_forward = True
 
     # ------------------------------------------------------------------ plan cache
     def invalidate_plans(self) -> None:
@@ -353,6 +405,10 @@ class ESMStereo(nn.Module):
         for hp in self._plans.values():
             hp.close()
         self._plans.clear()
+        for fg in self.__dict__.get("_fwd_graphs", {}).values():
+            fg.close()
+        self.__dict__["_fwd_graphs"] = collections.OrderedDict()
+        self.__dict__["_all_state"] = None
         self.__dict__["_hot_dicts"] = None
         self.__dict__["_hot_state"] = None
 
@@ -390,6 +446,17 @@ class ESMStereo(nn.Module):
             self.__dict__["_hot_state"] = st
         return st[2], sum(map(_VERSION, st[1]))
 
+    def _all_param_token(self) -> tuple:
+        """As :meth:`_hot_param_token` over EVERY parameter and buffer (the backbone side included): the
+        key of the captured whole-forward graphs."""
+        ep = _REG_EPOCH[0]
+        st = self.__dict__.get("_all_state")
+        if st is None or st[0] != ep:
+            ts = [t for t in itertools.chain(self.parameters(), self.buffers())]
+            st = (ep, ts, hash(tuple(map(id, ts))))
+            self.__dict__["_all_state"] = st
+        return st[2], sum(map(_VERSION, st[1]))
+
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self.invalidate_plans()
         # Warn when a checkpoint supplied hot-path weights but no usable backbone weight: every
@@ -415,19 +482,25 @@ class ESMStereo(nn.Module):
         return self._prefix(left, right)[:4]
 
     def _prefix(self, left: torch.Tensor, right: torch.Tensor):
+        """The backbone side with left and right as ONE batch [left; right] (eval BatchNorm and every other
+        op are per sample, so each half equals the reference's separate left / right passes, :640-697):
+        every backbone launch covers both images, half the launches of the reference's order."""
         vs = self.vol_size
-        fl = self.feature(left)
-        fr = self.feature(right)
+        B = int(left.shape[0])
+        if tuple(left.shape) != tuple(right.shape):
+            raise RuntimeError(f"left {tuple(left.shape)} and right {tuple(right.shape)} image sizes differ")
+        both = torch.cat((left, right), 0)
+        f = self.feature(both)
         if vs in (4, 8):
-            fl, fr = self.feature_up(fl, fr)
-        sx, sy = self.stem_2(left), self.stem_2(right)
-        stems_x, stems_y = [sx], [sy]
+            f = self.feature_up.one(f)
+        stems = [self.stem_2(both)]
         for name, _, _ in _STEMS[vs][1:]:
-            stems_x.append(getattr(self, name)(stems_x[-1]))
-            stems_y.append(getattr(self, name)(stems_y[-1]))
+            stems.append(getattr(self, name)(stems[-1]))
         idx = {4: 0, 8: 1, 16: 3}[vs]
-        ml = self.desc(self.conv(torch.cat((fl[idx], stems_x[-1]), 1)))
-        mr = self.desc(self.conv(torch.cat((fr[idx], stems_y[-1]), 1)))
+        m = self.desc(self.conv(torch.cat((f[idx], stems[-1]), 1)))
+        ml, mr = m[:B], m[B:]
+        fl = [t[:B] for t in f]
+        sx = stems[0][:B]
         att = self.semantic(fl[3]) if vs == 16 else None
         if vs == 4:
             up = [fl[1], fl[0], sx]
@@ -511,8 +584,24 @@ class ESMStereo(nn.Module):
         require_device(left, "left")
         require_device(right, "right")
         with torch.no_grad():
+            if self.use_graph and self.capture_forward:
+                return self._forward_graph(left, right, train_status)
             ml, mr, att, up = self.prefix(left, right)
             return self.hot_path(ml, mr, att, up, train_status)
+
+    def _forward_graph(self, left: torch.Tensor, right: torch.Tensor, train_status: bool) -> List[torch.Tensor]:
+        """The forward through a captured :class:`ForwardGraph` per (input shapes, weights)."""
+        key = (tuple(left.shape), tuple(right.shape), left.device, bool(train_status), self._all_param_token())
+        graphs = self.__dict__.setdefault("_fwd_graphs", collections.OrderedDict())
+        fg = graphs.get(key)
+        if fg is None:
+            fg = ForwardGraph(self, left, right, train_status)
+            graphs[key] = fg
+            while len(graphs) > 2:
+                graphs.popitem(last=False)[1].close()
+        else:
+            graphs.move_to_end(key)
+        return fg.run(left, right)
 
 
 class ESMStereo_trt(ESMStereo):

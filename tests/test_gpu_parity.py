@@ -950,6 +950,39 @@ def test_full_forward_golden(name):
     print(name, rep)
 
 
+@pytest.mark.parametrize("name", ["hot_S_gwc.npz", "hot_L_gwc.npz"])
+def test_forward_graph_matches_eager(name):
+    """The captured whole forward (model.ForwardGraph: the backbone side as a torch CUDA graph, the hot
+    path's plan bound to its outputs) against the same module with the backbone side launched eagerly:
+    bitwise, on the first images, on new images through the same captured graph, and after an in-place
+    edit of a BACKBONE weight (the capture is keyed by every parameter's version: re-captured)."""
+    model, sd, m = _model_from_manifest(name)
+    g = load_golden(name)
+    left, right = cu(g["left"]), cu(g["right"])
+
+    def both(a, b):
+        model.capture_forward = True
+        got = model(a, b, False)[0]
+        model.capture_forward = False
+        ref = model(a, b, False)[0]
+        model.capture_forward = True
+        return got, ref
+
+    with torch.no_grad():
+        got, ref = both(left, right)
+        assert torch.equal(got, ref), name
+        assert epe(got, g["disp_0"]) <= (1e-3 if m["cv_scale"] != 4 else 1.0)
+        fg = next(iter(model._fwd_graphs.values()))
+        got, ref = both(right.flip(-1).contiguous(), left.flip(-1).contiguous())  # new images, same graph
+        assert torch.equal(got, ref), name
+        assert next(iter(model._fwd_graphs.values())) is fg
+        w = next(p for n, p in model.named_parameters() if n.startswith("feature."))
+        w.mul_(1.5)  # in place: the captured backbone must not replay stale packed / cached state
+        got, ref = both(left, right)
+        assert torch.equal(got, ref), name
+        assert fg not in model._fwd_graphs.values()
+
+
 def test_trt_forward_equals_eval_output():
     """ESMStereo_trt.forward(left, right) -> disp [B, H, W] (models/ESMStereo_trt.py:638,735) is the
     eval output of ESMStereo on the same weights, and matches the reference golden."""
