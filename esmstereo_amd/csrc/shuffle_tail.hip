@@ -641,6 +641,19 @@ struct Sc4Geo {
     static constexpr int PNT = (LH * LW + 15) / 16;  // pre-conv N tiles (16 window pixels each)
 };
 
+#ifdef ESM_CONV_STAMPS
+// Diagnostic build only: s_memrealtime (100 MHz) of workgroup-thread 0 at each phase boundary of
+// shuffle_conv4_kernel, [workgroup][8] (esm_diag_sc4_stamps); never in the product library.
+__device__ unsigned long long sc4_stamps[4096 * 8];
+#define SC4_STAMP(k)                                                                                     \
+    do {                                                                                                 \
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);             \
+        if (threadIdx.x == 0 && wg_ < 4096) sc4_stamps[wg_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define SC4_STAMP(k) (void)0
+#endif
+
 template <int L, bool PRE>
 __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle_conv_desc d) {
     using G = Sc4Geo<L>;
@@ -663,6 +676,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
     const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
     const int Y0 = 4 * ly0, X0 = 4 * lx0;
     const float* xb = PRE ? nullptr : a.x + b * a.xb;
+    SC4_STAMP(0);
 
     // ---- stage (one round trip): every weight (head, tail, conv, BN) and the low-res window
     constexpr int WRN = (WN + NT - 1) / NT, XRN = (XN + NT - 1) / NT;
@@ -743,6 +757,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         for (int k = 0; k < PWR; ++k)
             if (tid + k * NT < G::PWN + G::PBN) pws[tid + k * NT] = rq[k];
         __syncthreads();
+        SC4_STAMP(1);
         // x = GELU(BN(conv3x3(pre_x))) on the low-res window (MFMA: M = the nf couts (rows 8..15 zero weights),
         // N = 16 window pixels, K = 16 channels x 9 taps), zero outside the image (the head's window padding)
         for (int nt = wave; nt < G::PNT; nt += NT / 64) {
@@ -775,6 +790,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         }
     }
     __syncthreads();
+    SC4_STAMP(2);
 
     // ---- shuffled interior (MFMA, as shuffle_tail4_kernel), rows 2 .. TR + 1
     {
@@ -823,6 +839,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         ring_value(c, 2 + q - k * TR, k == 0 ? 2 : (k == 1 ? 3 : 68));
     }
     __syncthreads();
+    SC4_STAMP(3);
 
     // ---- tail -> x in LDS: lane (g, n) of wave w -> x row Y0 + 4w + g, columns X0 + 4n .. + 3
     const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
@@ -864,6 +881,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         for (int j = 0; j < 4; ++j) o[j] = (oy < HO && ox + j < WO) ? acc[j] + tb : 0.f;  // the conv's zero padding
         *reinterpret_cast<conv::floatx4*>(&xs[1 + 4 * wave + g][4 + 4 * n]) = o;
     }
+    SC4_STAMP(4);
     // the x row above the tile (row 0, cols 3..67) and the column left of it (col 3, rows 1..TR): VALU
     for (int i = tid; i < 65 + TR; i += NT) {
         const int xr = i < 65 ? 0 : 1 + (i - 65), xc = i < 65 ? 3 + i : 3;
@@ -878,6 +896,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
         xs[xr][xc] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc + tb : 0.f;
     }
     __syncthreads();
+    SC4_STAMP(5);
 
     // ---- c1 = GELU(BN(conv 3x3 s2 p1 (x))): thread = one output pixel of the (2L) x 32 tile, all C channels
     {
@@ -903,6 +922,11 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
             conv::store_b32(__float_as_uint(v), ro, static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
         }
     }
+    SC4_STAMP(6);
+#ifdef ESM_CONV_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    SC4_STAMP(7);
+#endif
 }
 
 template <int L>
@@ -993,3 +1017,11 @@ extern "C" int esm_shuffle_tail_f32(const esm_shuffle_tail_desc* desc, void* str
 extern "C" int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream) {
     return esm::launch_shuffle_conv(desc, esm::as_stream(stream));
 }
+
+#ifdef ESM_CONV_STAMPS
+// Diagnostic build only: copy n <= 4096 * 8 shuffle_conv4 phase stamps to the host.
+extern "C" int esm_diag_sc4_stamps(unsigned long long* host, int n) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(esm::sc4_stamps), 8ull * n) == hipSuccess ? n : -1;
+}
+#endif
