@@ -929,6 +929,314 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
 #endif
 }
 
+// Round-5 form of the same launch (nf 8, r 4, C 16; st.flags bits 1-2 = 3): L-wave workgroups over L low-res
+// rows x 16 low-res pixels (L = 4: 480 workgroups at S-K's 96 x 312, 58 KB of LDS, two per CU), every phase
+// spread over all waves and the GEMM-shaped ones on the matrix cores:
+//   1. one round trip: the head / tail / conv weights (LDS), the pre-conv window (LDS) and every MFMA A
+//      operand (registers: the pre-conv's [tap][ci][co], the 1x1's [sub-pixel][c], the conv's [tap][co]);
+//   2. pre-conv (PRE): x = GELU(BN(conv3x3(pre_x))) on the (L + 2) x 18 low-res window, MFMA;
+//   3. the shuffled map SiLU(up(x)) on the WHOLE window by MFMA (its 1-pixel ring included: no VALU ring pass),
+//      rows Y0 - 2 .. Y0 + 4L kept;
+//   4. the 3x3 tail -> x rows Y0 - 1 .. Y0 + 4L - 1, cols X0 - 1 .. X0 + 63 (the row above and the column left
+//      of the tile that the stride-2 conv needs come out of the same pass), 2 rows x 4 columns per lane;
+//   5. c1 = GELU(BN(conv3x3 s2 (x))) as MFMA (M = 16 couts, N = 16 output pixels, K = 9 taps in 3 k-steps).
+// Arithmetic: the shuffled map and the tail as shuffle_conv4_kernel; the two convs sum their products in MFMA
+// k-step order (relative 1e-5 vs fp64, tests/test_gpu_parity.py test_shuffle_conv_*).
+template <int L>
+struct Sc5Geo {
+    static constexpr int NF = 8, C = 16, NT = 64 * L;
+    static constexpr int LH = L + 2, LW = 18, LP0 = LH * LW;           // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
+    static constexpr int LP = LP0 + ((16 - LP0 % 32) + 32) % 32;        // channel stride = 16 (mod 32) banks
+    static constexpr int LNT = (LP0 + 15) / 16;                         // window N-tiles
+    static constexpr int SR = 4 * L + 3, SC = 72;                       // shuffled map: row 0 = Y0 - 2, col 0 = X0 - 4
+    static constexpr int XR = 4 * L + 1;                                // x: row 0 = Y0 - 1, col 0 = X0 - 4
+    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = OW_TB + 1,
+                         OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, OW_PS = OW_SH + C, OW_PH = OW_PS + NF,
+                         WN = OW_PH + NF;
+    static constexpr int PR = L + 4, PW = 20, PCS0 = PR * PW;          // pre-conv window: rows ly0 - 2 .., cols lx0 - 2 ..
+    static constexpr int PCS = PCS0 + ((16 - PCS0 % 32) + 32) % 32, PXN = 16 * PCS;
+    static constexpr int POST = NF * SR * SC + XR * SC;                 // sh + xs
+    static constexpr int UN = POST > PXN ? POST : PXN;                  // the pre-conv window is dead once x is built
+    static constexpr int RP = (XR + 1) / 2, TQ = 17, TITEMS = RP * TQ;  // tail items: (row pair, column quad)
+};
+
+template <int L, bool PRE>
+__global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle_conv_desc d) {
+    using G = Sc5Geo<L>;
+    constexpr int NF = G::NF, C = G::C, NT = G::NT, LW = G::LW, LP = G::LP, LP0 = G::LP0, SR = G::SR, SC = G::SC;
+    constexpr int XR = G::XR, WN = G::WN;
+    const esm_shuffle_tail_desc& a = d.st;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ __attribute__((aligned(16))) float lr[NF * LP];
+    __shared__ __attribute__((aligned(16))) float un[G::UN];
+    float* const sh = un;                    // [NF][SR][SC]
+    float* const xs = un + NF * SR * SC;     // [XR][SC]
+    float* const pxs = un;                   // [16][PCS] (PRE, before the shuffled map is built)
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, HO = 4 * H, WO = 4 * W;
+    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
+    const int b = bk_.z;
+    const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
+    const int Y0 = 4 * ly0, X0 = 4 * lx0;
+
+    // ---- 1. stage (one round trip)
+    constexpr int WRN = (WN + NT - 1) / NT;
+    float rw[WRN];
+#pragma unroll
+    for (int k = 0; k < WRN; ++k) {
+        const int i = tid + k * NT;
+        const float* p;
+        int off;
+        float dflt = 0.f;
+        if (i < G::OW_UB) { p = a.up_w; off = i; }
+        else if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
+        else if (i < G::OW_TB) { p = a.tail_w; off = i - G::OW_TW; }
+        else if (i < G::OW_CW) { p = a.tail_b; off = 0; }
+        else if (i < G::OW_SC) { p = d.w; off = (i - G::OW_CW) / C * d.cin_pad * d.cout_pad + (i - G::OW_CW) % C; }
+        else if (i < G::OW_SH) { p = d.scale; off = i - G::OW_SC; dflt = 1.f; }
+        else if (i < G::OW_PS) { p = d.shift; off = i - G::OW_SH; }
+        else if (i < G::OW_PH) { p = PRE ? d.pre_scale : nullptr; off = i - G::OW_PS; dflt = 1.f; }
+        else { p = PRE ? d.pre_shift : nullptr; off = i - G::OW_PH; }
+        const bool ok = i < WN && p != nullptr;
+        const float v = (ok ? p : a.up_w)[ok ? off : 0];
+        rw[k] = ok ? v : dflt;
+    }
+    // MFMA A operands straight into registers.  1x1 up: A[m = sub-pixel][k = channel] of output channel c;
+    // c1: A[m = cout][k = tap 4s + g]; pre-conv: A[m = cout (8 .. 15 zero)][k = ci 4ks + g] of tap t
+    float ua[NF][2];
+#pragma unroll
+    for (int c = 0; c < NF; ++c)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ua[c][kk] = a.up_w[(c * 16 + n) * NF + 4 * kk + g];
+    float ca[3];
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3) {
+        const int t = 4 * s3 + g;
+        const float v = d.w[(t < 9 ? t : 0) * d.cin_pad * d.cout_pad + n];
+        ca[s3] = t < 9 ? v : 0.f;
+    }
+    constexpr int PXR = PRE ? (G::PXN + NT - 1) / NT : 1;
+    constexpr int XRN = PRE ? 1 : (NF * LP + NT - 1) / NT;
+    float pa[PRE ? 9 : 1][4];
+    float rp[PXR], rx[XRN];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int ci = 4 * ks + g;
+                const bool ok = ci < d.pre_cin && n < NF;
+                const float v = d.pre_w[ok ? (t * d.pre_cin_pad + ci) * d.pre_cout_pad + n : 0];
+                pa[t][ks] = ok ? v : 0.f;
+            }
+        const float* pb = d.pre_x + b * d.pb;
+#pragma unroll
+        for (int k = 0; k < PXR; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / G::PCS, rem = i - c * G::PCS;
+            const int yy = ly0 - 2 + rem / G::PW, xx = lx0 - 2 + rem % G::PW;
+            const bool ok = i < G::PXN && rem < G::PCS0 && c < d.pre_cin && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = pb[ok ? c * d.pc + yy * d.ph + xx : 0];
+            rp[k] = ok ? v : 0.f;
+        }
+    } else {
+        const float* xb = a.x + b * a.xb;
+#pragma unroll
+        for (int k = 0; k < XRN; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / LP, rem = i - c * LP;
+            const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
+            const bool ok = i < NF * LP && rem < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+            rx[k] = ok ? v : 0.f;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < WRN; ++k)
+        if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < PXR; ++k)
+            if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < XRN; ++k)
+            if (tid + k * NT < NF * LP) lr[tid + k * NT] = rx[k];
+    }
+    __syncthreads();
+
+    // ---- 2. pre-conv on the low-res window (MFMA: M = the nf couts, N = 16 window pixels, K = 16 ch x 9 taps)
+    if constexpr (PRE) {
+        for (int nt = wave; nt < G::LNT; nt += L) {
+            const int p = nt * 16 + n;
+            const int pp = p < LP0 ? p : 0;
+            const int py = pp / LW, px = pp - (pp / LW) * LW;
+            conv::floatx4 acc2[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int dy = t / 3, dx = t % 3;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks)
+                    acc2[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        pa[t][ks], pxs[(4 * ks + g) * G::PCS + (py + dy) * G::PW + px + dx], acc2[ks & 1], 0, 0, 0);
+            }
+            const conv::floatx4 acc = acc2[0] + acc2[1];
+            const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
+            const bool in = p < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            if (g < 2 && p < LP0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g + j;
+                    const float v = gelu_erf(acc[j] * wsh[G::OW_PS + co] + wsh[G::OW_PH + co]);
+                    lr[co * LP + p] = in ? v : 0.f;
+                }
+            }
+        }
+        __syncthreads();  // lr complete; the pre-conv window (aliased by the shuffled map) is dead
+    }
+
+    // ---- 3. shuffled map on the whole window (MFMA: M = the 16 sub-pixels of channel c, N = 16 window pixels,
+    //         K = the nf channels); lane (g, n): sub-row g, sub-columns 0..3 of window pixel n
+    for (int nt = wave; nt < G::LNT; nt += L) {
+        const int p = nt * 16 + n;
+        const int pp = p < LP0 ? p : 0;
+        const int py = pp / LW, px = pp - (pp / LW) * LW;
+        float bk[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) bk[kk] = lr[(4 * kk + g) * LP + pp];
+        const int row = 4 * py + g - 2;               // sh row (Y0 - 2 + row)
+        const int Y = Y0 - 2 + row, X = X0 - 4 + 4 * px;
+        const bool keep = p < LP0 && row >= 0 && row < SR;
+        const bool yok = Y >= 0 && Y < HO;
+#pragma unroll
+        for (int c = 0; c < NF; ++c) {
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[c][0], bk[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[c][1], bk[1], acc, 0, 0, 0);
+            conv::floatx4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
+                o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+            }
+            if (keep) *reinterpret_cast<conv::floatx4*>(&sh[(c * SR + row) * SC + 4 * px]) = o;
+        }
+    }
+    __syncthreads();
+
+    // ---- 4. tail -> x: lane item (row pair rp, column quad q): x rows 2rp, 2rp + 1, cols 4q .. 4q + 3
+    {
+        const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
+        for (int it = tid; it < G::TITEMS; it += NT) {
+            const int rp2 = it / G::TQ, q = it - (it / G::TQ) * G::TQ;
+            const int r0 = 2 * rp2;
+            float acc[2][4];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
+            const int cl = 4 * q - 1 < 0 ? 0 : 4 * q - 1;  // q = 0: only column 3 is used
+#pragma unroll 2
+            for (int c = 0; c < NF; ++c) {
+                float v[4][6];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int srow = r0 + rr < SR ? r0 + rr : SR - 1;
+                    const float* row = &sh[(c * SR + srow) * SC];
+                    const conv::floatx4 m4 = *reinterpret_cast<const conv::floatx4*>(row + 4 * q);
+                    v[rr][0] = row[cl];
+                    v[rr][1] = m4[0];
+                    v[rr][2] = m4[1];
+                    v[rr][3] = m4[2];
+                    v[rr][4] = m4[3];
+                    v[rr][5] = row[4 * q + 4];
+                }
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
+                        const f2v w2 = {w, w};
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                            const f2v lo = __builtin_elementwise_fma(w2, f2v{v[r + ky][kx], v[r + ky][1 + kx]}, f2v{acc[r][0], acc[r][1]});
+                            const f2v hi = __builtin_elementwise_fma(w2, f2v{v[r + ky][2 + kx], v[r + ky][3 + kx]}, f2v{acc[r][2], acc[r][3]});
+                            acc[r][0] = lo[0];
+                            acc[r][1] = lo[1];
+                            acc[r][2] = hi[0];
+                            acc[r][3] = hi[1];
+                        }
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (r0 + r >= XR) continue;
+                const int Y = Y0 - 1 + r0 + r;
+                conv::floatx4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int X = X0 - 4 + 4 * q + j;
+                    o[j] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc[r][j] + tb : 0.f;  // the conv's zero padding
+                }
+                *reinterpret_cast<conv::floatx4*>(&xs[(r0 + r) * SC + 4 * q]) = o;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 5. c1 = GELU(BN(conv 3x3 s2 p1 (x))) on the (2L) x 32 output tile: N-tile = 16 pixels of one output
+    //         row, lane (g, n): k-step s reads tap 4s + g of pixel n; C lane (g, n): couts 4g .. 4g + 3
+    {
+        const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            d.out + b * d.ob, static_cast<short>(0), static_cast<int>(4 * ((C - 1) * d.oc + (Ho2 - 1) * d.oh + Wo2)),
+            0x00020000);
+        float sc[4], shf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = wsh[G::OW_SC + 4 * g + j];
+            shf[j] = wsh[G::OW_SH + 4 * g + j];
+        }
+        for (int nt = wave; nt < 4 * L; nt += L) {
+            const int oyl = nt >> 1, oxl = 16 * (nt & 1) + n;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3) {
+                const int t = 4 * s3 + g;
+                const int tt = t < 9 ? t : 8;
+                const int ky = tt / 3, kx = tt - (tt / 3) * 3;
+                const float bv = xs[(2 * oyl + ky) * SC + 3 + 2 * oxl + kx];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[s3], t < 9 ? bv : 0.f, acc, 0, 0, 0);
+            }
+            const int oy = Y0 / 2 + oyl, ox = X0 / 2 + oxl;
+            const bool ok = oy < Ho2 && ox < Wo2;
+            const unsigned pix = 4u * static_cast<unsigned>(oy * d.oh + ox);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 4 * g + j;
+                const float v = gelu_erf(acc[j] * sc[j] + shf[j]);
+                conv::store_b32(__float_as_uint(v), ro,
+                                static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
+            }
+        }
+    }
+}
+
+template <int L>
+int launch_sc5(const esm_shuffle_conv_desc& a, hipStream_t s) {
+    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
+    if (a.pre_x)
+        hipLaunchKernelGGL((shuffle_conv5_kernel<L, true>), grid, dim3(64 * L), 0, s, a);
+    else
+        hipLaunchKernelGGL((shuffle_conv5_kernel<L, false>), grid, dim3(64 * L), 0, s, a);
+    return check_launch("shuffle_conv");
+}
+
 template <int L>
 int launch_sc4(const esm_shuffle_conv_desc& a, hipStream_t s) {
     const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
@@ -998,6 +1306,7 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
         const int form = (t.flags >> 1) & 3;
         const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
+        if (form == 3) return launch_sc5<4>(a, s);
         if (a.pre_x || form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
         return launch_sc<8, 4, 16>(a, s);
     }

@@ -919,6 +919,9 @@ def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[t
         conv.act == ACT_GELU
 
 
+# the (nf 8, r 4, C 16) head + conv form where the caller leaves the choice to the library (A/B knob: 1 window,
+# 2 shuffle_conv4_kernel, 3 shuffle_conv5_kernel; 0 = the library's rule)
+SC_FORM = int(_ab("ESM_SC_FORM", "0"))
 # the upsampler stage's spx_<t>[1] computed inside the row-form shuffle_conv launch (ESM_SHUFFLE_PRE=0: its own
 # launch, A/B measurements)
 SHUFFLE_PRE_ENABLED = _ab("ESM_SHUFFLE_PRE", "1") != "0"
@@ -936,11 +939,13 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
     3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
     stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)].  ``form`` (nf 8, r 4, C 16): 0
-    automatic, 1 the window form, 2 the row form.  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
+    automatic, 1 the window form, 2 the row form (8 low-res rows), 3 the round-5 row form (4 rows, MFMA convs).  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
     ``pre`` (the stage's spx_<t>[1], BasicConv(Cp, nf, 3, 1, 1)), computed inside the launch as well."""
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
+    if (p.nf, p.r, conv.cout) == (8, 4, 16) and form == 0 and SC_FORM:
+        form = SC_FORM
     if pre is not None:
         if not shuffle_conv_pre_supported(p, conv, pre):
             raise ValueError("shuffle_conv: unsupported pre-conv")
@@ -972,7 +977,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
         d.pre_cin, d.pre_cin_pad, d.pre_cout_pad = pre.cin, pre.cin_pad, pre.cout_pad
         require_on(x.device, "shuffle_conv pre-conv", pre.w, pre.scale, pre.shift)
         ctx.hold(pre.w, pre.scale, pre.shift)
-        form = 2
+        form = form if form == 3 else 2  # the row forms (2: shuffle_conv4_kernel, 3: shuffle_conv5_kernel)
     t.up_w, t.up_b, t.tail_w = p.up_w.data_ptr(), p.up_b.data_ptr(), p.tail_w.data_ptr()
     t.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
     t.out = None

@@ -699,7 +699,7 @@ def test_shuffle_conv_fused(nf, r, C, H, W):
     pc = pk(conv, bn, ACT_GELU)
     ctx = Ctx(DEV)
     two = run_conv(ctx, pc, [run_shuffle_tail(ctx, x.to(DEV), p)])
-    for form in ((0, 1, 2) if (nf, r) == (8, 4) else (0,)):  # (8, 4): the window and the row form
+    for form in ((0, 1, 2, 3) if (nf, r) == (8, 4) else (0,)):  # (8, 4): the window and both row forms
         y = run_shuffle_conv(ctx, x.to(DEV), p, pc, form=form)
         assert y.shape == ref.shape
         assert rel(y, ref) < 1e-5, form
@@ -725,11 +725,12 @@ def test_shuffle_conv_pre(cp, H, W):
     p = pack_shuffle_tail(copy.deepcopy(up).to(DEV), copy.deepcopy(tail).to(DEV), 4)
     pc, pp = pk(conv, bn, ACT_GELU), pk(pconv, pbn, ACT_GELU)
     ctx = Ctx(DEV)
-    y = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp)
-    assert y.shape == ref.shape
-    assert rel(y, ref) < 1e-5
     two = run_shuffle_conv(ctx, run_conv(ctx, pp, [c.to(DEV)]), p, pc, form=2)
-    assert rel(y, two) < 1e-5
+    for form in (2, 3):  # shuffle_conv4_kernel, shuffle_conv5_kernel
+        y = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp, form=form)
+        assert y.shape == ref.shape
+        assert rel(y, ref) < 1e-5, form
+        assert rel(y, two) < 1e-5, form
 
 
 PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones
