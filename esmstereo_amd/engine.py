@@ -919,8 +919,8 @@ def shuffle_conv_supported(p: PackedShuffleTail, conv: PackedConv, x: Optional[t
         conv.act == ACT_GELU
 
 
-# the (nf 8, r 4, C 16) head + conv form where the caller leaves the choice to the library (A/B knob: 1 window,
-# 2 shuffle_conv4_kernel, 3 shuffle_conv5_kernel; 0 = the library's rule)
+# the (nf 8, r 4, C 16) head + conv form with the pre-conv (the 4x stage) where the caller leaves the choice to the
+# library (A/B knob: 2 shuffle_conv4_kernel, 3 shuffle_conv5_kernel; 0 = the library's rule)
 SC_FORM = int(_ab("ESM_SC_FORM", "0"))
 # the upsampler stage's spx_<t>[1] computed inside the row-form shuffle_conv launch (ESM_SHUFFLE_PRE=0: its own
 # launch, A/B measurements)
@@ -944,7 +944,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
-    if (p.nf, p.r, conv.cout) == (8, 4, 16) and form == 0 and SC_FORM:
+    if (p.nf, p.r, conv.cout) == (8, 4, 16) and form == 0 and SC_FORM and pre is not None:
         form = SC_FORM
     if pre is not None:
         if not shuffle_conv_pre_supported(p, conv, pre):

@@ -595,6 +595,8 @@ class ESMStereo(nn.Module):
         graphs = self.__dict__.setdefault("_fwd_graphs", collections.OrderedDict())
         fg = graphs.get(key)
         if fg is None:
+            for k in [k for k in graphs if k[-1] != key[-1]]:  # captured under older weights: never hit again
+                graphs.pop(k).close()
             fg = ForwardGraph(self, left, right, train_status)
             graphs[key] = fg
             while len(graphs) > 2:

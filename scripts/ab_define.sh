@@ -10,7 +10,7 @@ objs=$(ls esmstereo_amd/_build/*.o)
 for f in $files; do
     b=$(basename "$f" .hip)
     hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wall -Wno-unused-result $defs -c "esmstereo_amd/csrc/$f" -o "$tmp/$b.o" &
-    objs=$(echo "$objs" | grep -v "/$b.o$")
+    objs=$(echo "$objs" | grep -v "/$b.o$" || true)
 done
 wait
 mkdir -p "$(dirname "$out")"
