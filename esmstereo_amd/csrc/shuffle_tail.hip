@@ -981,6 +981,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
     const int b = bk_.z;
     const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
     const int Y0 = 4 * ly0, X0 = 4 * lx0;
+    SC4_STAMP(0);
 
     // ---- 1. stage (one round trip)
     constexpr int WRN = (WN + NT - 1) / NT;
@@ -1068,6 +1069,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
             if (tid + k * NT < NF * LP) lr[tid + k * NT] = rx[k];
     }
     __syncthreads();
+    SC4_STAMP(1);
 
     // ---- 2. pre-conv on the low-res window (MFMA: M = the nf couts, N = 16 window pixels, K = 16 ch x 9 taps)
     if constexpr (PRE) {
@@ -1098,6 +1100,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
         }
         __syncthreads();  // lr complete; the pre-conv window (aliased by the shuffled map) is dead
     }
+    SC4_STAMP(2);
 
     // ---- 3. shuffled map on the whole window (MFMA: M = the 16 sub-pixels of channel c, N = 16 window pixels,
     //         K = the nf channels); lane (g, n): sub-row g, sub-columns 0..3 of window pixel n
@@ -1127,6 +1130,7 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
         }
     }
     __syncthreads();
+    SC4_STAMP(3);
 
     // ---- 4. tail -> x: lane item (row pair rp, column quad q): x rows 2rp, 2rp + 1, cols 4q .. 4q + 3
     {
@@ -1187,6 +1191,8 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
         }
     }
     __syncthreads();
+    SC4_STAMP(4);
+    SC4_STAMP(5);
 
     // ---- 5. c1 = GELU(BN(conv 3x3 s2 p1 (x))) on the (2L) x 32 output tile: N-tile = 16 pixels of one output
     //         row, lane (g, n): k-step s reads tap 4s + g of pixel n; C lane (g, n): couts 4g .. 4g + 3
@@ -1224,6 +1230,11 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv5_kernel(const esm_shuffle
             }
         }
     }
+    SC4_STAMP(6);
+#ifdef ESM_CONV_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    SC4_STAMP(7);
+#endif
 }
 
 template <int L>
@@ -1306,7 +1317,7 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
         const int form = (t.flags >> 1) & 3;
         const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
-        if (form == 3) return launch_sc5<4>(a, s);
+        if (form == 3) return (t.flags >> 3 & 1) ? launch_sc5<8>(a, s) : launch_sc5<4>(a, s);
         if (a.pre_x || form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
         return launch_sc<8, 4, 16>(a, s);
     }
