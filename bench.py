@@ -261,7 +261,8 @@ def concat_volume_roofline(device, reps: int = 6, B: int = 8, H: int = 136, W: i
     torch.cuda.empty_cache()
     return {"kernel": "concat_volume", "config": f"ESMStereo-L B={B} C=64 {H}x{W} D={D} (BASELINE configs[2])",
             "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2)}
+            "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": byts, "avg_us": round(avg * 1e3, 2),
+            "traffic": pmc_traffic("concat_volume", f"concat B{B} {H}x{W} D{D}")}
 
 
 def concurrent_streams(model, ml, mr, att, up, n: int, steps: int, warmup: int, device) -> dict:

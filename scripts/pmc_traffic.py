@@ -41,6 +41,27 @@ def per_dispatch(d: str, counter: str):
     return [vals[k] for k in order]
 
 
+def per_dispatch_named(d: str, counter: str):
+    """{kernel-name fragment in OURS: [per-dispatch value, in dispatch order]}."""
+    vals = defaultdict(float)
+    names = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] != counter:
+                    continue
+                frag = next((s for s in OURS if s in r["Kernel_Name"] and s != "esm::"), None)
+                if frag is None:
+                    continue
+                k = int(r["Dispatch_Id"])
+                vals[k] += float(r["Counter_Value"])
+                names[k] = frag
+    out = defaultdict(list)
+    for k in sorted(vals):
+        out[names[k]].append(vals[k])
+    return out
+
+
 def kernel_ops(ops) -> list:
     """Launch-list op index of each kernel dispatch of one step (an op may launch several kernels:
     ``launches`` in its table entry, e.g. the two-launch FMBlock)."""
