@@ -65,6 +65,7 @@ def summarize(fdir: str, wdir: str, table: str) -> dict:
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--summarize":
     print(json.dumps(summarize(*sys.argv[2:5]), indent=1))
 elif __name__ == "__main__":
+    bench._load_package()
     dev = torch.device("cuda", 0)
     out = {"gwc_L_K": bench.cost_volume_roofline(dev, reps=24),
            "gwc_configs2": bench.cost_volume_roofline(dev, reps=8, B=8, H=136, W=240, D=48),
