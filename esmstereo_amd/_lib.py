@@ -18,7 +18,7 @@ HEADER_PATH = os.path.join(ROOT, "include", "esmstereo_amd.h")
 MAX_SRC = 3
 SMIX_MAX_STAGES = 2
 
-ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU, ACT_SIGMOID, ACT_RELU6 = 0, 1, 2, 3, 4, 5
 CONF_COST_FEATURES, CONF_ATTEND, CONF_ENLARGE, CONF_COMBINE, CONF_SIGMOID = 1, 2, 3, 4, 5
 
 
@@ -88,6 +88,13 @@ class EsmConfDesc(Structure):
                 ("x", c_void_p * 4), ("out", c_void_p)]
 
 
+class EsmDwconvDesc(Structure):
+    _fields_ = [("x", c_void_p), ("xb", c_int64), ("xc", c_int64), ("xh", c_int64), ("w", c_void_p),
+                ("scale", c_void_p), ("shift", c_void_p), ("out", c_void_p), ("ob", c_int64), ("oc", c_int64),
+                ("oh", c_int64), ("B", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32), ("K", c_int32),
+                ("stride", c_int32), ("pad", c_int32), ("act", c_int32), ("Ho", c_int32), ("Wo", c_int32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/esmstereo_amd.h
 SIGNATURES = {
     "esm_last_error": (ctypes.c_char_p, []),
@@ -106,6 +113,7 @@ SIGNATURES = {
     "esm_shuffle_conv_f32": (c_int, [POINTER(EsmShuffleConvDesc), c_void_p]),
     "esm_conv_pair2_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
+    "esm_dwconv_f32": (c_int, [POINTER(EsmDwconvDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "esm_disp_to_u16": (c_int, [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "esm_node_filter_u16": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_float, c_void_p]),
@@ -152,7 +160,7 @@ def _load() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     for which, st in ((0, EsmSrc), (1, EsmConvDesc), (2, EsmSmixStage), (3, EsmSmixDesc), (4, EsmShuffleTailDesc),
-                      (5, EsmFmnetDesc), (6, EsmConfDesc), (8, EsmShuffleConvDesc)):
+                      (5, EsmFmnetDesc), (6, EsmConfDesc), (8, EsmShuffleConvDesc), (9, EsmDwconvDesc)):
         if lib.esm_struct_size(which) != ctypes.sizeof(st):
             raise ImportError(f"esmstereo_amd: ABI mismatch for {st.__name__}: "
                               f"C {lib.esm_struct_size(which)} vs ctypes {ctypes.sizeof(st)}")

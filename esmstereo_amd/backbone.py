@@ -29,7 +29,7 @@ so the golden tests construct ``ESMStereo(..., feature_cls=StubFeature)``; nothi
 from __future__ import annotations
 
 import math
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -203,6 +203,8 @@ class Feature(nn.Module):
         _he_init(self)
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
+        if fast_path_ok(self, x):
+            return fast_features(self, x)
         x = self.act1(self.bn1(self.conv_stem(x)))
         x2 = self.block0(x)
         x4 = self.block1(x2)
@@ -252,3 +254,86 @@ class StubFeature(nn.Module):
             x = stage(x)
             feats.append(x)
         return feats
+
+
+# ----------------------------------------------------------------------------- HIP inference path
+# The same blocks in eval mode with no autograd, launched on the HIP kernels of this package instead of MIOpen
+# (round 5): every dense conv (the stem, the 1x1 expand / project convs) through esm_conv_f32 with its
+# BatchNorm folded and the activation / residual in the epilogue, every depthwise conv through esm_dwconv_f32
+# with its BatchNorm and activation.  On PyTorch-ROCm these were MIOpen's naive grouped-conv kernel
+# (~55 us a launch at 192 x 624) plus separate BatchNorm and clamp kernels: 2.5 ms of the S-K forward's
+# backbone side.  SqueezeExcite (EfficientNet only) stays in torch ops on its [B, C, 1, 1] vectors.
+# Results agree with the modules' own forward to fp32 rounding (tests/test_gpu_backbone.py).
+
+
+def fast_path_ok(mod: nn.Module, x: torch.Tensor) -> bool:
+    return (not mod.training and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and x.dim() == 4)
+
+
+def _act_code(act: nn.Module) -> int:
+    from .engine import ACT_NONE, ACT_RELU, ACT_RELU6, ACT_SILU
+    if isinstance(act, nn.ReLU6):
+        return ACT_RELU6
+    if isinstance(act, nn.SiLU):
+        return ACT_SILU
+    if isinstance(act, nn.ReLU):
+        return ACT_RELU
+    if isinstance(act, nn.Identity):
+        return ACT_NONE
+    raise ValueError(f"backbone fast path: unsupported activation {act}")
+
+
+def _conv_bn(ctx, owner: nn.Module, name: str, conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor,
+             res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv (groups 1) -> BN(+act) as one esm_conv_f32 launch (BN folded into the epilogue)."""
+    from .engine import cached_pack, pack_conv, run_conv
+    act = _act_code(bn.act) if isinstance(bn, BatchNormAct2d) else 0
+    pc = cached_pack(owner, name, (conv, bn), lambda: pack_conv(conv, bn, act), act)
+    return run_conv(ctx, pc, [x], res=res, tag=name)
+
+
+def _dw_bn(ctx, owner: nn.Module, conv: nn.Conv2d, bn: "BatchNormAct2d", x: torch.Tensor) -> torch.Tensor:
+    """depthwise conv -> BN + act as one esm_dwconv_f32 launch."""
+    from .engine import bn_affine, cached_pack, run_dwconv
+    k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+    if conv.groups != conv.in_channels or conv.out_channels != conv.in_channels or conv.bias is not None:
+        raise ValueError("backbone fast path: expected a bias-free depthwise conv")
+
+    def build():
+        sc, sh = bn_affine(bn)
+        return conv.weight.detach().float().reshape(conv.out_channels, k * k).contiguous(), sc, sh
+
+    w, sc, sh = cached_pack(owner, "dw", (conv, bn), build)
+    return run_dwconv(ctx, x, w, sc, sh, k, s, p, _act_code(bn.act), tag="dw")
+
+
+def _se(se: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    if isinstance(se, nn.Identity):
+        return x
+    return se(x)
+
+
+def fast_features(feat: "Feature", x: torch.Tensor) -> List[torch.Tensor]:
+    """Feature.forward (models/ESMStereo.py:68-77) on the HIP kernels, eval mode."""
+    from .engine import Ctx
+    ctx = Ctx(x.device)
+    y = _conv_bn(ctx, feat, "stem", feat.conv_stem, feat.bn1, x)
+    if not isinstance(feat.bn1.act, nn.ReLU6):  # act1 = ReLU6 behind the model's own activation
+        y = y.clamp_(0.0, 6.0)
+    outs = []
+    for i in range(5):
+        for blk in getattr(feat, f"block{i}"):
+            for b in (blk if isinstance(blk, nn.Sequential) else [blk]):
+                inp = y
+                if isinstance(b, DepthwiseSeparableConv):
+                    y = _se(b.se, _dw_bn(ctx, b, b.conv_dw, b.bn1, y))
+                    y = _conv_bn(ctx, b, "pw", b.conv_pw, b.bn2, y, res=inp if b.has_skip else None)
+                elif isinstance(b, InvertedResidual):
+                    y = _conv_bn(ctx, b, "pw", b.conv_pw, b.bn1, y)
+                    y = _se(b.se, _dw_bn(ctx, b, b.conv_dw, b.bn2, y))
+                    y = _conv_bn(ctx, b, "pwl", b.conv_pwl, b.bn3, y, res=inp if b.has_skip else None)
+                else:
+                    y = b(y)
+        outs.append(y)
+    return outs

@@ -72,6 +72,8 @@ SCRATCH_OK = {
     "_ZN3esm4conv12dconv_kernelILb0ELi3ELi1ELb0ELi1ELi1ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
     "_ZN3esm4conv12dconv_kernelILb0ELi3ELi2ELb0ELi1ELi1ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
     "_ZN3esm4conv12dconv_kernelILb1ELi1ELi1ELb0ELi1ELi2ELi1ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb0ELi3ELi1ELb0ELi1ELi1ELi4ELi4ELb1EEEv13esm_conv_desc": 20,
+    "_ZN3esm4conv12dconv_kernelILb0ELi3ELi2ELb0ELi1ELi1ELi4ELi4ELb1EEEv13esm_conv_desc": 20,
 }
 
 

@@ -116,6 +116,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
         case ESM_ACT_SILU: return silu(v);
         case ESM_ACT_RELU: return v > 0.f ? v : 0.f;
         case ESM_ACT_SIGMOID: return 1.0f / (1.0f + expf(-v));
+        case ESM_ACT_RELU6: return fminf(fmaxf(v, 0.f), 6.f);
         default: return v;
     }
 }

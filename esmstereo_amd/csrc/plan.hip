@@ -335,6 +335,7 @@ int esm_struct_size(int which) {
         case 5: return static_cast<int>(sizeof(esm_fmnet_desc));
         case 6: return static_cast<int>(sizeof(esm_conf_desc));
         case 8: return static_cast<int>(sizeof(esm_shuffle_conv_desc));
+        case 9: return static_cast<int>(sizeof(esm_dwconv_desc));
         default: return -1;
     }
 }

@@ -23,11 +23,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleConvDesc,
+from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_RELU6, ACT_SIGMOID, ACT_SILU, EsmConfDesc, EsmConvDesc, EsmShuffleConvDesc,
                    EsmShuffleTailDesc, EsmSmixDesc, check, lib)
 
 __all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_fmnet", "run_shuffle_tail", "pack_shuffle_tail",
-           "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID"]
+           "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID", "ACT_RELU6", "run_dwconv", "cached_pack"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -160,6 +160,17 @@ def pack_conv(conv: torch.nn.Module, bn: Optional[torch.nn.Module] = None, act: 
     cin, cout = (W.shape[0], W.shape[1]) if transposed else (W.shape[1], W.shape[0])
     return PackedConv(P, scale, shift, act, nd, ks.pop(), ss.pop(), ps.pop(), transposed, int(cin), int(cout),
                       cin_pad, cout_pad)
+
+
+def cached_pack(owner: torch.nn.Module, name: str, mods: Sequence[Optional[torch.nn.Module]], build, *extra):
+    """``build()`` (packed weights of ``mods``) cached on ``owner`` under ``name`` until a tensor of ``mods`` is
+    replaced, moved or edited in place (param_token)."""
+    tok = param_token(*mods) + tuple(extra)
+    packs = owner.__dict__.setdefault("_esm_packs", {})
+    c = packs.get(name)
+    if c is None or c[0] != tok:
+        c = packs[name] = (tok, build())
+    return c[1]
 
 
 def param_token(*mods: torch.nn.Module) -> Tuple:
@@ -344,6 +355,13 @@ class Ctx:
             check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv")
         else:
             check(lib.esm_shuffle_conv_f32(ctypes.byref(d), self.stream), "shuffle_conv")
+
+    def dwconv(self, d) -> None:
+        if not self._submit():
+            return
+        if self.plan:
+            raise RuntimeError("dwconv: the backbone's depthwise convs run eagerly (no plan op)")
+        check(lib.esm_dwconv_f32(ctypes.byref(d), self.stream), "dwconv")
 
     def gwc(self, L, R, att, V, B, C, H, W, D, G) -> None:
         self.meta.append(dict(name="gwc_volume", kind="gwc", flops=2 * B * C * D * H * W,
@@ -721,6 +739,28 @@ def run_pair2(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: Packed
     ctx.meta.append(dict(name=name, kind="conv_pair", flops=flops, bytes=byts, shape=f"pair {ma['shape']} + {mb['shape']}",
                          reads=reads, writes=writes, key=ma["key"] + " | " + mb["key"], hint=0))
     ctx.pair2(da, db)
+    return out
+
+
+def run_dwconv(ctx: Ctx, x: torch.Tensor, w: torch.Tensor, scale: Optional[torch.Tensor], shift: Optional[torch.Tensor],
+               k: int, stride: int, pad: int, act: int, tag: str = "dwconv") -> torch.Tensor:
+    """Depthwise KxK conv (groups = C) + folded BN + activation (``esm_dwconv_f32``): timm's ``conv_dw -> bn``
+    (+ act) of the backbone blocks.  ``w``: [C, K*K] contiguous."""
+    require_device(x, "dwconv input")
+    B, C, H, W = (int(v) for v in x.shape)
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = ctx.empty(B, C, Ho, Wo)
+    require_on(x.device, "dwconv", x, w, scale, shift, out)
+    d = _lib.EsmDwconvDesc()
+    d.x, d.xb, d.xc, d.xh = x.data_ptr(), x.stride(0), x.stride(1), x.stride(2)
+    d.w = w.data_ptr()
+    d.scale = scale.data_ptr() if scale is not None else None
+    d.shift = shift.data_ptr() if shift is not None else None
+    d.out, d.ob, d.oc, d.oh = out.data_ptr(), out.stride(0), out.stride(1), out.stride(2)
+    d.B, d.C, d.H, d.W, d.K, d.stride, d.pad, d.act, d.Ho, d.Wo = B, C, H, W, k, stride, pad, act, Ho, Wo
+    ctx.meta.append(dict(name=tag, kind="dwconv", flops=2 * B * C * Ho * Wo * k * k,
+                         bytes=4 * (x.numel() + out.numel() + C * k * k), reads=_spans(x), writes=_spans(out)))
+    ctx.dwconv(d)
     return out
 
 

@@ -36,9 +36,9 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import check, lib
-from .backbone import Feature
+from .backbone import Feature, fast_path_ok
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
-from .engine import Ctx, require_device
+from .engine import ACT_NONE, ACT_RELU, Ctx, cached_pack, pack_conv, require_device, run_conv
 
 __all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath", "plan_ops"]
 
@@ -105,6 +105,28 @@ class FeatUp(nn.Module):
 def _stem(cin: int, c: int) -> nn.Sequential:
     return nn.Sequential(BasicConv(cin, c, kernel_size=3, stride=2, padding=1), nn.Conv2d(c, c, 3, 1, 1, bias=False),
                          nn.BatchNorm2d(c), nn.ReLU())
+
+
+def _seq_fast(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """A backbone-side Sequential of [BasicConv, Conv2d(, BatchNorm2d, ReLU)] (the stems, ESMStereo.py:528-583;
+    ``semantic``, :600-607) with the trailing plain conv (+ BN + ReLU) as one HIP conv launch (BN folded, ReLU in
+    the epilogue) in eval mode without autograd; the module's own forward otherwise."""
+    if not fast_path_ok(seq, x):
+        return seq(x)
+    y = seq[0](x)
+    conv = seq[1]
+    bn = seq[2] if len(seq) > 2 else None
+    act = ACT_RELU if len(seq) > 3 else ACT_NONE
+    pc = cached_pack(seq, "conv", (conv, bn), lambda: pack_conv(conv, bn, act), act)
+    return run_conv(Ctx(y.device), pc, [y], tag=getattr(seq, "_esm_name", "stem") + ".1")
+
+
+def _conv_fast(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """A plain nn.Conv2d of the backbone side (``desc``, ESMStereo.py:597) as one HIP conv launch in eval mode."""
+    if not fast_path_ok(conv, x):
+        return conv(x)
+    pc = cached_pack(conv, "conv", (conv,), lambda: pack_conv(conv, None, ACT_NONE))
+    return run_conv(Ctx(x.device), pc, [x], tag=getattr(conv, "_esm_name", "conv"))
 
 
 # stems per cost-volume scale (reference ESMStereo.py:528-583): name -> (cin, cout)
@@ -493,15 +515,20 @@ class ESMStereo(nn.Module):
         f = self.feature(both)
         if vs in (4, 8):
             f = self.feature_up.one(f)
-        stems = [self.stem_2(both)]
+        stems = [_seq_fast(self.stem_2, both)]
         for name, _, _ in _STEMS[vs][1:]:
-            stems.append(getattr(self, name)(stems[-1]))
+            stems.append(_seq_fast(getattr(self, name), stems[-1]))
         idx = {4: 0, 8: 1, 16: 3}[vs]
-        m = self.desc(self.conv(torch.cat((f[idx], stems[-1]), 1)))
+        src = [f[idx], stems[-1]]
+        if fast_path_ok(self.conv, both) and all(int(t.shape[1]) % 4 == 0 for t in src):
+            mc = self.conv.emit(Ctx(both.device), src)  # the concat as two conv sources, never materialised
+        else:
+            mc = self.conv(torch.cat(src, 1))
+        m = _conv_fast(self.desc, mc)
         ml, mr = m[:B], m[B:]
         fl = [t[:B] for t in f]
         sx = stems[0][:B]
-        att = self.semantic(fl[3]) if vs == 16 else None
+        att = _seq_fast(self.semantic, fl[3]) if vs == 16 else None
         if vs == 4:
             up = [fl[1], fl[0], sx]
         elif vs == 8:

@@ -64,6 +64,7 @@ extern "C" {
 #define ESM_ACT_SILU 2
 #define ESM_ACT_RELU 3
 #define ESM_ACT_SIGMOID 4 /* 1 / (1 + exp(-x)), torch.sigmoid */
+#define ESM_ACT_RELU6 5   /* min(max(x, 0), 6), nn.ReLU6 (the MobileNetV2 backbone) */
 
 #define ESM_MAX_SRC 3
 
@@ -248,11 +249,26 @@ typedef struct {
     int32_t pre_cin, pre_cin_pad, pre_cout_pad, pre_reserved;
 } esm_shuffle_conv_desc;
 
+/* Depthwise KxK conv (groups = C, no bias) + folded BN (out = act(conv * scale[c] + shift[c]); scale NULL = 1,
+ * shift NULL = 0): timm's conv_dw + bn of the backbone blocks (models/ESMStereo.py:40-77).  x: [B, C, H, W]
+ * (strides xb, xc, xh; innermost 1), w: [C][K][K], out: [B, C, Ho, Wo] (strides ob, oc, oh), zero padding
+ * `pad`, (K, stride) in {(3, 1), (3, 2), (5, 1), (5, 2)}, act one of ESM_ACT_*. */
+typedef struct {
+    const float* x;
+    int64_t xb, xc, xh;
+    const float* w;
+    const float* scale;
+    const float* shift;
+    float* out;
+    int64_t ob, oc, oh;
+    int32_t B, C, H, W, K, stride, pad, act, Ho, Wo;
+} esm_dwconv_desc;
+
 const char* esm_last_error(void);
 int esm_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 esm_src, 1 esm_conv_desc,
  * 2 esm_smix_stage, 3 esm_smix_desc, 4 esm_shuffle_tail_desc, 5 esm_fmnet_desc, 6 esm_conf_desc,
- * 8 esm_shuffle_conv_desc;
+ * 8 esm_shuffle_conv_desc, 9 esm_dwconv_desc;
  * -1 for an unknown id. */
 int esm_struct_size(int which);
 
@@ -314,6 +330,9 @@ typedef struct {
     float* out;
 } esm_conf_desc;
 int esm_conf_f32(const esm_conf_desc* desc, void* stream);
+/* The backbone's depthwise conv + BN + activation (esm_dwconv_desc; replaces MIOpen's grouped conv + BatchNorm +
+ * activation of timm's blocks, backbone side of models/ESMStereo.py:640-697). */
+int esm_dwconv_f32(const esm_dwconv_desc* desc, void* stream);
 
 /* img: [B, H, W, 3] uint8 RGB (PIL order); out: [B, 3, Hp, Wp] fp32.  The image lands at rows
  * [top, top+H), columns [left, left+W); pad_normalized = 1 fills the rest with normalised zeros
