@@ -324,18 +324,20 @@ class ForwardGraph:
 
     def __init__(self, model: "ESMStereo", left: torch.Tensor, right: torch.Tensor, train_status: bool):
         self.device = left.device
-        self.left, self.right = left.clone(), right.clone()
+        B = int(left.shape[0])
+        self.both = torch.cat((left, right), 0)  # the static image buffer: [left; right], the backbone's batch
+        self.left, self.right = self.both[:B], self.both[B:]
         cur = torch.cuda.current_stream(self.device)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(2):
-                ml, mr, att, up = model.prefix(self.left, self.right)
+                ml, mr, att, up = model.prefix(self.left, self.right, self.both)
         cur.wait_stream(side)
         torch.cuda.synchronize(self.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.ml, self.mr, self.att, self.up = model.prefix(self.left, self.right)
+            self.ml, self.mr, self.att, self.up = model.prefix(self.left, self.right, self.both)
         self.hp = HotPath(model, int(self.ml.shape[0]), int(self.ml.shape[2]), int(self.ml.shape[3]),
                           0 if self.att is None else int(self.att.shape[1]), [tuple(u.shape) for u in self.up],
                           self.device, train_status, graph=True, channels=int(self.ml.shape[1]))
@@ -499,11 +501,12 @@ class ESMStereo(nn.Module):
         return super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     # ------------------------------------------------------------------ forward pieces
-    def prefix(self, left: torch.Tensor, right: torch.Tensor):
-        """Backbone side, reference lines 640-697 -> (match_left, match_right, att, upsampler feats)."""
-        return self._prefix(left, right)[:4]
+    def prefix(self, left: torch.Tensor, right: torch.Tensor, both: Optional[torch.Tensor] = None):
+        """Backbone side, reference lines 640-697 -> (match_left, match_right, att, upsampler feats).
+        ``both``: [left; right] already as one [2B, ...] tensor (left / right its halves): no concat."""
+        return self._prefix(left, right, both)[:4]
 
-    def _prefix(self, left: torch.Tensor, right: torch.Tensor):
+    def _prefix(self, left: torch.Tensor, right: torch.Tensor, both: Optional[torch.Tensor] = None):
         """The backbone side with left and right as ONE batch [left; right] (eval BatchNorm and every other
         op are per sample, so each half equals the reference's separate left / right passes, :640-697):
         every backbone launch covers both images, half the launches of the reference's order."""
@@ -511,7 +514,8 @@ class ESMStereo(nn.Module):
         B = int(left.shape[0])
         if tuple(left.shape) != tuple(right.shape):
             raise RuntimeError(f"left {tuple(left.shape)} and right {tuple(right.shape)} image sizes differ")
-        both = torch.cat((left, right), 0)
+        if both is None:
+            both = torch.cat((left, right), 0)
         f = self.feature(both)
         if vs in (4, 8):
             f = self.feature_up.one(f)
@@ -666,10 +670,10 @@ class ESMStereo_confidence(ESMStereo):
             for name, mod in self.confidence_net.named_modules():
                 object.__setattr__(mod, "_esm_name", "confidence_net" + ("." + name if name else ""))
 
-    def prefix(self, left: torch.Tensor, right: torch.Tensor):
+    def prefix(self, left: torch.Tensor, right: torch.Tensor, both: Optional[torch.Tensor] = None):
         """As :meth:`ESMStereo.prefix`, with features_left[3] appended to the upsampler features
         (the confidence head's ``left_f1x``, ``:972``)."""
-        ml, mr, att, up, fl = self._prefix(left, right)
+        ml, mr, att, up, fl = self._prefix(left, right, both)
         if self.vol_size == 16:
             up = list(up) + [fl[3]]
         return ml, mr, att, up
