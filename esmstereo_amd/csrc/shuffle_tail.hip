@@ -654,7 +654,7 @@ __device__ unsigned long long sc4_stamps[4096 * 8];
 #define SC4_STAMP(k) (void)0
 #endif
 
-template <int L, bool PRE>
+template <int L, bool PRE, bool MC1 = false>
 __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle_conv_desc d) {
     using G = Sc4Geo<L>;
     constexpr int NF = G::NF, C = G::C, SR = G::SR, SC = G::SC, LH = G::LH, LW = G::LW, WN = G::WN, XN = G::XN;
@@ -898,8 +898,49 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
     __syncthreads();
     SC4_STAMP(5);
 
-    // ---- c1 = GELU(BN(conv 3x3 s2 p1 (x))): thread = one output pixel of the (2L) x 32 tile, all C channels
-    {
+    // ---- c1 = GELU(BN(conv 3x3 s2 p1 (x)))
+    if constexpr (MC1) {
+        // on the matrix cores (round 5): N-tile = 16 output pixels of one row, M = the 16 couts, K = the 9 taps in
+        // 3 k-steps (lane (g, n): tap 4s + g of pixel n); C lane (g, n): couts 4g .. 4g + 3.  Phase stamps of the
+        // VALU form below: 3.4 of the kernel's 15.6 us; this form 1.2 us (profiles/r05_sc4_stamps.txt)
+        const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            d.out + b * d.ob, static_cast<short>(0), static_cast<int>(4 * ((C - 1) * d.oc + (Ho2 - 1) * d.oh + Wo2)),
+            0x00020000);
+        float ca[3], sc[4], shf[4];
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+            const int t = 4 * s3 + g;
+            ca[s3] = t < 9 ? wsh[G::OW_CW + t * C + n] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = wsh[G::OW_SC + 4 * g + j];
+            shf[j] = wsh[G::OW_SH + 4 * g + j];
+        }
+        for (int nt = wave; nt < 4 * L; nt += L) {
+            const int oyl = nt >> 1, oxl = 16 * (nt & 1) + n;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3) {
+                const int t = 4 * s3 + g;
+                const int tt = t < 9 ? t : 8;
+                const int ky = tt / 3, kx = tt - (tt / 3) * 3;
+                const float bv = xs[2 * oyl + ky][3 + 2 * oxl + kx];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[s3], t < 9 ? bv : 0.f, acc, 0, 0, 0);
+            }
+            const int oy = Y0 / 2 + oyl, ox = X0 / 2 + oxl;
+            const bool ok = oy < Ho2 && ox < Wo2;
+            const unsigned pix = 4u * static_cast<unsigned>(oy * d.oh + ox);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 4 * g + j;
+                const float v = gelu_erf(acc[j] * sc[j] + shf[j]);
+                conv::store_b32(__float_as_uint(v), ro,
+                                static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
+            }
+        }
+    } else {
         const int yy = tid >> 5, xx = tid & 31;
         const int oy = Y0 / 2 + yy, ox = X0 / 2 + xx;
         float xv[9];
@@ -929,314 +970,14 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
 #endif
 }
 
-// Round-5 form of the same launch (nf 8, r 4, C 16; st.flags bits 1-2 = 3): shuffle_conv4_kernel's tile (8 low-res
-// rows x 16 low-res pixels -> a 32 x 64 x tile -> the conv's 16 x 32 output tile) on a 16-wave workgroup, every
-// phase cut into balanced items over all 16 waves and the GEMM-shaped ones on the matrix cores.  Phase stamps of
-// shuffle_conv4_kernel in the S-K step (profiles/r05_sc4_stamps.txt) showed each phase latency-bound on a few
-// lanes' long chains (8 waves, two MFMA rounds on half of them, the ring / x row on a fraction of the lanes):
-//   1. one round trip: weights (LDS), the pre-conv weights as [tap][ci][co] and the pre-conv window (LDS);
-//   2. pre-conv (PRE) on the 10 x 18 low-res window with the 16-block MFMA (4 couts x 4 pixels per block, no
-//      padded output rows): 12 waves = 3 pixel tiles x 4 channel quarters, partial sums added in a fixed order;
-//   3. the shuffled map on the WHOLE window (its ring included) by 16x16x4 MFMA: 96 (window tile, channel) items;
-//   4. the 3x3 tail -> x rows Y0 - 1 .. Y0 + 31, cols X0 - 1 .. X0 + 63 in ONE pass of 561 (row, quad) items;
-//   5. c1 = GELU(BN(conv3x3 s2 (x))) by MFMA (M = 16 couts, N = 16 output pixels, K = 9 taps in 3 k-steps).
-// The shuffled map and the tail compute as shuffle_conv4_kernel; the two convs sum in MFMA k-step order
-// (relative 1e-5 vs fp64, tests/test_gpu_parity.py test_shuffle_conv_*).
-struct Sc6Geo {
-    static constexpr int NF = 8, C = 16, L = 8, NT = 1024, NWV = NT / 64;
-    static constexpr int LH = L + 2, LW = 18, LP0 = LH * LW;            // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
-    static constexpr int LP = LP0 + ((16 - LP0 % 32) + 32) % 32;        // channel stride = 16 (mod 32) banks
-    static constexpr int LNT = (LP0 + 15) / 16;                          // 16-pixel window tiles (12)
-    static constexpr int SR = 4 * L + 3, SC = 72;                        // shuffled map: row 0 = Y0 - 2, col 0 = X0 - 4
-    static constexpr int XR = 4 * L + 1;                                 // x: row 0 = Y0 - 1, col 0 = X0 - 4
-    // the conv weights start 16-B aligned (4 floats) so that its BN vectors are float4 reads
-    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = (OW_TB + 1 + 3) / 4 * 4,
-                         OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, OW_PS = OW_SH + C, OW_PH = OW_PS + NF,
-                         OW_PW = OW_PH + NF, WN = OW_PW + 9 * 16 * NF;   // + the pre-conv weights [tap][ci][co]
-    static constexpr int PR = L + 4, PW = 20, PCS0 = PR * PW;           // pre-conv window: rows ly0 - 2 .., cols lx0 - 2 ..
-    static constexpr int PCS = PCS0 + ((16 - PCS0 % 32) + 32) % 32, PXN = 16 * PCS;
-    static constexpr int PT = (LP0 + 63) / 64;                           // 64-pixel tiles of the 16-block MFMA (3)
-    static constexpr int PART = 4 * PT * 64 * NF;                        // partial sums [quarter][tile][lane][co]
-    static constexpr int POST = NF * SR * SC + XR * SC;                  // sh + xs
-    static constexpr int PRE_N = PXN + PART;
-    static constexpr int UN = POST > PRE_N ? POST : PRE_N;
-    static constexpr int TQ = 17, TITEMS = XR * TQ;                      // tail items: (x row, column quad)
-};
-
-template <bool PRE>
-__global__ void __launch_bounds__(1024) shuffle_conv6_kernel(const esm_shuffle_conv_desc d) {
-    using G = Sc6Geo;
-    constexpr int NF = G::NF, C = G::C, NT = G::NT, NWV = G::NWV, LW = G::LW, LP = G::LP, LP0 = G::LP0;
-    constexpr int SR = G::SR, SC = G::SC, XR = G::XR, WN = G::WN, L = G::L;
-    const esm_shuffle_tail_desc& a = d.st;
-    __shared__ __attribute__((aligned(16))) float wsh[WN];
-    __shared__ __attribute__((aligned(16))) float lr[NF * LP];
-    __shared__ __attribute__((aligned(16))) float un[G::UN];
-    float* const sh = un;                    // [NF][SR][SC]
-    float* const xs = un + NF * SR * SC;     // [XR][SC]
-    float* const pxs = un;                   // [16][PCS]            (PRE, until lr is built)
-    float* const part = un + G::PXN;         // [4][PT][64][NF]       (PRE, until lr is built)
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int H = a.H, W = a.W, HO = 4 * H, WO = 4 * W;
-    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
-    const int b = bk_.z;
-    const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
-    const int Y0 = 4 * ly0, X0 = 4 * lx0;
-    SC4_STAMP(0);
-
-    // ---- 1. stage (one round trip)
-    constexpr int WRN = (WN + NT - 1) / NT;
-    float rw[WRN];
-#pragma unroll
-    for (int k = 0; k < WRN; ++k) {
-        const int i = tid + k * NT;
-        const float* p;
-        int off;
-        float dflt = 0.f;
-        if (i < G::OW_UB) { p = a.up_w; off = i; }
-        else if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
-        else if (i < G::OW_TB) { p = a.tail_w; off = i - G::OW_TW; }
-        else if (i == G::OW_TB) { p = a.tail_b; off = 0; }
-        else if (i < G::OW_CW) { p = nullptr; off = 0; }  // alignment padding
-        else if (i < G::OW_SC) { p = d.w; off = (i - G::OW_CW) / C * d.cin_pad * d.cout_pad + (i - G::OW_CW) % C; }
-        else if (i < G::OW_SH) { p = d.scale; off = i - G::OW_SC; dflt = 1.f; }
-        else if (i < G::OW_PS) { p = d.shift; off = i - G::OW_SH; }
-        else if (i < G::OW_PH) { p = PRE ? d.pre_scale : nullptr; off = i - G::OW_PS; dflt = 1.f; }
-        else if (i < G::OW_PW) { p = PRE ? d.pre_shift : nullptr; off = i - G::OW_PH; }
-        else {  // pre-conv weights [tap][ci][co] <- packed [tap][cin_pad][cout_pad]
-            const int j = i - G::OW_PW, co = j % NF, ci = (j / NF) % 16, tap = j / (16 * NF);
-            const bool ok = PRE && ci < d.pre_cin;
-            p = ok ? d.pre_w : nullptr;
-            off = ok ? (tap * d.pre_cin_pad + ci) * d.pre_cout_pad + co : 0;
-        }
-        const bool ok = i < WN && p != nullptr;
-        const float v = (ok ? p : a.up_w)[ok ? off : 0];
-        rw[k] = ok ? v : dflt;
-    }
-    constexpr int PXR = PRE ? (G::PXN + NT - 1) / NT : 1;
-    constexpr int XRN = PRE ? 1 : (NF * LP + NT - 1) / NT;
-    float rp[PXR], rx[XRN];
-    if constexpr (PRE) {
-        const float* pb = d.pre_x + b * d.pb;
-#pragma unroll
-        for (int k = 0; k < PXR; ++k) {
-            const int i = tid + k * NT;
-            const int c = i / G::PCS, rem = i - c * G::PCS;
-            const int yy = ly0 - 2 + rem / G::PW, xx = lx0 - 2 + rem % G::PW;
-            const bool ok = i < G::PXN && rem < G::PCS0 && c < d.pre_cin && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            const float v = pb[ok ? c * d.pc + yy * d.ph + xx : 0];
-            rp[k] = ok ? v : 0.f;
-        }
-    } else {
-        const float* xb = a.x + b * a.xb;
-#pragma unroll
-        for (int k = 0; k < XRN; ++k) {
-            const int i = tid + k * NT;
-            const int c = i / LP, rem = i - c * LP;
-            const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
-            const bool ok = i < NF * LP && rem < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
-            rx[k] = ok ? v : 0.f;
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < WRN; ++k)
-        if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
-    if constexpr (PRE) {
-#pragma unroll
-        for (int k = 0; k < PXR; ++k)
-            if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < XRN; ++k)
-            if (tid + k * NT < NF * LP) lr[tid + k * NT] = rx[k];
-    }
-    __syncthreads();
-    SC4_STAMP(1);
-
-    // ---- 2. pre-conv: 16-block MFMA (block = 4 lanes: A = 4 couts of one k, B = the k value of 4 pixels), lane =
-    //         window pixel 64t + lane, wave (t, q) sums channels 4q .. 4q + 3 over the 9 taps
-    if constexpr (PRE) {
-        if (wave < 4 * G::PT) {
-            const int t = wave >> 2, q = wave & 3;
-            const int p = 64 * t + lane;
-            const int pp = p < LP0 ? p : 0;
-            const int py = pp / LW, px = pp - (pp / LW) * LW;
-            const int i4 = lane & 3;
-            conv::floatx4 acc[2][2] = {{conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}},
-                                       {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}}};
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int dy = tap / 3, dx = tap % 3;
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const int ci = 4 * q + cc;
-                    const float bv = pxs[ci * G::PCS + (py + dy) * G::PW + px + dx];
-                    const float* wr = &wsh[G::OW_PW + (tap * 16 + ci) * NF];
-                    acc[cc & 1][0] = __builtin_amdgcn_mfma_f32_4x4x1f32(wr[i4], bv, acc[cc & 1][0], 0, 0, 0);
-                    acc[cc & 1][1] = __builtin_amdgcn_mfma_f32_4x4x1f32(wr[4 + i4], bv, acc[cc & 1][1], 0, 0, 0);
-                }
-            }
-            // D_b[i][j] (VGPR i, lane 4b + j) = cout 4h + i at this lane's pixel
-            float* pr = &part[((q * G::PT + t) * 64 + lane) * NF];
-            *reinterpret_cast<conv::floatx4*>(pr) = acc[0][0] + acc[1][0];
-            *reinterpret_cast<conv::floatx4*>(pr + 4) = acc[0][1] + acc[1][1];
-        }
-        __syncthreads();
-        // the four channel quarters added in a fixed order, BN + GELU, zero outside the image -> lr
-        for (int e = tid; e < LP0 * NF; e += NT) {
-            const int p = e % LP0, co = e / LP0;
-            const int t = p >> 6, l = p & 63;
-            float v = 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v += part[((q * G::PT + t) * 64 + l) * NF + co];
-            const int py = p / LW, px = p - (p / LW) * LW;
-            const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
-            const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
-            const float gv = gelu_erf(v * wsh[G::OW_PS + co] + wsh[G::OW_PH + co]);
-            lr[co * LP + p] = in ? gv : 0.f;
-        }
-        __syncthreads();  // lr complete; the pre-conv window and the partial sums (aliased by sh) are dead
-    }
-    SC4_STAMP(2);
-
-    // ---- 3. shuffled map on the whole window: item (window tile wt, channel c), 16x16x4 MFMA with M = the 16
-    //         sub-pixels of channel c, N = 16 window pixels, K = the nf channels; lane (g, n): sub-row g,
-    //         sub-columns 0..3 of window pixel n
-    for (int it = wave; it < G::LNT * NF; it += NWV) {
-        const int wt = it >> 3, c = it & 7;
-        const int p = wt * 16 + n;
-        const int pp = p < LP0 ? p : 0;
-        const int py = pp / LW, px = pp - (pp / LW) * LW;
-        conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wsh[(c * 16 + n) * NF + 4 * kk + g], lr[(4 * kk + g) * LP + pp],
-                                                      acc, 0, 0, 0);
-        const int row = 4 * py + g - 2;  // sh row (Y0 - 2 + row)
-        const int Y = Y0 - 2 + row, X = X0 - 4 + 4 * px;
-        const bool yok = Y >= 0 && Y < HO;
-        const conv::floatx4 bias = *reinterpret_cast<const conv::floatx4*>(&wsh[G::OW_UB + c * 16 + 4 * g]);
-        conv::floatx4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float v = silu_fast(acc[j] + bias[j]);
-            o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
-        }
-        if (p < LP0 && row >= 0 && row < SR) *reinterpret_cast<conv::floatx4*>(&sh[(c * SR + row) * SC + 4 * px]) = o;
-    }
-    __syncthreads();
-    SC4_STAMP(3);
-
-    // ---- 4. tail -> x: item (x row r, column quad q): x row Y0 - 1 + r, cols X0 - 4 + 4q .. + 3 (quad 0: only
-    //         X0 - 1 is used), 4 outputs a lane with packed FMA as shuffle_conv4_kernel
-    {
-        const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
-        for (int it = tid; it < G::TITEMS; it += NT) {
-            const int r = it / G::TQ, q = it - (it / G::TQ) * G::TQ;
-            const int cl = 4 * q - 1 < 0 ? 0 : 4 * q - 1;
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-            for (int c = 0; c < NF; ++c) {
-#pragma unroll
-                for (int ky = 0; ky < 3; ++ky) {
-                    const float* row = &sh[(c * SR + r + ky) * SC];
-                    const conv::floatx4 m4 = *reinterpret_cast<const conv::floatx4*>(row + 4 * q);
-                    const float v[6] = {row[cl], m4[0], m4[1], m4[2], m4[3], row[4 * q + 4]};
-#pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) {
-                        const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
-                        const f2v w2 = {w, w};
-                        const f2v lo = __builtin_elementwise_fma(w2, f2v{v[kx], v[1 + kx]}, f2v{acc[0], acc[1]});
-                        const f2v hi = __builtin_elementwise_fma(w2, f2v{v[2 + kx], v[3 + kx]}, f2v{acc[2], acc[3]});
-                        acc[0] = lo[0];
-                        acc[1] = lo[1];
-                        acc[2] = hi[0];
-                        acc[3] = hi[1];
-                    }
-                }
-            }
-            const int Y = Y0 - 1 + r;
-            conv::floatx4 o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int X = X0 - 4 + 4 * q + j;
-                o[j] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc[j] + tb : 0.f;  // the conv's zero padding
-            }
-            *reinterpret_cast<conv::floatx4*>(&xs[r * SC + 4 * q]) = o;
-        }
-    }
-    __syncthreads();
-    SC4_STAMP(4);
-    SC4_STAMP(5);
-
-    // ---- 5. c1 = GELU(BN(conv 3x3 s2 p1 (x))) on the 16 x 32 output tile: N-tile = 16 pixels of one output row;
-    //         lane (g, n): k-step s reads tap 4s + g of pixel n; C lane (g, n): couts 4g .. 4g + 3
-    {
-        const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
-        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-            d.out + b * d.ob, static_cast<short>(0), static_cast<int>(4 * ((C - 1) * d.oc + (Ho2 - 1) * d.oh + Wo2)),
-            0x00020000);
-        float ca[3];
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) {
-            const int t = 4 * s3 + g;
-            ca[s3] = t < 9 ? wsh[G::OW_CW + t * C + n] : 0.f;
-        }
-        const conv::floatx4 sc = *reinterpret_cast<const conv::floatx4*>(&wsh[G::OW_SC + 4 * g]);
-        const conv::floatx4 shf = *reinterpret_cast<const conv::floatx4*>(&wsh[G::OW_SH + 4 * g]);
-        for (int nt = wave; nt < 4 * L; nt += NWV) {
-            const int oyl = nt >> 1, oxl = 16 * (nt & 1) + n;
-            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s3 = 0; s3 < 3; ++s3) {
-                const int t = 4 * s3 + g;
-                const int tt = t < 9 ? t : 8;
-                const int ky = tt / 3, kx = tt - (tt / 3) * 3;
-                const float bv = xs[(2 * oyl + ky) * SC + 3 + 2 * oxl + kx];
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[s3], t < 9 ? bv : 0.f, acc, 0, 0, 0);
-            }
-            const int oy = Y0 / 2 + oyl, ox = X0 / 2 + oxl;
-            const bool ok = oy < Ho2 && ox < Wo2;
-            const unsigned pix = 4u * static_cast<unsigned>(oy * d.oh + ox);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int co = 4 * g + j;
-                const float v = gelu_erf(acc[j] * sc[j] + shf[j]);
-                conv::store_b32(__float_as_uint(v), ro,
-                                static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
-            }
-        }
-    }
-    SC4_STAMP(6);
-#ifdef ESM_CONV_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    SC4_STAMP(7);
-#endif
-}
-
-int launch_sc6(const esm_shuffle_conv_desc& a, hipStream_t s) {
-    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, Sc6Geo::L), a.st.B);
-    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
-    if (a.pre_x)
-        hipLaunchKernelGGL((shuffle_conv6_kernel<true>), grid, dim3(Sc6Geo::NT), 0, s, a);
-    else
-        hipLaunchKernelGGL((shuffle_conv6_kernel<false>), grid, dim3(Sc6Geo::NT), 0, s, a);
-    return check_launch("shuffle_conv");
-}
-
-template <int L>
+template <int L, bool MC1 = false>
 int launch_sc4(const esm_shuffle_conv_desc& a, hipStream_t s) {
     const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
     if (a.pre_x)
-        hipLaunchKernelGGL((shuffle_conv4_kernel<L, true>), grid, dim3(64 * L), 0, s, a);
+        hipLaunchKernelGGL((shuffle_conv4_kernel<L, true, MC1>), grid, dim3(64 * L), 0, s, a);
     else
-        hipLaunchKernelGGL((shuffle_conv4_kernel<L, false>), grid, dim3(64 * L), 0, s, a);
+        hipLaunchKernelGGL((shuffle_conv4_kernel<L, false, MC1>), grid, dim3(64 * L), 0, s, a);
     return check_launch("shuffle_conv");
 }
 
@@ -1298,7 +1039,7 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
         const int form = (t.flags >> 1) & 3;
         const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
-        if (form == 3) return launch_sc6(a, s);
+        if (form == 3) return launch_sc4<8, true>(a, s);
         if (a.pre_x || form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
         return launch_sc<8, 4, 16>(a, s);
     }

@@ -979,8 +979,8 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
     3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
     stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)].  ``form`` (nf 8, r 4, C 16): 0
-    automatic, 1 the window form, 2 the row form (8 low-res rows, 8 waves), 3 the round-5 row form (16 waves, MFMA
-    convs).  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
+    automatic, 1 the window form, 2 the row form (8 low-res rows), 3 the row form with the refinement conv on
+    the matrix cores.  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
     ``pre`` (the stage's spx_<t>[1], BasicConv(Cp, nf, 3, 1, 1)), computed inside the launch as well."""
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
@@ -1018,7 +1018,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
         d.pre_cin, d.pre_cin_pad, d.pre_cout_pad = pre.cin, pre.cin_pad, pre.cout_pad
         require_on(x.device, "shuffle_conv pre-conv", pre.w, pre.scale, pre.shift)
         ctx.hold(pre.w, pre.scale, pre.shift)
-        form = form if form == 3 else 2  # the row forms (2: shuffle_conv4_kernel, 3: shuffle_conv6_kernel)
+        form = form if form == 3 else 2  # the row forms (3: the refinement conv on the matrix cores)
     t.up_w, t.up_b, t.tail_w = p.up_w.data_ptr(), p.up_b.data_ptr(), p.tail_w.data_ptr()
     t.tail_b = p.tail_b.data_ptr() if p.tail_b is not None else None
     t.out = None

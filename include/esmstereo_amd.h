@@ -227,7 +227,7 @@ typedef struct {
  * folded BN (scale NULL = 1); out: [B, C, ceil(r*H/2), ceil(r*W/2)] with strides ob, oc, oh.
  * (nf, r, C) in {(8, 4, 16), (8, 2, 16), (16, 2, 32), (16, 4, 32)}.  st.flags bit 0: XCD-slab tile order;
  * bits 1-2, (8, 4, 16) only: 0 automatic, 1 the low-res-window form, 2 the MFMA row form (8 low-res rows
- * per workgroup), 3 the round-5 row form (the same tile on 16 waves, both convs on the matrix cores). */
+ * per workgroup), 3 the same row form with the refinement conv on the matrix cores. */
 typedef struct {
     esm_shuffle_tail_desc st;
     const float* w;

@@ -49,23 +49,33 @@ def record(model, left, right):
 
 
 def time_hint(E, pc, shapes, res_shape, hint, dev, reps=20):
+    """Device time per launch: ``reps`` launches captured into one CUDA graph (no host work between them),
+    the graph replayed 3 times between one hipEvent pair."""
     srcs = [torch.randn(s, device=dev) for s in shapes]
     res = None
     if res_shape is not None:
         res = torch.randn(res_shape, device=dev)
-    ctx = E.engine.Ctx(dev)
     try:
-        for _ in range(3):
-            E.engine.run_conv(ctx, pc, srcs, res=res, hint=hint)
+        E.engine.run_conv(E.engine.Ctx(dev), pc, srcs, res=res, hint=hint)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(dev)
+        with torch.cuda.stream(side), torch.cuda.graph(g):
+            ctx = E.engine.Ctx(dev)
+            for _ in range(reps):
+                E.engine.run_conv(ctx, pc, srcs, res=res, hint=hint)
     except Exception:
+        torch.cuda.synchronize()
         return None
+    g.replay()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        E.engine.run_conv(ctx, pc, srcs, res=res, hint=hint)
+    for _ in range(3):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e3
+    del g
+    return a.elapsed_time(b) / (3 * reps) * 1e3
 
 
 def main():

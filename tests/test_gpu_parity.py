@@ -726,7 +726,7 @@ def test_shuffle_conv_pre(cp, H, W):
     pc, pp = pk(conv, bn, ACT_GELU), pk(pconv, pbn, ACT_GELU)
     ctx = Ctx(DEV)
     two = run_shuffle_conv(ctx, run_conv(ctx, pp, [c.to(DEV)]), p, pc, form=2)
-    for form in (2, 3):  # shuffle_conv4_kernel, shuffle_conv6_kernel
+    for form in (2, 3):  # the row form with the refinement conv on the VALU / on the matrix cores
         y = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp, form=form)
         assert y.shape == ref.shape
         assert rel(y, ref) < 1e-5, form
