@@ -1039,8 +1039,10 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups
         const int form = (t.flags >> 1) & 3;
         const long long t8 = static_cast<long long>(ceil_div(t.W, 16)) * ceil_div(t.H, 8) * t.B;
-        if (form == 3) return launch_sc4<8, true>(a, s);
-        if (a.pre_x || form == 2 || (form == 0 && t8 >= 128)) return launch_sc4<8>(a, s);
+        // automatic: the refinement conv on the matrix cores (S-K step 0.3193 -> 0.3180 ms, three alternations,
+        // profiles/r05_sc_form_ab.txt); form 2 keeps it on the VALU
+        if (form == 2) return launch_sc4<8, false>(a, s);
+        if (a.pre_x || form == 3 || (form == 0 && t8 >= 128)) return launch_sc4<8, true>(a, s);
         return launch_sc<8, 4, 16>(a, s);
     }
     if (t.nf == 8 && t.r == 2 && a.C == 16) return launch_sc<8, 2, 16>(a, s);
