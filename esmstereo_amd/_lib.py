@@ -80,7 +80,8 @@ class EsmShuffleConvDesc(Structure):
                 ("C", c_int32), ("cin_pad", c_int32), ("cout_pad", c_int32), ("reserved", c_int32),
                 ("pre_x", c_void_p), ("pb", c_int64), ("pc", c_int64), ("ph", c_int64), ("pre_w", c_void_p),
                 ("pre_scale", c_void_p), ("pre_shift", c_void_p), ("pre_cin", c_int32), ("pre_cin_pad", c_int32),
-                ("pre_cout_pad", c_int32), ("pre_reserved", c_int32)]
+                ("pre_cout_pad", c_int32), ("pre_reserved", c_int32), ("w2", c_void_p), ("scale2", c_void_p),
+                ("shift2", c_void_p), ("cin_pad2", c_int32), ("cout_pad2", c_int32)]
 
 
 class EsmConfDesc(Structure):

@@ -23,7 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail, pair2_auto, param_token,
+from .engine import (ACT_GELU, ACT_NONE, SC11_ENABLED, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail,
+                     pair2_auto, param_token,
                      run_conv, run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_pre_supported,
                      shuffle_conv_supported)
 from .mixer import FMBlock
@@ -139,10 +140,15 @@ class _Hourglass(nn.Module):
 
     def _emit(self, ctx: Ctx, x: Optional[torch.Tensor], extra0: Sequence[torch.Tensor] = (),
               extra1: Sequence[torch.Tensor] = (), crop1: bool = True, c10: Optional[torch.Tensor] = None,
-              **last) -> torch.Tensor:
+              c11: Optional[torch.Tensor] = None, **last) -> torch.Tensor:
         """``c10``: conv1[0]'s output, when the caller fused that layer into its producer (then ``x`` is
-        not read)."""
-        c1 = self.conv1[1].emit(ctx, [c10]) if c10 is not None else _pair(ctx, self.conv1[0], [x], self.conv1[1])
+        not read); ``c11``: conv1's output (both of its layers fused into the producer)."""
+        if c11 is not None:
+            c1 = c11
+        elif c10 is not None:
+            c1 = self.conv1[1].emit(ctx, [c10])
+        else:
+            c1 = _pair(ctx, self.conv1[0], [x], self.conv1[1])
         c2 = _pair(ctx, self.conv2[0], [c1], self.conv2[1])
         c3 = _pair(ctx, self.conv3[0], [c2], self.conv3[1])
         u3 = self.conv3_up.emit(ctx, [c3])
@@ -188,8 +194,8 @@ class up_refinement(_Hourglass):
         self._build(1, C, C, C, 2 * C + cf1, 2 * C + cf2)
 
     def emit(self, ctx: Ctx, disp: Optional[torch.Tensor], left_f1x: torch.Tensor, left_f2x: torch.Tensor,
-             c10: Optional[torch.Tensor] = None, **last) -> torch.Tensor:
-        return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, c10=c10, **last)
+             c10: Optional[torch.Tensor] = None, c11: Optional[torch.Tensor] = None, **last) -> torch.Tensor:
+        return self._emit(ctx, disp, extra0=[left_f1x], extra1=[left_f2x], crop1=False, c10=c10, c11=c11, **last)
 
     def forward(self, disp: torch.Tensor, left_f1x: torch.Tensor, left_f2x: torch.Tensor) -> torch.Tensor:
         return eager_emit(disp.device, self.emit, disp, left_f1x, left_f2x)
@@ -281,8 +287,12 @@ class _ESMUpsampler(nn.Module):
                     x = blk.emit(ctx, x)
             # upsampling (1x1 -> PixelShuffle -> SiLU) + tail (3x3 -> 1): one launch, with the refinement
             # hourglass's first conv fused behind it where the kernel has the shape
-            c10 = None
-            if pre is not None:
+            c10 = c11 = None
+            if pre is not None and SC11_ENABLED:  # ... and the refinement's conv1[1] too (the whole conv1)
+                c11 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(), pre=pre, conv2=ref.conv1[1].packed(),
+                                       tag=f"{me}.spx_{tag}.1+upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1")
+                x = None
+            elif pre is not None:
                 c10 = run_shuffle_conv(ctx, x, p[f"up_{tag}"], ref.conv1[0].packed(), pre=pre,
                                        tag=f"{me}.spx_{tag}.1+upsampling{tag[:-1]}+tail{tag}+ref{tag}.conv1.0")
                 x = None
@@ -300,7 +310,7 @@ class _ESMUpsampler(nn.Module):
                 cp = ctx.empty(B, 1, H * r_, W * r_)
                 epi.update(out2=cp, post_scale2=scaled_copies)
                 copies.append(cp)
-            prev = ref.emit(ctx, x, feats[ra], feats[rb], c10=c10, **epi)
+            prev = ref.emit(ctx, x, feats[ra], feats[rb], c10=c10, c11=c11, **epi)
             outs.append(prev)
         outs.reverse()
         copies.reverse()

@@ -107,8 +107,16 @@ __device__ __forceinline__ Blk3 xcd_block(bool slab) {
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 // SiLU with the hardware exp2 / reciprocal (a few ulp): per-pixel chains where the libm forms'
-// division and exp sequences dominate the instruction count (smix, shuffle_tail)
-__device__ __forceinline__ float silu_fast(float x) { return __fdividef(x, 1.0f + __expf(-x)); }
+// division and exp sequences dominate the instruction count (smix, shuffle_tail).  The reciprocal is the
+// v_rcp_f32 builtin: __fdividef compiles to the full IEEE division sequence (v_div_scale x2, v_rcp, 4 FMAs,
+// v_div_fmas, v_div_fixup) without fast-math, 34 such sequences in the 4x head alone (round 5)
+__device__ __forceinline__ float silu_fast(float x) {
+#ifdef ESM_SILU_DIV  // A/B builds: the division form
+    return __fdividef(x, 1.0f + __expf(-x));
+#else
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
+#endif
+}
 
 __device__ __forceinline__ float apply_act(float v, int act) {
     switch (act) {

@@ -242,7 +242,8 @@ struct esm_plan {
             case kShuffleTail: return rb.tail(op.st);
             case kShuffleConv:
                 return rb.tail(op.sc.st) + rb(op.sc.w) + rb(op.sc.scale) + rb(op.sc.shift) + rb(op.sc.out) +
-                       rb(op.sc.pre_x) + rb(op.sc.pre_w) + rb(op.sc.pre_scale) + rb(op.sc.pre_shift);
+                       rb(op.sc.pre_x) + rb(op.sc.pre_w) + rb(op.sc.pre_scale) + rb(op.sc.pre_shift) + rb(op.sc.w2) +
+                       rb(op.sc.scale2) + rb(op.sc.shift2);
             case kConf: {
                 int n = rb(op.cf.out);
                 for (int k = 0; k < 4; ++k) n += rb(op.cf.x[k]);

@@ -970,6 +970,340 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
 #endif
 }
 
+// The 4x stage's spx_4x[1] + upsampling4 + tail4x + ref4x.conv1[0] + ref4x.conv1[1] in ONE launch (round 5,
+// esm_shuffle_conv_desc.w2): shuffle_conv4_kernel's low-res tile (8 rows x 16 pixels) grown by the second conv's
+// one-pixel halo, which the low-res window already covers: the shuffled map on the WHOLE 10 x 18 window by MFMA
+// (rows Y0 - 4 .. Y0 + 35, no VALU ring), x on 37 x 69, the first conv (c1) on its 18 x 34 tile + halo by MFMA into
+// LDS (zero outside the map: the second conv's padding), then the second conv (3x3 16 -> 16, K = 144 in 36
+// k-steps) by MFMA with BN + GELU, stored.  c1 never leaves LDS: the second conv's own launch (10 us at S-K,
+// 0.33 of the fp32 MFMA peak) becomes ~2 us of matrix-core time here.  Arithmetic: the pre-conv, shuffled map
+// and tail as shuffle_conv4_kernel; the convs in MFMA k-step order (relative 1e-5 vs fp64).
+struct Sc7Geo {
+    static constexpr int NF = 8, C = 16, L = 8, NT = 64 * L;
+    static constexpr int LH = L + 2, LW = 18, LP0 = LH * LW;           // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
+    static constexpr int LP = LP0 + ((16 - LP0 % 32) + 32) % 32;
+    static constexpr int LNT = (LP0 + 15) / 16;                         // window N-tiles (12)
+    static constexpr int SR = 4 * LH, SC = 72;                          // shuffled map: row 0 = Y0 - 4, col 0 = X0 - 4
+    static constexpr int XR = 4 * L + 5, XC = 72;                       // x: row 0 = Y0 - 3, col 0 = X0 - 4
+    static constexpr int TQ = 18, TITEMS = XR * TQ;                      // tail items (x row, column quad)
+    static constexpr int QR = 2 * L + 2, QW = 34, QWP = 36;             // c1: row 0 = oy0 - 1, col 0 = ox0 - 1
+    static constexpr int QS0 = QR * QWP, QS = QS0 + ((16 - QS0 % 32) + 32) % 32;  // c1 channel stride (16 mod 32)
+    static constexpr int QP = QR * QW, QNT = (QP + 15) / 16;            // c1 pixels, N-tiles (39)
+    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = (OW_TB + 1 + 3) / 4 * 4,
+                         OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, OW_PS = OW_SH + C, OW_PH = OW_PS + NF,
+                         OW_PW = OW_PH + NF, OW_W2 = OW_PW + 9 * 16 * 16, OW_S2 = OW_W2 + 9 * C * C, OW_H2 = OW_S2 + C,
+                         WN = OW_H2 + C;
+    static constexpr int PR = L + 4, PW = 20, PCS = PR * PW, PXN = 16 * PCS;  // pre-conv window (PCS = 240: 16 mod 32)
+    static constexpr int POST = NF * SR * SC + XR * XC;
+    static constexpr int UN = POST > PXN ? POST : PXN;
+    static_assert(PCS % 32 == 16 && 16 * QS <= NF * SR * SC, "layout");
+};
+
+template <bool PRE>
+__global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_conv_desc d) {
+    using G = Sc7Geo;
+    constexpr int NF = G::NF, C = G::C, NT = G::NT, L = G::L, LW = G::LW, LP = G::LP, LP0 = G::LP0;
+    constexpr int SR = G::SR, SC = G::SC, XC = G::XC, WN = G::WN;
+    const esm_shuffle_tail_desc& a = d.st;
+    __shared__ __attribute__((aligned(16))) float wsh[WN];
+    __shared__ __attribute__((aligned(16))) float lr[NF * LP];
+    __shared__ __attribute__((aligned(16))) float un[G::UN];
+    float* const sh = un;                    // [NF][SR][SC]
+    float* const xs = un + NF * SR * SC;     // [XR][XC]
+    float* const pxs = un;                   // [16][PCS]  (PRE, until lr is built)
+    float* const qs = un;                    // c1 [C][QS] (over sh, once x is built)
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, HO = 4 * H, WO = 4 * W;
+    const int Ho2 = (HO + 1) / 2, Wo2 = (WO + 1) / 2;
+    const Blk3 bk_ = xcd_block((a.flags & 1) != 0);
+    const int b = bk_.z;
+    const int ly0 = bk_.y * L, lx0 = bk_.x * 16;
+    const int Y0 = 4 * ly0, X0 = 4 * lx0, oy0 = Y0 / 2, ox0 = X0 / 2;
+    SC4_STAMP(0);
+
+    // ---- 1. stage (one round trip): every weight and the pre-conv window (or the low-res window)
+    constexpr int WRN = (WN + NT - 1) / NT;
+    float rw[WRN];
+#pragma unroll
+    for (int k = 0; k < WRN; ++k) {
+        const int i = tid + k * NT;
+        const float* p;
+        int off;
+        float dflt = 0.f;
+        if (i < G::OW_UB) { p = a.up_w; off = i; }
+        else if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
+        else if (i < G::OW_TB) { p = a.tail_w; off = i - G::OW_TW; }
+        else if (i == G::OW_TB) { p = a.tail_b; off = 0; }
+        else if (i < G::OW_CW) { p = nullptr; off = 0; }
+        else if (i < G::OW_SC) { p = d.w; off = (i - G::OW_CW) / C * d.cin_pad * d.cout_pad + (i - G::OW_CW) % C; }
+        else if (i < G::OW_SH) { p = d.scale; off = i - G::OW_SC; dflt = 1.f; }
+        else if (i < G::OW_PS) { p = d.shift; off = i - G::OW_SH; }
+        else if (i < G::OW_PH) { p = PRE ? d.pre_scale : nullptr; off = i - G::OW_PS; dflt = 1.f; }
+        else if (i < G::OW_PW) { p = PRE ? d.pre_shift : nullptr; off = i - G::OW_PH; }
+        else if (i < G::OW_W2) {  // pre-conv A image [tap][ci][co 16] (co >= nf: zero rows)
+            const int j = i - G::OW_PW, co = j & 15, ci = (j >> 4) & 15, tap = j >> 8;
+            const bool ok = PRE && ci < d.pre_cin && co < NF;
+            p = ok ? d.pre_w : nullptr;
+            off = ok ? (tap * d.pre_cin_pad + ci) * d.pre_cout_pad + co : 0;
+        } else if (i < G::OW_S2) {  // second conv A image [tap][ci][co]
+            const int j = i - G::OW_W2, co = j & 15, ci = (j >> 4) & 15, tap = j >> 8;
+            p = d.w2;
+            off = (tap * d.cin_pad2 + ci) * d.cout_pad2 + co;
+        } else if (i < G::OW_H2) { p = d.scale2; off = i - G::OW_S2; dflt = 1.f; }
+        else { p = d.shift2; off = i - G::OW_H2; }
+        const bool ok = i < WN && p != nullptr;
+        const float v = (ok ? p : a.up_w)[ok ? off : 0];
+        rw[k] = ok ? v : dflt;
+    }
+    constexpr int PXR = PRE ? (G::PXN + NT - 1) / NT : 1;
+    constexpr int XRN = PRE ? 1 : (NF * LP + NT - 1) / NT;
+    float rp[PXR], rx[XRN];
+    if constexpr (PRE) {
+        const float* pb = d.pre_x + b * d.pb;
+#pragma unroll
+        for (int k = 0; k < PXR; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / G::PCS, rem = i - c * G::PCS;
+            const int yy = ly0 - 2 + rem / G::PW, xx = lx0 - 2 + rem % G::PW;
+            const bool ok = i < G::PXN && c < d.pre_cin && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = pb[ok ? c * d.pc + yy * d.ph + xx : 0];
+            rp[k] = ok ? v : 0.f;
+        }
+    } else {
+        const float* xb = a.x + b * a.xb;
+#pragma unroll
+        for (int k = 0; k < XRN; ++k) {
+            const int i = tid + k * NT;
+            const int c = i / LP, rem = i - c * LP;
+            const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
+            const bool ok = i < NF * LP && rem < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
+            rx[k] = ok ? v : 0.f;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < WRN; ++k)
+        if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < PXR; ++k)
+            if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < XRN; ++k)
+            if (tid + k * NT < NF * LP) lr[tid + k * NT] = rx[k];
+    }
+    __syncthreads();
+    SC4_STAMP(1);
+
+    // ---- 2. pre-conv on the low-res window (shuffle_conv4_kernel's MFMA form)
+    if constexpr (PRE) {
+        for (int nt = wave; nt < G::LNT; nt += L) {
+            const int p = nt * 16 + n;
+            const int pp = p < LP0 ? p : 0;
+            const int py = pp / LW, px = pp - (pp / LW) * LW;
+            conv::floatx4 acc2[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int ci = 4 * ks + g;
+                    acc2[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        wsh[G::OW_PW + (tap * 16 + ci) * 16 + n], pxs[ci * G::PCS + (py + dy) * G::PW + px + dx],
+                        acc2[ks & 1], 0, 0, 0);
+                }
+            }
+            const conv::floatx4 acc = acc2[0] + acc2[1];
+            const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
+            const bool in = p < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            if (g < 2 && p < LP0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g + j;
+                    const float v = gelu_erf(acc[j] * wsh[G::OW_PS + co] + wsh[G::OW_PH + co]);
+                    lr[co * LP + p] = in ? v : 0.f;
+                }
+            }
+        }
+        __syncthreads();  // lr complete; the pre-conv window (aliased by sh) is dead
+    }
+    SC4_STAMP(2);
+
+    // ---- 3. shuffled map on the whole window: item (window tile, channel), 16x16x4 MFMA
+    for (int it = wave; it < G::LNT * NF; it += L) {
+        const int wt = it >> 3, c = it & 7;
+        const int p = wt * 16 + n;
+        const int pp = p < LP0 ? p : 0;
+        const int py = pp / LW, px = pp - (pp / LW) * LW;
+        conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wsh[(c * 16 + n) * NF + 4 * kk + g], lr[(4 * kk + g) * LP + pp],
+                                                      acc, 0, 0, 0);
+        const int row = 4 * py + g;  // sh row: Y0 - 4 + row
+        const int Y = Y0 - 4 + row, X = X0 - 4 + 4 * px;
+        const bool yok = Y >= 0 && Y < HO;
+        conv::floatx4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
+            o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+        }
+        if (p < LP0) *reinterpret_cast<conv::floatx4*>(&sh[(c * SR + row) * SC + 4 * px]) = o;
+    }
+    __syncthreads();
+    SC4_STAMP(3);
+
+    // ---- 4. tail -> x rows Y0 - 3 .. Y0 + 33, cols X0 - 4 + 4q .. + 3 (q = 0 .. 17; cols X0 - 3 .. X0 + 65 used)
+    {
+        const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
+        for (int it = tid; it < G::TITEMS; it += NT) {
+            const int r = it / G::TQ, q = it - (it / G::TQ) * G::TQ;
+            const int cl = 4 * q - 1 < 0 ? 0 : 4 * q - 1, cr = 4 * q + 4 < SC ? 4 * q + 4 : SC - 1;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+            for (int c = 0; c < NF; ++c) {
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky) {
+                    const float* row = &sh[(c * SR + r + ky) * SC];
+                    const conv::floatx4 m4 = *reinterpret_cast<const conv::floatx4*>(row + 4 * q);
+                    const float v[6] = {row[cl], m4[0], m4[1], m4[2], m4[3], row[cr]};
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const float w = wsh[G::OW_TW + (c * 3 + ky) * 3 + kx];
+                        const f2v w2 = {w, w};
+                        const f2v lo = __builtin_elementwise_fma(w2, f2v{v[kx], v[1 + kx]}, f2v{acc[0], acc[1]});
+                        const f2v hi = __builtin_elementwise_fma(w2, f2v{v[2 + kx], v[3 + kx]}, f2v{acc[2], acc[3]});
+                        acc[0] = lo[0];
+                        acc[1] = lo[1];
+                        acc[2] = hi[0];
+                        acc[3] = hi[1];
+                    }
+                }
+            }
+            const int Y = Y0 - 3 + r;
+            conv::floatx4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int X = X0 - 4 + 4 * q + j;
+                o[j] = (Y >= 0 && Y < HO && X >= 0 && X < WO) ? acc[j] + tb : 0.f;  // the first conv's zero padding
+            }
+            *reinterpret_cast<conv::floatx4*>(&xs[r * XC + 4 * q]) = o;
+        }
+    }
+    __syncthreads();
+    SC4_STAMP(4);
+
+    // ---- 5. c1 = GELU(BN(conv 3x3 s2 (x))) on rows oy0 - 1 .. oy0 + 16, cols ox0 - 1 .. ox0 + 32 (612 pixels in 16-
+    //         pixel N-tiles), zero outside the map (the second conv's padding) -> LDS
+    {
+        float ca[3], sc[4], shf[4];
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+            const int t = 4 * s3 + g;
+            ca[s3] = t < 9 ? wsh[G::OW_CW + t * C + n] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = wsh[G::OW_SC + 4 * g + j];
+            shf[j] = wsh[G::OW_SH + 4 * g + j];
+        }
+        for (int nt = wave; nt < G::QNT; nt += L) {
+            const int p = nt * 16 + n;
+            const int pp = p < G::QP ? p : 0;
+            const int qa = pp / G::QW, qb = pp - (pp / G::QW) * G::QW;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3) {
+                const int t = 4 * s3 + g;
+                const int tt = t < 9 ? t : 8;
+                const int ky = tt / 3, kx = tt - (tt / 3) * 3;
+                const float bv = xs[(2 * qa + ky) * XC + 2 * qb + kx + 1];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[s3], t < 9 ? bv : 0.f, acc, 0, 0, 0);
+            }
+            const int oy = oy0 - 1 + qa, ox = ox0 - 1 + qb;
+            const bool in = p < G::QP && oy >= 0 && oy < Ho2 && ox >= 0 && ox < Wo2;
+            if (p < G::QP) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = gelu_erf(acc[j] * sc[j] + shf[j]);
+                    qs[(4 * g + j) * G::QS + qa * G::QWP + qb] = in ? v : 0.f;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    SC4_STAMP(5);
+
+    // ---- 6. the second conv (3x3 16 -> 16, BN, GELU) on the 16 x 32 output tile: N-tile = 16 pixels of one row,
+    //         two tiles per wave iteration on independent accumulators; lane (g, n): k-step (tap, ks) reads channel
+    //         4ks + g of pixel n; C lane (g, n): couts 4g .. 4g + 3
+    {
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            d.out + b * d.ob, static_cast<short>(0), static_cast<int>(4 * ((C - 1) * d.oc + (Ho2 - 1) * d.oh + Wo2)),
+            0x00020000);
+        float sc[4], shf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = wsh[G::OW_S2 + 4 * g + j];
+            shf[j] = wsh[G::OW_H2 + 4 * g + j];
+        }
+        for (int nt = 2 * wave; nt < 4 * L; nt += 2 * L) {
+            conv::floatx4 acc[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int ci = 4 * ks + g;
+                    const float av = wsh[G::OW_W2 + (tap * 16 + ci) * 16 + n];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int t2 = nt + u;
+                        const int oyl = t2 >> 1, oxl = 16 * (t2 & 1) + n;
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            av, qs[ci * G::QS + (oyl + dy) * G::QWP + oxl + dx], acc[u], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t2 = nt + u;
+                const int oy = oy0 + (t2 >> 1), ox = ox0 + 16 * (t2 & 1) + n;
+                const bool ok = oy < Ho2 && ox < Wo2;
+                const unsigned pix = 4u * static_cast<unsigned>(oy * d.oh + ox);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g + j;
+                    const float v = gelu_erf(acc[u][j] * sc[j] + shf[j]);
+                    conv::store_b32(__float_as_uint(v), ro,
+                                    static_cast<int>(ok ? pix + 4u * static_cast<unsigned>(co * d.oc) : conv::kOOB), 0);
+                }
+            }
+        }
+    }
+    SC4_STAMP(6);
+#ifdef ESM_CONV_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    SC4_STAMP(7);
+#endif
+}
+
+int launch_sc11(const esm_shuffle_conv_desc& a, hipStream_t s) {
+    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, Sc7Geo::L), a.st.B);
+    if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
+    if (a.pre_x)
+        hipLaunchKernelGGL((shuffle_conv11_kernel<true>), grid, dim3(Sc7Geo::NT), 0, s, a);
+    else
+        hipLaunchKernelGGL((shuffle_conv11_kernel<false>), grid, dim3(Sc7Geo::NT), 0, s, a);
+    return check_launch("shuffle_conv");
+}
+
 template <int L, bool MC1 = false>
 int launch_sc4(const esm_shuffle_conv_desc& a, hipStream_t s) {
     const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, L), a.st.B);
@@ -1034,6 +1368,13 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
     const long long Ho2 = (static_cast<long long>(t.H) * t.r + 1) / 2, Wo2 = (static_cast<long long>(t.W) * t.r + 1) / 2;
     if (a.oh < Wo2 || a.oc < Ho2 * a.oh || a.ob < a.C * a.oc) return arg_error("shuffle_conv: output strides");
     if (4 * (a.C * a.oc) >= 0x7fffffffLL) return arg_error("shuffle_conv: output too large");
+    if (a.w2) {  // the second conv fused (the row form only)
+        if (!(t.nf == 8 && t.r == 4 && a.C == 16) || (t.flags >> 1 & 3) == 1)
+            return arg_error("shuffle_conv: the second conv needs nf 8, r 4, C 16 and the row form");
+        if (a.cin_pad2 < a.C || a.cout_pad2 < a.C || a.cin_pad2 % 16 || a.cout_pad2 % 32)
+            return arg_error("shuffle_conv: bad second-conv weight padding");
+        return launch_sc11(a, s);
+    }
     if (t.nf == 8 && t.r == 4 && a.C == 16) {
         // st.flags bits 1-2: 0 automatic, 1 the window form, 2 the row form (shuffle_conv4_kernel, 8 low-res
         // rows per workgroup); automatic: the row form where it gives >= 128 workgroups

@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(NTH) fmnet_kernel(const esm_fmnet_desc a) {
                     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
                         for (int kx = 0; kx < 3; ++kx) acc += w0[c * 9 + ky * 3 + kx] * s3[(c * CH + py + ky) * CW + px + kx];
-                sh[hc * NPX + pp] = silu(acc + lw_cv0[HID * C * 9 + hc]);
+                sh[hc * NPX + pp] = silu_fast(acc + lw_cv0[HID * C * 9 + hc]);
             }
         } else {  // C = 16: a wave owns HID / 8 hidden channels (scalar weight loads), a lane one pixel
             constexpr int HPW = HID / NWAVES;
@@ -525,7 +525,7 @@ __global__ void __launch_bounds__(NTH) fmnet_kernel(const esm_fmnet_desc a) {
 #pragma unroll
                 for (int j = 0; j < HPW; ++j) {
                     const int hc = wave * HPW + j;
-                    sh[hc * NPX + lane] = silu(acc[j] + a.conv0_b[hc]);
+                    sh[hc * NPX + lane] = silu_fast(acc[j] + a.conv0_b[hc]);
                 }
             }
         }
@@ -867,7 +867,7 @@ __global__ void __launch_bounds__(kF2Threads) fm2b_kernel(const esm_fmnet_desc a
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int h = 16 * mt + 4 * g + j;
-                if (h < HID) sd[h * (TH * TW) + pp] = silu(acc[nt][mt][j] + w0[W0 + h]);
+                if (h < HID) sd[h * (TH * TW) + pp] = silu_fast(acc[nt][mt][j] + w0[W0 + h]);
             }
     }
     __syncthreads();

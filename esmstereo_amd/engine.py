@@ -967,6 +967,11 @@ SC_FORM = int(_ab("ESM_SC_FORM", "0"))
 SHUFFLE_PRE_ENABLED = _ab("ESM_SHUFFLE_PRE", "1") != "0"
 
 
+# the refinement's conv1[1] inside the same launch as well (esm_shuffle_conv_desc.w2, the whole conv1 of the 4x
+# stage in one launch; ESM_SC11=0: conv1[1] as its own launch, A/B measurements)
+SC11_ENABLED = _ab("ESM_SC11", "1") != "0"
+
+
 def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: PackedConv) -> bool:
     """Whether ``pre`` (BasicConv(Cp <= 16, nf, 3, 1, 1), BN + GELU) can run inside the row-form launch."""
     return SHUFFLE_PRE_ENABLED and shuffle_conv_supported(p, conv) and (p.nf, p.r, conv.cout) == (8, 4, 16) and \
@@ -975,13 +980,16 @@ def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: Pack
 
 
 def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: PackedConv,
-                     tag: str = "shuffle_conv", form: int = 0, pre: Optional[PackedConv] = None) -> torch.Tensor:
+                     tag: str = "shuffle_conv", form: int = 0, pre: Optional[PackedConv] = None,
+                     conv2: Optional[PackedConv] = None) -> torch.Tensor:
     """``conv(tail(SiLU(PixelShuffle(r)(up(x)))))`` with ``conv`` = up_refinement.conv1[0] (BasicConv(1, C,
     3, 2, 1): BN + GELU), one launch (``esm_shuffle_conv_f32``); the 1-channel map between them is never
     stored.  Returns the conv output [B, C, ceil(r*H/2), ceil(r*W/2)].  ``form`` (nf 8, r 4, C 16): 0
     automatic, 1 the window form, 2 the row form (8 low-res rows), 3 the row form with the refinement conv on
     the matrix cores.  ``pre`` (nf 8, r 4, C 16): ``x`` is then the input of
-    ``pre`` (the stage's spx_<t>[1], BasicConv(Cp, nf, 3, 1, 1)), computed inside the launch as well."""
+    ``pre`` (the stage's spx_<t>[1], BasicConv(Cp, nf, 3, 1, 1)), computed inside the launch as well.
+    ``conv2`` (with ``pre``): up_refinement.conv1[1] (BasicConv(C, C, 3, 1, 1)) too; the result is then its
+    output (the whole conv1), the first conv's map never stored."""
     require_device(x, "shuffle_conv input")
     B, nf, H, W = (int(v) for v in x.shape)
     r = p.r
@@ -1031,17 +1039,33 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
     d.ob, d.oc, d.oh = out.stride(0), out.stride(1), out.stride(2)
     d.C, d.cin_pad, d.cout_pad = conv.cout, conv.cin_pad, conv.cout_pad
     ctx.hold(x, out, p.up_w, p.up_b, p.tail_w, p.tail_b, conv.w, conv.scale, conv.shift)
+    if conv2 is not None:
+        if pre is None or (p.nf, p.r, conv.cout) != (8, 4, 16) or conv2.nd != 2 or conv2.transposed or \
+                (conv2.k, conv2.stride, conv2.pad, conv2.cin, conv2.cout) != (3, 1, 1, conv.cout, conv.cout) or \
+                conv2.act != ACT_GELU:
+            raise ValueError("shuffle_conv: the fused second conv must be BasicConv(C, C, 3, 1, 1) behind the "
+                             "(8, 4, 16) row form with its pre-conv")
+        require_on(x.device, "shuffle_conv second conv", conv2.w, conv2.scale, conv2.shift)
+        d.w2 = conv2.w.data_ptr()
+        d.scale2 = conv2.scale.data_ptr() if conv2.scale is not None else None
+        d.shift2 = conv2.shift.data_ptr() if conv2.shift is not None else None
+        d.cin_pad2, d.cout_pad2 = conv2.cin_pad, conv2.cout_pad
+        ctx.hold(conv2.w, conv2.scale, conv2.shift)
     npix = B * H * W * r * r
     flops = 2 * npix * nf * (nf + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9  # head as shuffle_tail + the 1 -> C 3x3
     cin_read = nf
     if pre is not None:  # + the 3x3 Cp -> nf pre-conv on the low-resolution map, whose weights are read too
         flops += 2 * B * H * W * nf * pre.cin * 9
         cin_read = pre.cin
+    if conv2 is not None:  # + the 3x3 C -> C second conv on the output map
+        flops += 2 * B * Ho2 * Wo2 * conv.cout * conv.cout * 9
     ctx.meta.append(dict(name=tag, kind="shuffle_conv", flops=flops,
                          bytes=4 * (B * cin_read * H * W + B * conv.cout * Ho2 * Wo2) +
-                         (4 * 9 * pre.cin * nf if pre is not None else 0),
+                         (4 * 9 * pre.cin * nf if pre is not None else 0) +
+                         (4 * 9 * conv.cout * conv.cout if conv2 is not None else 0),
                          shape=(f"pre {pre.cin}->{nf} k3 " if pre is not None else "") +
-                         f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}",
+                         f"nf{nf} r{r} in {H}x{W} -> x {H * r}x{W * r} -> C{conv.cout} {Ho2}x{Wo2}" +
+                         (f" -> k3 C{conv.cout}" if conv2 is not None else ""),
                          reads=_spans(x), writes=_spans(out)))
     ctx.shuffle_conv(d)
     return out

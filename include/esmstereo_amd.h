@@ -247,6 +247,14 @@ typedef struct {
     const float* pre_scale;
     const float* pre_shift;
     int32_t pre_cin, pre_cin_pad, pre_cout_pad, pre_reserved;
+    /* Optional second conv (nf 8, r 4, C 16 row form with pre_x only): with w2 set, the refinement's
+     * conv1[1] (BasicConv(C, C, 3, 1, 1): folded BN scale2 / shift2 (scale2 NULL = 1) + exact GELU, packed
+     * w2 [9][cin_pad2][cout_pad2]) runs in the same launch on the first conv's map, which is never stored:
+     * `out` receives conv1[1]'s output (same shape and strides). */
+    const float* w2;
+    const float* scale2;
+    const float* shift2;
+    int32_t cin_pad2, cout_pad2;
 } esm_shuffle_conv_desc;
 
 /* Depthwise KxK conv (groups = C, no bias) + folded BN (out = act(conv * scale[c] + shift[c]); scale NULL = 1,

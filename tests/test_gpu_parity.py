@@ -731,6 +731,14 @@ def test_shuffle_conv_pre(cp, H, W):
         assert y.shape == ref.shape
         assert rel(y, ref) < 1e-5, form
         assert rel(y, two) < 1e-5, form
+    # round 5: up_refinement.conv1[1] (BasicConv(16, 16, 3, 1, 1)) fused behind it: the whole conv1 in one launch
+    conv2, bn2 = _mk(2, 16, 16, 3, 1, 1, seed=H + 2)
+    ref2 = _ref_conv([ref.double()], conv2, bn2, ACT_GELU)
+    pc2 = pk(conv2, bn2, ACT_GELU)
+    y2 = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp, conv2=pc2)
+    assert y2.shape == ref2.shape
+    assert rel(y2, ref2) < 1e-5
+    assert rel(y2, run_conv(ctx, pc2, [y])) < 1e-5
 
 
 PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones

@@ -130,6 +130,9 @@ def test_plan_per_op_cost(case):
             if kind == "shuffle_tail":
                 assert op["flops"] == head and op["bytes"] == 4 * (B * nf * hi * wi + npix), name
             else:
+                g3 = re.search(r" -> k3 C(\d+)$", shape)  # round 5: up_refinement.conv1[1] fused behind it
+                if g3:
+                    shape = shape[:g3.start()]
                 g2 = re.search(r"C(\d+) (\d+)x(\d+)$", shape)
                 c, ho, wo = (int(v) for v in g2.groups())
                 gp = re.match(r"pre (\d+)->(\d+) k3 ", shape)  # the stage's spx_<t>[1] inside the launch
@@ -138,8 +141,13 @@ def test_plan_per_op_cost(case):
                     spx1 = _layer(m, name.split("+")[0])
                     assert tuple(spx1.weight.shape) == (nf, cp, 3, 3), name
                 pre_f = 2 * B * hi * wi * nf * cp * 9
-                assert op["flops"] == head + 2 * B * ho * wo * c * 9 + pre_f, name
-                assert op["bytes"] == 4 * (B * (cp or nf) * hi * wi + B * c * ho * wo) + 4 * 9 * cp * nf, name
+                c2f, c2b = 0, 0
+                if g3:
+                    conv11 = _layer(m, name.split(".", 1)[0] + "." + name.rsplit("+", 1)[-1] + ".1")
+                    assert tuple(conv11.weight.shape) == (c, c, 3, 3), name
+                    c2f, c2b = 2 * B * ho * wo * c * c * 9, 4 * 9 * c * c
+                assert op["flops"] == head + 2 * B * ho * wo * c * 9 + pre_f + c2f, name
+                assert op["bytes"] == 4 * (B * (cp or nf) * hi * wi + B * c * ho * wo) + 4 * 9 * cp * nf + c2b, name
         elif kind == "fmnet":
             g = re.search(r"C(\d+) (\d+)x(\d+) dw(\d+)", shape)
             C, hh, ww, k = (int(v) for v in g.groups())
@@ -169,5 +177,8 @@ def test_shuffle_head_flops_s_k():
     if op["name"].endswith("+ref4x.conv1.0"):
         assert op["kind"] == "shuffle_conv"
         assert op["flops"] == head + 2 * 192 * 624 * 16 * 9 + pre
+    elif op["name"].endswith("+ref4x.conv1"):  # round 5: conv1[1] (3x3 16 -> 16 on 192 x 624) in the launch too
+        assert op["kind"] == "shuffle_conv"
+        assert op["flops"] == head + 2 * 192 * 624 * 16 * 9 + pre + 2 * 192 * 624 * 16 * 16 * 9
     else:
         assert op["flops"] == head
