@@ -102,6 +102,7 @@ SIGNATURES = {
     "esm_version": (c_int, []),
     "esm_struct_size": (c_int, [c_int]),
     "esm_gwc_volume_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6 + [c_void_p]),
+    "esm_gwc_stem_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "esm_concat_volume_f32": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "esm_normcorr_volume_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "esm_disp_regression_f32": (c_int, [c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
@@ -127,6 +128,7 @@ SIGNATURES = {
     "esm_plan_add_shuffle_conv": (c_int, [c_void_p, POINTER(EsmShuffleConvDesc)]),
     "esm_plan_add_conv_pair2": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
+    "esm_plan_add_gwc_stem": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_normcorr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),
     "esm_plan_add_regression": (c_int, [c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 4),

@@ -20,6 +20,8 @@ int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 int launch_shuffle_conv(const esm_shuffle_conv_desc*, hipStream_t);
 namespace conv {
 int launch_pair2(const esm_conv_desc&, const esm_conv_desc&, hipStream_t);
+int gwc_stem_check(const esm_conv_desc&, const float*, const float*, int, int);                // gwc_stem.hip
+int launch_gwc_stem(const esm_conv_desc&, const float*, const float*, int, int, hipStream_t);  // gwc_stem.hip
 }
 int launch_conf(const esm_conf_desc*, hipStream_t);
 
@@ -36,7 +38,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12, kPair2 = 13 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12, kPair2 = 13, kGwcStem = 14 };
 
 struct VolArgs {
     const float* L;
@@ -77,6 +79,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kShuffleConv: return esm::launch_shuffle_conv(&op.sc, s);
         case kPair2: return esm::conv::launch_pair2(op.conv, op.conv2, s);
         case kConf: return esm::launch_conf(&op.cf, s);
+        case kGwcStem: return esm::conv::launch_gwc_stem(op.conv, op.vol.L, op.vol.R, op.vol.C, op.vol.G, s);
         case kGwc:
             return esm::launch_gwc(op.vol.L, op.vol.R, op.vol.att, op.vol.V, op.vol.B, op.vol.C, op.vol.H, op.vol.W,
                                    op.vol.D, op.vol.G, s);
@@ -228,6 +231,7 @@ struct esm_plan {
         switch (op.kind) {
             case kConv: return rb.conv(op.conv);
             case kPair2: return rb.conv(op.conv) + rb.conv(op.conv2);
+            case kGwcStem: return rb.conv(op.conv) + rb(op.vol.L) + rb(op.vol.R);
             case kSmix: {
                 int n = rb(op.smix.x) + rb(op.smix.out) + rb(op.smix.res) + rb(op.smix.dw_w) + rb(op.smix.dw_b);
                 for (int k = 0; k < op.smix.nstages && k < ESM_SMIX_MAX_STAGES; ++k) n += rb.stage(op.smix.stage[k]);
@@ -406,6 +410,17 @@ int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float
     Op op;
     op.kind = kGwc;
     op.vol = VolArgs{L, R, att, V, nullptr, B, C, H, W, D, G};
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_gwc_stem(esm_plan* plan, const esm_conv_desc* stem, const float* L, const float* R, int C, int G) {
+    if (!stem) return esm::arg_error("plan: null gwc_stem desc");
+    const int rc = esm::conv::gwc_stem_check(*stem, L, R, C, G);
+    if (rc != ESM_OK) return rc;
+    Op op;
+    op.kind = kGwcStem;
+    op.conv = *stem;
+    op.vol = VolArgs{L, R, nullptr, nullptr, nullptr, stem->B, C, stem->Hi, stem->Wi, stem->Di, G};
     return add_op(plan, std::move(op));
 }
 

@@ -377,6 +377,15 @@ class Ctx:
             check(lib.esm_gwc_volume_f32(L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G, self.stream),
                   "gwc")
 
+    def gwc_stem(self, d: EsmConvDesc, L, R, C: int, G: int) -> None:
+        if not self._submit():
+            return
+        if self.plan:
+            self.hold(L, R)
+            check(lib.esm_plan_add_gwc_stem(self.plan, ctypes.byref(d), L.data_ptr(), R.data_ptr(), C, G), "gwc_stem")
+        else:
+            check(lib.esm_gwc_stem_f32(ctypes.byref(d), L.data_ptr(), R.data_ptr(), C, G, self.stream), "gwc_stem")
+
     def concat(self, L, R, V, B, C, H, W, D) -> None:
         self.meta.append(dict(name="concat_volume", kind="concat", flops=0,
                               bytes=4 * B * (2 * C * H * W + 2 * C * D * H * W), reads=_spans(L, R), writes=_spans(V)))
@@ -642,6 +651,42 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
                       f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
                 reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint)
     return d, out, meta
+
+
+# The gwc volume and group_stem as one launch (esm_gwc_stem_f32, gwc_stem.hip) on the volumes the LDS-tiled
+# stem takes (ESMStereo-L / -M); ESM_GWC_STEM=0 keeps the two launches (A/B measurements)
+GWC_STEM_ENABLED = _ab("ESM_GWC_STEM", "1") != "0"
+
+
+def gwc_stem_supported(pc: PackedConv, L: torch.Tensor, G: int, D: int, att) -> bool:
+    """Python mirror of gwc_stem.hip gwc_stem_check, restricted to where the fused form replaces the tiled
+    stem (tile3_auto: >= 2^16 output voxels; the S volumes keep their row-streaming stem)."""
+    if att is not None or pc.nd != 3 or pc.transposed or (pc.k, pc.stride, pc.pad) != (3, 1, 1):
+        return False
+    B, C, H, W = (int(v) for v in L.shape)
+    if pc.cin != G or G % 4 or C != 2 * G or pc.cout > 8 or not L.is_contiguous():
+        return False
+    return B * D * H * W >= (1 << 16) and 4 * C * H * W < (1 << 30) and 4 * pc.cout * D * H * W < (1 << 30)
+
+
+def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, G: int, D: int,
+                 tag: str = "gwc_volume+group_stem", hint: int = 0) -> torch.Tensor:
+    """``group_stem(build_gwc_volume(L, R, D, G))`` (models/submodule.py:151-161, models/ESMStereo.py:703-704)
+    as one launch: the volume is formed in LDS per k-step and never written (bit-identical to the two
+    launches with the tiled stem)."""
+    B, C, H, W = (int(v) for v in L.shape)
+    if tuple(R.shape) != (B, C, H, W) or not R.is_contiguous() or not L.is_contiguous():
+        raise ValueError("gwc_stem: L and R must be contiguous tensors of one shape")
+    virt = L.as_strided((B, G, D, H, W), (0, 0, 0, 0, 1))  # the volume's geometry only, never read
+    d, out, meta = _conv_desc(ctx, pc, [virt], tag=tag, hint=hint)
+    d.hint &= HINT_XCD_SLAB | (3 << 26)  # tile order and rows per wave; a standalone stem's form bits do not apply
+    vol_flops = 2 * B * C * D * H * W
+    meta.update(kind="gwc_stem", flops=meta["flops"] + vol_flops,
+                bytes=4 * B * 2 * C * H * W + 4 * B * pc.cout * D * H * W + 4 * pc.cin * pc.cout * 27,
+                reads=_spans(L, R), shape=f"gwc G{G} D{D} + " + meta["shape"])
+    ctx.meta.append(meta)
+    ctx.gwc_stem(d, L, R, C, G)
+    return out
 
 
 # Two consecutive 2-D BasicConvs as one launch (esm_conv_pair2_f32, conv_pair2.hip); ESM_PAIR2=0

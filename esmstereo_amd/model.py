@@ -38,7 +38,9 @@ from . import _lib
 from ._lib import check, lib
 from .backbone import Feature, fast_path_ok
 from .blocks import BasicConv, Conv2x, aggregation, upsample4, upsample8, upsample16
-from .engine import ACT_NONE, ACT_RELU, Ctx, cached_pack, pack_conv, require_device, run_conv
+from . import engine as _engine
+from .engine import (ACT_NONE, ACT_RELU, Ctx, cached_pack, gwc_stem_supported, pack_conv, require_device, run_conv,
+                     run_gwc_stem)
 
 __all__ = ["ESMStereo", "ESMStereo_trt", "ESMStereo_confidence", "FeatUp", "HotPath", "plan_ops"]
 
@@ -548,9 +550,14 @@ class ESMStereo(nn.Module):
         vs = self.vol_size
         if self.gwc:
             a = att.reshape(B, self.num_groups, h, w) if (vs == 16 and att is not None) else None
-            V = ctx.empty(B, self.num_groups, D, h, w)
-            ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
-            vol = self.group_stem.emit(ctx, [V])
+            pc = self.group_stem.packed()
+            if _engine.GWC_STEM_ENABLED and gwc_stem_supported(pc, ml, self.num_groups, D, a):
+                vol = run_gwc_stem(ctx, pc, ml, mr, self.num_groups, D,
+                                   tag=f"gwc_volume+{self.group_stem._esm_name}")
+            else:
+                V = ctx.empty(B, self.num_groups, D, h, w)
+                ctx.gwc(ml, mr, a, V, B, C, h, w, D, self.num_groups)
+                vol = self.group_stem.emit(ctx, [V])
         elif self.norm_correlation:
             V = ctx.empty(B, 1, D, h, w)
             work = ctx.empty(2, B, C, h, w)

@@ -282,6 +282,13 @@ int esm_struct_size(int which);
 
 int esm_gwc_volume_f32(const float* L, const float* R, const float* att, float* V, int B, int C, int H, int W,
                        int D, int G, void* stream);
+/* The gwc volume and the first 3-D conv over it in one launch (ESMStereo-L / -M: build_gwc_volume,
+ * models/submodule.py:151-161, then group_stem, models/ESMStereo.py:610-611 / 703-704): `stem` describes the
+ * conv as esm_conv_f32 would take it over the [B, G, D, H, W] volume (Cin = G, Di x Hi x Wi = D x H x W,
+ * 3x3x3 stride 1 pad 1, <= 8 outputs; its src[] is ignored and no volume is written); L / R are contiguous
+ * [B, C, H, W] features with C = 2 G, G a multiple of 4.  Bit-identical to esm_gwc_volume_f32 followed by
+ * esm_conv_f32 with the LDS-tiled form (hint bit 23); bits 26-27 of stem->hint: rows per wave 2 / 4. */
+int esm_gwc_stem_f32(const esm_conv_desc* stem, const float* L, const float* R, int C, int G, void* stream);
 int esm_concat_volume_f32(const float* L, const float* R, float* V, int B, int C, int H, int W, int D,
                           void* stream);
 /* work: unused since the single-launch kernel (normalises in LDS); may be NULL.  C <= 64. */
@@ -370,6 +377,7 @@ int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc)
 int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
+int esm_plan_add_gwc_stem(esm_plan* plan, const esm_conv_desc* stem, const float* L, const float* R, int C, int G);
 int esm_plan_add_concat(esm_plan* plan, const float* L, const float* R, float* V, int B, int C, int H, int W,
                         int D);
 int esm_plan_add_normcorr(esm_plan* plan, const float* L, const float* R, float* V, float* work, int B, int C,
@@ -379,8 +387,8 @@ int esm_plan_add_regression(esm_plan* plan, int kind, const float* cost, float* 
 int esm_plan_add_conf(esm_plan* plan, const esm_conf_desc* desc);
 int esm_plan_num_ops(const esm_plan* plan);
 /* 0 = unknown, 1 = conv, 2 = smix, 3 = gwc, 4 = concat, 5 = normcorr, 6 = regression,
- * 7 = shuffle_tail, 9 = fmnet, 10 = conf, 12 = shuffle_conv, 13 = conv_pair2 (8 and 11 were retired
- * fused forms) */
+ * 7 = shuffle_tail, 9 = fmnet, 10 = conf, 12 = shuffle_conv, 13 = conv_pair2, 14 = gwc_stem (8 and 11
+ * were retired fused forms) */
 int esm_plan_op_kind(const esm_plan* plan, int index);
 /* Replace the tile hint of conv op `index` (see esm_conv_desc.hint); returns the previous hint
  * (>= 0) or an error.  Bit 30 (tile order) is kept as the op was added, and is not part of the

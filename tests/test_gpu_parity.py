@@ -306,6 +306,29 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
     assert rel(out2, want * 2.0) < 1e-5
 
 
+@pytest.mark.parametrize("B,G,D,H,W", [(1, 32, 12, 24, 78), (2, 32, 9, 13, 37), (1, 8, 5, 7, 20), (1, 4, 3, 5, 9),
+                                       (1, 32, 48, 96, 312), (2, 32, 10, 17, 70)])
+def test_gwc_stem_fused(B, G, D, H, W):
+    """The gwc volume + group_stem in one launch (gwc_stem.hip; ESMStereo-L / -M): bit-identical to the
+    two launches (gwc_volume, then the tiled stem: same staged window, same MFMA order and epilogue), for
+    every rows-per-wave variant, 1 / 2 / many k-steps and ragged extents; and vs fp64 torch (1e-5)."""
+    from esmstereo_amd.engine import run_gwc_stem
+    C = 2 * G
+    conv, bn = _mk(3, G, 8, 3, 1, 1, seed=G + D)
+    L, R = feature_pair(B, C, H, W, 7, max(D, 2))
+    Ld, Rd = L.to(DEV), R.to(DEV)
+    p = pk(conv, bn, ACT_GELU)
+    V = E.build_gwc_volume(Ld, Rd, D, G)
+    two = run_conv(Ctx(DEV), p, [V], hint=HINT_TILE3)
+    for hint in (0, 2 << 26, 3 << 26):
+        y = run_gwc_stem(Ctx(DEV), p, Ld, Rd, G, D, hint=hint)
+        assert torch.equal(y, two), (hex(hint), float((y - two).abs().max()))
+    if B * D * H * W <= 1 << 16:
+        assert rel(two, _ref_conv([O.gwc_volume(L, R, D, G)], conv, bn, ACT_GELU)) < 1e-5
+    with pytest.raises(E.EsmError):  # C != 2 G
+        run_gwc_stem(Ctx(DEV), p, Ld[:, :C - 4].contiguous(), Rd[:, :C - 4].contiguous(), G, D)
+
+
 @pytest.mark.parametrize("cin,cout,shape,B", [(40, 24, (6, 12, 39), 1), (72, 40, (3, 6, 20), 2), (24, 16, (5, 7, 17), 1),
                                               (40, 72, (3, 5, 9), 1), (16, 2, (4, 4, 20), 1)])
 def test_conv_tile3_transposed(cin, cout, shape, B):
@@ -1062,6 +1085,28 @@ def test_hot_path_full_size_vs_oracle(var, cv, B, H, W, maxdisp, noise):
         return
     for i, o in enumerate(outs):
         _check_disp(f"{tag} disp_{i}", o, ref[f"disp_{i}"])
+
+
+def test_hot_path_gwc_stem_ab():
+    """The L hot path with the fused gwc volume + group_stem launch equals the two-launch path bit for bit
+    (every output), at a size where the fused form is taken (>= 2^16 volume voxels)."""
+    from esmstereo_amd import engine
+    model, sd, m = _model_from_manifest("hot_L_gwc.npz")
+    ml, mr, att, up = _full_inputs(model, 2, 192, 624, 13, 192, False)
+    outs = {}
+    saved = engine.GWC_STEM_ENABLED
+    try:
+        for on in (True, False):
+            engine.GWC_STEM_ENABLED = on
+            model._plans.clear()
+            outs[on] = [o.clone() for o in model.hot_path(ml, mr, att, up, True)]
+            names = [x["name"] for x in model._plans[next(iter(model._plans))].ctx.meta]
+            assert ("gwc_volume+group_stem" in names) == on, names[:3]
+    finally:
+        engine.GWC_STEM_ENABLED = saved
+        model._plans.clear()
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("name", sorted(fullsize_manifest()))

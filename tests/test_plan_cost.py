@@ -32,7 +32,7 @@ CASES = {  # name: (variant, backbone, cv_scale, B, H, W, maxdisp)
     "L-K B4": ("L", "efficientnet_b2", 4, 4, 384, 1248, 192),
     "Mid": ("L", "efficientnet_b2", 4, 1, 1024, 1504, 256),
 }
-CONV_KINDS = ("conv", "conv_pair", "shuffle_tail", "shuffle_conv", "fmnet")
+CONV_KINDS = ("conv", "conv_pair", "shuffle_tail", "shuffle_conv", "fmnet", "gwc_stem")
 
 
 def _plan(case):
@@ -58,6 +58,8 @@ def test_plan_flops_equal_flop_counter_on_oracle(case):
     # the flop counter sees convolutions only: take out disparity_regression's 2·B·D·h·w where the first pair
     # of the upsampler computes it (the `disparity_regression+` pair)
     reg = sum(2 * B * (md // cvs) * h * w for x in meta if x["name"].startswith("disparity_regression+"))
+    # and the gwc volume's 2·B·C·D·h·w where the fused gwc_stem launch forms it (round 5)
+    reg += sum(2 * B * 64 * (md // cvs) * h * w for x in meta if x["kind"] == "gwc_stem")
     ours = sum(x["flops"] for x in meta if x["kind"] in CONV_KINDS) - reg
     assert ours == counted, (case, ours, counted, ours - counted)
 
@@ -160,6 +162,13 @@ def test_plan_per_op_cost(case):
             G = 32
             assert op["flops"] == 2 * B * 64 * D * h * w
             assert op["bytes"] == 4 * B * (2 * 64 * h * w + G * D * h * w + (G * h * w if cvs == 16 else 0))
+        elif kind == "gwc_stem":  # the volume formed in LDS, never written: features in, stem output out
+            g = re.search(r"in (\S+) out (\S+)", shape)
+            stem = _layer(m, name.split("+", 1)[1])
+            f, _, want, nout = _conv_cost(stem, B, _ext(g.group(1)), _ext(g.group(2)))
+            assert _ext(g.group(1)) == (D, h, w) and want == (D, h, w), name
+            assert op["flops"] == f + 2 * B * 64 * D * h * w, name
+            assert op["bytes"] == 4 * (B * 2 * 64 * h * w + nout + stem.weight.numel()), name
         elif kind == "regression":
             assert op["bytes"] == 4 * B * (D + 1) * h * w
         else:
