@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
                                                               const float* __restrict__ Rf, int C) {
     using G = GsGeo<NT, CPG>;
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, CS0 = G::CS0;
-    constexpr int XR = G::XR, WR = G::WR, LR = G::LR, RR = G::RR, NR = NT + 2;
+    constexpr int WR = G::WR, LR = G::LR, RR = G::RR, NR = NT + 2;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
     __shared__ __attribute__((aligned(16))) float ws[2][G::WE];
     __shared__ float fs[2][G::FE];  // [left: FC][IY][IX] then [right: FC][IY][RX]
@@ -86,18 +86,30 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
         const bool ok = f < G::RE && y >= 0 && y < H && x >= 0 && x < W;
         roff[k] = ok ? 4u * static_cast<unsigned>(c * HW + y * W + x) : kOOB;
     }
-    // this thread's volume elements: packed LDS indices of its (left, right) feature pair, bit 30 = the
-    // element exists (disparity plane inside [0, D), pixel inside the map, x >= d)
-    unsigned pk[XR];
+    // the volume window is built by columns: a thread owns window columns (ci, iy, ix) and forms all IZ
+    // disparity planes of each from one left value per channel and IZ consecutive right values (the
+    // shifts), NRND columns per thread (a thread past the last column repeats its first one: the same
+    // values to the same addresses).  cl / cr: LDS indices of the left value / the right value of plane
+    // 0 (channel CPG ci); cx: xs index of plane 0; vm: the elements that exist (bit r * IZ + iz:
+    // disparity plane inside [0, D), pixel inside the map, x >= d), the rest are the conv's zero padding
+    constexpr int IZ = G::IZ, NCOL = 4 * IY * IX, NRND = (NCOL + kGsThreads - 1) / kGsThreads;
+    static_assert(NCOL >= kGsThreads && NRND * IZ <= 32, "column plan");
+    unsigned cl[NRND], cr[NRND], cx[NRND], vm = 0;
 #pragma unroll
-    for (int k = 0; k < XR; ++k) {
-        const int e = tid + k * kGsThreads;
-        const int ci = e / CS0, r = e % CS0, iz = r / PLANE, iy = (r / IX) % IY, ix = r % IX;
-        const int d = zi0 + iz, y = yi0 + iy, x = xi0 + ix;
-        const bool ok = e < G::XE && d >= 0 && d < D && y >= 0 && y < H && x < W && x >= d;
-        const unsigned la = static_cast<unsigned>(CPG * ci * G::LW + iy * IX + ix);
-        const unsigned ra = static_cast<unsigned>(G::LE + CPG * ci * G::RW + iy * G::RX + ix - iz + G::IZ - 1);
-        pk[k] = e < G::XE ? (la | (ra << 15) | (ok ? 1u << 30 : 0u)) : 0u;
+    for (int r = 0; r < NRND; ++r) {
+        int col = tid + r * kGsThreads;
+        col = col < NCOL ? col : tid;
+        const int ci = col / (IY * IX), iy = (col / IX) % IY, ix = col % IX;
+        cl[r] = static_cast<unsigned>(CPG * ci * G::LW + iy * IX + ix);
+        cr[r] = static_cast<unsigned>(G::LE + CPG * ci * G::RW + iy * G::RX + ix + IZ - 1);
+        cx[r] = static_cast<unsigned>(ci * CS + iy * IX + ix);
+        const int y = yi0 + iy, x = xi0 + ix;
+#pragma unroll
+        for (int iz = 0; iz < IZ; ++iz) {
+            const int d = zi0 + iz;
+            const bool ok = d >= 0 && d < D && y >= 0 && y < H && x < W && x >= d;
+            vm |= (ok ? 1u : 0u) << (r * IZ + iz);
+        }
     }
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
@@ -142,26 +154,35 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
             if (e < G::WE) ws[buf][e] = wv[k];
         }
     };
-    // the volume window of one k-step from the staged feature windows (volumes.hip gwc_kernel's arithmetic)
-    auto volume = [&](int fb, int buf) __attribute__((always_inline)) {
-        const float inv = 1.0f / static_cast<float>(CPG);
+    // two planes (iz, iz + 1) of one column of a k-step's window from the staged feature windows
+    // (volumes.hip gwc_kernel's arithmetic: products and the pairwise sum rounded one operation at a time)
+    float lft[NRND][CPG];
+    auto load_left = [&](int fb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < XR; ++k) {
-            const int e = tid + k * kGsThreads;
-            if (k + 1 < XR || e < G::XE) {
-                const unsigned la = pk[k] & 0x7fffu, ra = (pk[k] >> 15) & 0x7fffu;
-                float s;
-                {
-#pragma clang fp contract(off)
-                    s = fs[fb][la] * fs[fb][ra];
+        for (int r = 0; r < NRND; ++r)
 #pragma unroll
-                    for (int c = 1; c < CPG; ++c) s = s + fs[fb][la + c * G::LW] * fs[fb][ra + c * G::RW];
-                    s = s * inv;
-                }
-                xs[buf][e + (e / CS0) * (CS - CS0)] = (pk[k] >> 30) ? s : 0.f;
-            }
-        }
+            for (int c = 0; c < CPG; ++c) lft[r][c] = fs[fb][cl[r] + c * G::LW];
     };
+    auto volume_pair = [&](int u, int fb, int buf) __attribute__((always_inline)) {
+        const int r = u / (IZ / 2), iz = 2 * (u % (IZ / 2));
+        const float inv = 1.0f / static_cast<float>(CPG);
+        float s0, s1;
+        {
+#pragma clang fp contract(off)
+            s0 = lft[r][0] * fs[fb][cr[r] - iz];
+            s1 = lft[r][0] * fs[fb][cr[r] - iz - 1];
+#pragma unroll
+            for (int c = 1; c < CPG; ++c) {
+                s0 = s0 + lft[r][c] * fs[fb][cr[r] + c * G::RW - iz];
+                s1 = s1 + lft[r][c] * fs[fb][cr[r] + c * G::RW - iz - 1];
+            }
+            s0 = s0 * inv;
+            s1 = s1 * inv;
+        }
+        xs[buf][cx[r] + iz * PLANE] = (vm >> (r * IZ + iz)) & 1u ? s0 : 0.f;
+        xs[buf][cx[r] + (iz + 1) * PLANE] = (vm >> (r * IZ + iz + 1)) & 1u ? s1 : 0.f;
+    };
+    constexpr int NU = NRND * IZ / 2;  // plane pairs per thread and k-step
 
     float scl[4], shf[4];
 #pragma unroll
@@ -174,42 +195,49 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+    // k-steps past the last one load zeros (range-checked offsets past the buffers) and build windows no
+    // MFMA reads, so the loop body has no branch between its MFMAs and the next window's work
     const int nchunk = a.Cin >> 2;
     fload(0);
     wload(0);
     fstore(0);
     wstore(0);
-    if (nchunk > 1) fload(1);
+    fload(1);
     __syncthreads();
-    volume(0, 0);
-    if (nchunk > 1) fstore(1);
+    load_left(0);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) volume_pair(u, 0, 0);
+    fstore(1);
     __syncthreads();
     for (int ch = 0; ch < nchunk; ++ch) {
         const int buf = ch & 1;
-        if (ch + 2 < nchunk) fload(ch + 2);
-        if (ch + 1 < nchunk) wload(ch + 1);
+        fload(ch + 2);
+        wload(ch + 1);
+        // keep the loads here: left to itself the scheduler sinks them below the MFMAs, next to the LDS
+        // stores that wait for them, and every k-step then waits out a full memory latency
+        __builtin_amdgcn_sched_barrier(0);
         const float* xw = &xs[buf][g * CS + n];
         const float* wp = &ws[buf][g * 16 + n];
+        load_left((ch + 1) & 1);
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
+        for (int it = 0; it < 12; ++it) {
+            const int p = it / 3, dx = it % 3;
+            float br[NR];
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-                float br[NR];
+            for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
 #pragma unroll
-                for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
+            for (int dy = 0; dy < 3; ++dy) {
+                const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy) {
-                    const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt], 0, 0, 0);
-                }
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt], 0, 0, 0);
             }
-        if (ch + 1 < nchunk) {
-            volume((ch + 1) & 1, buf ^ 1);
-            wstore(buf ^ 1);
+            // k-step ch + 1's volume window, spread over the MFMA stream
+#pragma unroll
+            for (int u = it; u < NU; u += 12) volume_pair(u, (ch + 1) & 1, buf ^ 1);
         }
-        if (ch + 2 < nchunk) fstore(ch & 1);
+        wstore(buf ^ 1);
+        fstore(ch & 1);
         __syncthreads();
     }
 
