@@ -357,6 +357,141 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
         if (ox0 + j < Wo) conv_put(a, conv_finish(a, acc[j], b, 0, oz, oy, ox0 + j), b, 0, oz, oy, ox0 + j);
 }
 
+// 3-D, register-blocked over the parity classes: a thread owns MX = 2 consecutive input-grid
+// positions m (along x) of one input-grid row and plane and computes all 8 parity classes of both, the
+// 2 x 2 x 4 output block (2m + q per dim).  Every class of m reads input m + p, p = q - t in {-1, 0, 1}
+// per dim, so per channel the thread reads the 3 x 3 rows of 4 input values around its positions once
+// (two 8-byte LDS reads per row) and does 128 FMAs with them (the per-class form above: 16 FMAs per 8
+// reads).  A workgroup (16 x 16 threads) owns a 16-row x 32-column input-grid tile of one plane: it
+// stages the 3 planes x 18 rows x 36 columns the tile reads, CC channels per chunk, double-buffered (one
+// barrier per chunk, the next chunk's loads in flight during this one's FMAs), and every weight of the
+// layer once ([c][cls][tap], wave-uniform LDS reads).  Each (qz, qy) class pair of a thread is 4
+// consecutive output columns: one 16-byte store.  Accumulation order per output: channel, plane tap,
+// row tap, column tap.
+constexpr int kC2TY = 16, kC2TX = 16, kC2MX = 2, kC2CC = 2;
+
+__global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_desc a) {
+    constexpr int MXW = kC2TX * kC2MX;            // input-grid columns per tile (32)
+    constexpr int IR = kC2TY + 2, IC = MXW + 4;   // staged rows / columns (m0 - 1 .. m0 + 34)
+    constexpr int NP = 3, CC = kC2CC;
+    constexpr int XN = NP * CC * IR * IC;
+    constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
+    constexpr int WCAP = 32 * 64;                 // [c < 32][cls 8][tap 8]
+    __shared__ __attribute__((aligned(16))) float xs[2][NP][CC][IR][IC];
+    __shared__ __attribute__((aligned(16))) float ws[WCAP];
+
+    const int tid = threadIdx.x;
+    const int Di = a.Di, Hi = a.Hi, Wi = a.Wi;
+    const Blk3 bk = xcd_block((a.hint & kHintXcd) != 0);
+    const int my0 = bk.y * kC2TY, mx0 = bk.x * MXW;
+    const int b = bk.z / Di;
+    const int mz = bk.z - b * Di;
+    const int sc = static_cast<int>(a.src[0].sc);
+    const __amdgpu_buffer_rsrc_t rs = c1_src_rsrc(a, b, true);
+    const C1Stage<XR, XN, NP, CC, IR, IC, IC> stg(a, tid, mz - 1, my0 - 1, mx0 - 1);
+    const int nch = (a.Cin + CC - 1) / CC;
+    float rx[XR];
+    stg.load(rx, rs, sc, 0, a.Cin);
+    {
+        constexpr int WR = WCAP / kC1Threads;
+        float rw[WR];
+#pragma unroll
+        for (int k = 0; k < WR; ++k) {  // ws[(c * 8 + cls) * 8 + tap] <- packed w[cls][tap][c][0]
+            const int i = tid + k * kC1Threads;
+            const int tap = i & 7, cls = (i >> 3) & 7, c = i >> 6;
+            const bool ok = c < a.Cin;
+            const float v = a.w[ok ? ((static_cast<long long>(cls) * 8 + tap) * a.cin_pad + c) * a.cout_pad : 0];
+            rw[k] = ok ? v : 0.f;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // every load issued before the first LDS store
+#pragma unroll
+        for (int k = 0; k < WR; ++k) ws[tid + k * kC1Threads] = rw[k];
+    }
+    stg.store(&xs[0][0][0][0][0], rx);
+    __syncthreads();
+
+    const int ty = tid / kC2TX, tx = tid % kC2TX;
+    // acc[qz][qy][j][qx]: output (2 mz + qz, 2 (my0 + ty) + qy, 2 (mx0 + 2 tx + j) + qx)
+    float acc[2][2][kC2MX][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < kC2MX; ++j) acc[i][k][j][0] = acc[i][k][j][1] = 0.f;
+    for (int ch = 0; ch < nch; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nch) stg.load(rx, rs, sc, (ch + 1) * CC, a.Cin);
+        __builtin_amdgcn_sched_barrier(0);  // the next chunk's loads stay ahead of this chunk's FMAs
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+            const float* wc = ws + (ch * CC + c) * 64;
+#pragma unroll
+            for (int pz = 0; pz < 3; ++pz)
+#pragma unroll
+                for (int py = 0; py < 3; ++py) {
+                    // input row m_y + py - 1 of plane m_z + pz - 1: columns m0 - 1 .. m0 + 2 (m0 = mx0 + 2 tx)
+                    const float* row = &xs[buf][pz][c][ty + py][2 * tx];
+                    const f32x2 r01 = *reinterpret_cast<const f32x2*>(row);
+                    const f32x2 r23 = *reinterpret_cast<const f32x2*>(row + 2);
+                    const float v[4] = {r01.x, r01.y, r23.x, r23.y};
+                    // classes q with tap t = q - p + 1 in {0, 1} (p = pz - 1): q = 0 <- t = 1 - p ... per dim
+#pragma unroll
+                    for (int qz = 0; qz < 2; ++qz) {
+                        const int tz = qz - (pz - 1);
+                        if (tz < 0 || tz > 1) continue;
+#pragma unroll
+                        for (int qy = 0; qy < 2; ++qy) {
+                            const int tyy = qy - (py - 1);
+                            if (tyy < 0 || tyy > 1) continue;
+#pragma unroll
+                            for (int qx = 0; qx < 2; ++qx)
+#pragma unroll
+                                for (int txx = 0; txx < 2; ++txx) {
+                                    const float w = wc[(qz << 2 | qy << 1 | qx) * 8 + (tz << 2 | tyy << 1 | txx)];
+#pragma unroll
+                                    for (int j = 0; j < kC2MX; ++j)  // input m_j + qx - tx at v[j + qx - tx + 1]
+                                        acc[qz][qy][j][qx] = fmaf(w, v[j + qx - txx + 1], acc[qz][qy][j][qx]);
+                                }
+                        }
+                    }
+                }
+        }
+        if (ch + 1 < nch) stg.store(&xs[buf ^ 1][0][0][0][0], rx);
+        __syncthreads();
+    }
+
+    const int my = my0 + ty, m0 = mx0 + kC2MX * tx;
+    if (my >= Hi || m0 >= Wi) return;
+    const bool plain = !a.mul && !a.res && !a.out2;
+    const bool vec = plain && m0 + kC2MX <= Wi && (a.oh & 3) == 0 && (a.od & 3) == 0 && (a.ob & 3) == 0 &&
+                     (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+    const float ep_s = a.scale ? a.scale[0] : 1.f, ep_h = a.shift ? a.shift[0] : 0.f;
+#pragma unroll
+    for (int qz = 0; qz < 2; ++qz)
+#pragma unroll
+        for (int qy = 0; qy < 2; ++qy) {
+            const int oz = 2 * mz + qz, oy = 2 * my + qy, ox0 = 2 * m0;
+            const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;
+            if (vec) {
+                floatx4 v4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float t = acc[qz][qy][e >> 1][e & 1];
+                    t = a.scale ? t * ep_s + ep_h : t + ep_h;
+                    v4[e] = apply_act(t, a.act) * a.post_scale;
+                }
+                *reinterpret_cast<floatx4*>(a.out + o) = v4;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if ((m0 + (e >> 1)) < Wi)
+                        conv_put(a, conv_finish(a, acc[qz][qy][e >> 1][e & 1], b, 0, oz, oy, ox0 + e), b, 0, oz, oy,
+                                 ox0 + e);
+            }
+        }
+}
+
 // Whether the VALU form takes this layer: transposed k4 s2 p1, one output channel, one source,
 // at most 32 input channels.
 inline bool convt_c1_ok(const esm_conv_desc& a) {
@@ -383,6 +518,13 @@ int launch_convt_c1_q(const esm_conv_desc& a, hipStream_t s) {
 // per CU, else 32-column tiles (twice the workgroups for the small hourglass outputs).
 template <bool D3>
 int launch_convt_c1(const esm_conv_desc& a, hipStream_t s) {
+    // 3-D: the register-blocked form unless bits 26-27 of the hint ask for the per-class form (A/B)
+    if (D3 && ((a.hint >> 26) & 3) != 1) {
+        const dim3 grid(ceil_div(a.Wi, kC2TX * kC2MX), ceil_div(a.Hi, kC2TY), static_cast<unsigned>(a.B) * a.Di);
+        if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
+        hipLaunchKernelGGL(convt_c1v2_kernel, grid, dim3(kC1Threads), 0, s, a);
+        return check_launch("conv(c1 transposed, blocked)");
+    }
     const long long wg64 = static_cast<long long>(ceil_div(a.Wo, 64)) * ceil_div(a.Ho, kC1TH) * a.B * (D3 ? a.Do : 1);
     return wg64 >= 256 ? launch_convt_c1_q<D3, 4>(a, s) : launch_convt_c1_q<D3, 2>(a, s);
 }

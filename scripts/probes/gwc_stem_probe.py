@@ -37,9 +37,10 @@ def main():
     ap.add_argument("--H", type=int, default=96)
     ap.add_argument("--W", type=int, default=312)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--G", type=int, default=32)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    B, D, H, W, G = args.B, args.D, args.H, args.W, 32
+    B, D, H, W, G = args.B, args.D, args.H, args.W, args.G
     torch.manual_seed(0)
     conv = torch.nn.Conv3d(G, 8, 3, 1, 1, bias=False)
     bn = torch.nn.BatchNorm3d(8).eval()
@@ -49,6 +50,9 @@ def main():
     ctx = Ctx(dev)
     res = {}
     res["gwc"] = timed(lambda i: ctx.gwc(feats[i % 3][0], feats[i % 3][1], None, V, B, 2 * G, H, W, D, G), args.reps)
+    if args.B * D * H * W < (1 << 18):  # small volumes: the forms the S chain picks from
+        for h, nm in ((1 << 24, "stem wide3"), (0, "stem auto")):
+            res[nm] = timed(lambda i: run_conv(ctx, p, [V], hint=h), args.reps)
     for rs in (2, 3):
         res[f"stem tile3 rows{2 if rs == 2 else 4}"] = timed(
             lambda i: run_conv(ctx, p, [V], hint=(1 << 23) | (rs << 26)), args.reps)
