@@ -67,6 +67,11 @@ struct C1Stage {
         for (int k = 0; k < XR; ++k)
             if (k * kC1Threads + static_cast<int>(threadIdx.x) < XN) xs[sidx[k]] = rx[k];
     }
+    // without a branch: the lanes past the tile write to xs[dummy] (a word nothing reads)
+    __device__ __forceinline__ void store_all(float* xs, const float (&rx)[XR], int dummy) const {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) xs[(k + 1) * kC1Threads <= XN || crel[k] < (1 << 30) ? sidx[k] : dummy] = rx[k];
+    }
 };
 
 // buffer descriptor over one batch item of the single source (range = its last element + 1)
@@ -357,28 +362,28 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
         if (ox0 + j < Wo) conv_put(a, conv_finish(a, acc[j], b, 0, oz, oy, ox0 + j), b, 0, oz, oy, ox0 + j);
 }
 
-// 3-D, register-blocked over the parity classes: a thread owns MX = 2 consecutive input-grid
-// positions m (along x) of one input-grid row and plane and computes all 8 parity classes of both, the
-// 2 x 2 x 4 output block (2m + q per dim).  Every class of m reads input m + p, p = q - t in {-1, 0, 1}
-// per dim, so per channel the thread reads the 3 x 3 rows of 4 input values around its positions once
-// (two 8-byte LDS reads per row) and does 128 FMAs with them (the per-class form above: 16 FMAs per 8
-// reads).  A workgroup (16 x 16 threads) owns a 16-row x 32-column input-grid tile of one plane: it
-// stages the 3 planes x 18 rows x 36 columns the tile reads, CC channels per chunk, double-buffered (one
-// barrier per chunk, the next chunk's loads in flight during this one's FMAs), and every weight of the
-// layer once ([c][cls][tap], wave-uniform LDS reads).  Each (qz, qy) class pair of a thread is 4
-// consecutive output columns: one 16-byte store.  Accumulation order per output: channel, plane tap,
-// row tap, column tap.
-constexpr int kC2TY = 16, kC2TX = 16, kC2MX = 2, kC2CC = 2;
+// 3-D, register-blocked over the parity classes: a thread owns MX = 4 consecutive input-grid
+// positions m (along x) of one input-grid row and plane and computes all 8 parity classes of each, the
+// 2 x 2 x 8 output block (2m + q per dim).  Every class of m reads input m + p, p = q - t in {-1, 0, 1}
+// per dim, so per channel the thread reads each of the 3 x 3 input rows around its positions once (6
+// values: one 16-byte and one 8-byte LDS read) and does 256 FMAs with them and 64 wave-uniform weights
+// (16-byte LDS reads; the per-class form above: 16 FMAs per 8 reads).  A workgroup (16 x 16 threads)
+// owns a 16-row x 64-column input-grid tile of one plane: it stages the 3 planes x 18 rows x 68 columns
+// the tile reads, one channel per chunk, double-buffered (one barrier per chunk, the next chunk's loads
+// in flight during this one's FMAs), and every weight of the layer once, as [c][qz][qy][tz][ty][qx][tx].
+// Each (qz, qy) class pair of a thread is 8 consecutive output columns: two 16-byte stores.
+// Accumulation order per output: channel, plane tap, row tap, column tap.
+constexpr int kC2TY = 16, kC2TX = 16, kC2MX = 4;
 
 __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_desc a) {
-    constexpr int MXW = kC2TX * kC2MX;            // input-grid columns per tile (32)
-    constexpr int IR = kC2TY + 2, IC = MXW + 4;   // staged rows / columns (m0 - 1 .. m0 + 34)
-    constexpr int NP = 3, CC = kC2CC;
+    constexpr int MXW = kC2TX * kC2MX;            // input-grid columns per tile (64)
+    constexpr int IR = kC2TY + 2, IC = MXW + 4;   // staged rows / columns (m0 - 1 .. m0 + 66)
+    constexpr int NP = 3, CC = 1;
     constexpr int XN = NP * CC * IR * IC;
     constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
-    constexpr int WCAP = 32 * 64;                 // [c < 32][cls 8][tap 8]
-    __shared__ __attribute__((aligned(16))) float xs[2][NP][CC][IR][IC];
-    __shared__ __attribute__((aligned(16))) float ws[WCAP];
+    constexpr int WCAP = 32 * 64;
+    __shared__ __attribute__((aligned(16))) float xs[2][NP][IR][IC];
+    __shared__ __attribute__((aligned(16))) float ws[WCAP + 1];  // + the staging's dummy word
 
     const int tid = threadIdx.x;
     const int Di = a.Di, Hi = a.Hi, Wi = a.Wi;
@@ -389,16 +394,18 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
     const int sc = static_cast<int>(a.src[0].sc);
     const __amdgpu_buffer_rsrc_t rs = c1_src_rsrc(a, b, true);
     const C1Stage<XR, XN, NP, CC, IR, IC, IC> stg(a, tid, mz - 1, my0 - 1, mx0 - 1);
-    const int nch = (a.Cin + CC - 1) / CC;
+    const int nch = a.Cin;
     float rx[XR];
     stg.load(rx, rs, sc, 0, a.Cin);
     {
         constexpr int WR = WCAP / kC1Threads;
         float rw[WR];
 #pragma unroll
-        for (int k = 0; k < WR; ++k) {  // ws[(c * 8 + cls) * 8 + tap] <- packed w[cls][tap][c][0]
+        for (int k = 0; k < WR; ++k) {  // ws[c][qz][qy][tz][ty][qx][tx] <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
             const int i = tid + k * kC1Threads;
-            const int tap = i & 7, cls = (i >> 3) & 7, c = i >> 6;
+            const int tx = i & 1, qx = (i >> 1) & 1, ty = (i >> 2) & 1, tz = (i >> 3) & 1, qy = (i >> 4) & 1,
+                      qz = (i >> 5) & 1, c = i >> 6;
+            const int cls = qz << 2 | qy << 1 | qx, tap = tz << 2 | ty << 1 | tx;
             const bool ok = c < a.Cin;
             const float v = a.w[ok ? ((static_cast<long long>(cls) * 8 + tap) * a.cin_pad + c) * a.cout_pad : 0];
             rw[k] = ok ? v : 0.f;
@@ -407,11 +414,11 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
 #pragma unroll
         for (int k = 0; k < WR; ++k) ws[tid + k * kC1Threads] = rw[k];
     }
-    stg.store(&xs[0][0][0][0][0], rx);
+    stg.store_all(&xs[0][0][0][0], rx, static_cast<int>(&ws[WCAP] - &xs[0][0][0][0]));
     __syncthreads();
 
     const int ty = tid / kC2TX, tx = tid % kC2TX;
-    // acc[qz][qy][j][qx]: output (2 mz + qz, 2 (my0 + ty) + qy, 2 (mx0 + 2 tx + j) + qx)
+    // acc[qz][qy][j][qx]: output (2 mz + qz, 2 (my0 + ty) + qy, 2 (mx0 + 4 tx + j) + qx)
     float acc[2][2][kC2MX][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -421,43 +428,46 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
             for (int j = 0; j < kC2MX; ++j) acc[i][k][j][0] = acc[i][k][j][1] = 0.f;
     for (int ch = 0; ch < nch; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < nch) stg.load(rx, rs, sc, (ch + 1) * CC, a.Cin);
+        // unconditional: past the last channel the loads return zeros into a buffer nothing reads, and the
+        // loop body stays one block (a conditional store let the FMAs sink below it, behind its waits)
+        stg.load(rx, rs, sc, ch + 1, a.Cin);
         __builtin_amdgcn_sched_barrier(0);  // the next chunk's loads stay ahead of this chunk's FMAs
+        const float* wc = ws + ch * 64;
 #pragma unroll
-        for (int c = 0; c < CC; ++c) {
-            const float* wc = ws + (ch * CC + c) * 64;
+        for (int pz = 0; pz < 3; ++pz)
 #pragma unroll
-            for (int pz = 0; pz < 3; ++pz)
+            for (int py = 0; py < 3; ++py) {
+                // input row m_y + py - 1 of plane m_z + pz - 1, columns m0 - 1 .. m0 + 4 (m0 = mx0 + 4 tx)
+                const float* row = &xs[buf][pz][ty + py][kC2MX * tx];
+                const floatx4 r4 = *reinterpret_cast<const floatx4*>(row);
+                const f32x2 r2 = *reinterpret_cast<const f32x2*>(row + 4);
+                const float v[6] = {r4[0], r4[1], r4[2], r4[3], r2.x, r2.y};
 #pragma unroll
-                for (int py = 0; py < 3; ++py) {
-                    // input row m_y + py - 1 of plane m_z + pz - 1: columns m0 - 1 .. m0 + 2 (m0 = mx0 + 2 tx)
-                    const float* row = &xs[buf][pz][c][ty + py][2 * tx];
-                    const f32x2 r01 = *reinterpret_cast<const f32x2*>(row);
-                    const f32x2 r23 = *reinterpret_cast<const f32x2*>(row + 2);
-                    const float v[4] = {r01.x, r01.y, r23.x, r23.y};
-                    // classes q with tap t = q - p + 1 in {0, 1} (p = pz - 1): q = 0 <- t = 1 - p ... per dim
+                for (int qz = 0; qz < 2; ++qz) {
+                    const int tz = qz - pz + 1;  // input plane m + q - t
+                    if (tz < 0 || tz > 1) continue;
 #pragma unroll
-                    for (int qz = 0; qz < 2; ++qz) {
-                        const int tz = qz - (pz - 1);
-                        if (tz < 0 || tz > 1) continue;
+                    for (int qy = 0; qy < 2; ++qy) {
+                        const int tyy = qy - py + 1;
+                        if (tyy < 0 || tyy > 1) continue;
+                        const floatx4 w4 = *reinterpret_cast<const floatx4*>(wc + (((qz * 2 + qy) * 2 + tz) * 2 + tyy) * 4);
 #pragma unroll
-                        for (int qy = 0; qy < 2; ++qy) {
-                            const int tyy = qy - (py - 1);
-                            if (tyy < 0 || tyy > 1) continue;
+                        for (int qx = 0; qx < 2; ++qx)
 #pragma unroll
-                            for (int qx = 0; qx < 2; ++qx)
+                            for (int txx = 0; txx < 2; ++txx)
 #pragma unroll
-                                for (int txx = 0; txx < 2; ++txx) {
-                                    const float w = wc[(qz << 2 | qy << 1 | qx) * 8 + (tz << 2 | tyy << 1 | txx)];
-#pragma unroll
-                                    for (int j = 0; j < kC2MX; ++j)  // input m_j + qx - tx at v[j + qx - tx + 1]
-                                        acc[qz][qy][j][qx] = fmaf(w, v[j + qx - txx + 1], acc[qz][qy][j][qx]);
-                                }
-                        }
+                                for (int j = 0; j < kC2MX; ++j)  // input m_j + qx - tx at v[j + qx - tx + 1]
+                                    acc[qz][qy][j][qx] = fmaf(w4[qx * 2 + txx], v[j + qx - txx + 1], acc[qz][qy][j][qx]);
                     }
                 }
-        }
-        if (ch + 1 < nch) stg.store(&xs[buf ^ 1][0][0][0][0], rx);
+                // one input row (and its weights) live at a time: left to itself the scheduler issues every
+                // LDS read of the channel first (118 values live, 216 VGPRs)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        // and the next chunk's LDS stores after this chunk's FMAs (moved above them, their waits for the
+        // global loads put a full memory latency before the FMAs of every chunk)
+        __builtin_amdgcn_sched_barrier(0);
+        stg.store_all(&xs[buf ^ 1][0][0][0], rx, static_cast<int>(&ws[WCAP] - &xs[buf ^ 1][0][0][0]));
         __syncthreads();
     }
 
@@ -474,18 +484,21 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
             const int oz = 2 * mz + qz, oy = 2 * my + qy, ox0 = 2 * m0;
             const long long o = b * a.ob + static_cast<long long>(oz) * a.od + static_cast<long long>(oy) * a.oh + ox0;
             if (vec) {
-                floatx4 v4;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float t = acc[qz][qy][e >> 1][e & 1];
-                    t = a.scale ? t * ep_s + ep_h : t + ep_h;
-                    v4[e] = apply_act(t, a.act) * a.post_scale;
+                for (int h = 0; h < 2; ++h) {
+                    floatx4 v4;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float t = acc[qz][qy][2 * h + (e >> 1)][e & 1];
+                        t = a.scale ? t * ep_s + ep_h : t + ep_h;
+                        v4[e] = apply_act(t, a.act) * a.post_scale;
+                    }
+                    *reinterpret_cast<floatx4*>(a.out + o + 4 * h) = v4;
                 }
-                *reinterpret_cast<floatx4*>(a.out + o) = v4;
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if ((m0 + (e >> 1)) < Wi)
+                for (int e = 0; e < 2 * kC2MX; ++e)
+                    if (m0 + (e >> 1) < Wi)
                         conv_put(a, conv_finish(a, acc[qz][qy][e >> 1][e & 1], b, 0, oz, oy, ox0 + e), b, 0, oz, oy,
                                  ox0 + e);
             }

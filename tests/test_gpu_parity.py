@@ -661,8 +661,11 @@ def test_convt_c1_form(nd, cin):
     x = torch.randn(*shape)
     ref = _ref_conv([x], conv, None, ACT_NONE)
     p = pk(conv, None, ACT_NONE)
-    for h in (0, 1 << 16):
+    for h in (0, 1 << 16, 1 << 16 | 1 << 26):  # 3-D: register-blocked form, then the per-class form (bits 26-27 = 1)
         assert rel(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=h), ref) < 1e-5, hex(h)
+    if nd == 3:  # several blocked tiles per plane (64-column x 16-row input tiles), odd extents, B 3
+        xb = torch.randn(3, cin, 3, 19, 70)
+        assert rel(run_conv(Ctx(DEV), p, [xb.to(DEV)]), _ref_conv([xb], conv, None, ACT_NONE)) < 1e-5
     # a channel slice of a wider tensor (batch stride > C * plane): channels past Cin in a staged chunk
     # must read as zero, not as the wider tensor's next channels
     wide = torch.randn(shape[0], cin + 7, *shape[2:], device=DEV)
