@@ -375,15 +375,18 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
 // Accumulation order per output: channel, plane tap, row tap, column tap.
 constexpr int kC2TY = 16, kC2TX = 16, kC2MX = 4;
 
+template <bool D3>  // (3-D only; a template so that both conv2d.hip and conv3d.hip may include it)
 __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_desc a) {
+    static_assert(D3, "the register-blocked ConvT form is 3-D");
     constexpr int MXW = kC2TX * kC2MX;            // input-grid columns per tile (64)
     constexpr int IR = kC2TY + 2, IC = MXW + 4;   // staged rows / columns (m0 - 1 .. m0 + 66)
     constexpr int NP = 3, CC = 1;
     constexpr int XN = NP * CC * IR * IC;
     constexpr int XR = (XN + kC1Threads - 1) / kC1Threads;
     constexpr int WCAP = 32 * 64;
-    __shared__ __attribute__((aligned(16))) float xs[2][NP][IR][IC];
-    __shared__ __attribute__((aligned(16))) float ws[WCAP + 1];  // + the staging's dummy word
+    constexpr int XS = NP * IR * IC + 4;          // one staged chunk + the staging's dummy word (XS - 1)
+    __shared__ __attribute__((aligned(16))) float xs[2][XS];
+    __shared__ __attribute__((aligned(16))) float ws[WCAP];
 
     const int tid = threadIdx.x;
     const int Di = a.Di, Hi = a.Hi, Wi = a.Wi;
@@ -414,7 +417,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
 #pragma unroll
         for (int k = 0; k < WR; ++k) ws[tid + k * kC1Threads] = rw[k];
     }
-    stg.store_all(&xs[0][0][0][0], rx, static_cast<int>(&ws[WCAP] - &xs[0][0][0][0]));
+    stg.store_all(&xs[0][0], rx, XS - 1);
     __syncthreads();
 
     const int ty = tid / kC2TX, tx = tid % kC2TX;
@@ -438,7 +441,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
 #pragma unroll
             for (int py = 0; py < 3; ++py) {
                 // input row m_y + py - 1 of plane m_z + pz - 1, columns m0 - 1 .. m0 + 4 (m0 = mx0 + 4 tx)
-                const float* row = &xs[buf][pz][ty + py][kC2MX * tx];
+                const float* row = &xs[buf][(pz * IR + ty + py) * IC + kC2MX * tx];
                 const floatx4 r4 = *reinterpret_cast<const floatx4*>(row);
                 const f32x2 r2 = *reinterpret_cast<const f32x2*>(row + 4);
                 const float v[6] = {r4[0], r4[1], r4[2], r4[3], r2.x, r2.y};
@@ -467,7 +470,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
         // and the next chunk's LDS stores after this chunk's FMAs (moved above them, their waits for the
         // global loads put a full memory latency before the FMAs of every chunk)
         __builtin_amdgcn_sched_barrier(0);
-        stg.store_all(&xs[buf ^ 1][0][0][0], rx, static_cast<int>(&ws[WCAP] - &xs[buf ^ 1][0][0][0]));
+        stg.store_all(&xs[buf ^ 1][0], rx, XS - 1);
         __syncthreads();
     }
 
@@ -532,11 +535,13 @@ int launch_convt_c1_q(const esm_conv_desc& a, hipStream_t s) {
 template <bool D3>
 int launch_convt_c1(const esm_conv_desc& a, hipStream_t s) {
     // 3-D: the register-blocked form unless bits 26-27 of the hint ask for the per-class form (A/B)
-    if (D3 && ((a.hint >> 26) & 3) != 1) {
-        const dim3 grid(ceil_div(a.Wi, kC2TX * kC2MX), ceil_div(a.Hi, kC2TY), static_cast<unsigned>(a.B) * a.Di);
-        if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
-        hipLaunchKernelGGL(convt_c1v2_kernel, grid, dim3(kC1Threads), 0, s, a);
-        return check_launch("conv(c1 transposed, blocked)");
+    if constexpr (D3) {
+        if (((a.hint >> 26) & 3) != 1) {
+            const dim3 grid(ceil_div(a.Wi, kC2TX * kC2MX), ceil_div(a.Hi, kC2TY), static_cast<unsigned>(a.B) * a.Di);
+            if (grid.y > 65535u || grid.z > 65535u) return arg_error("conv: grid too large");
+            hipLaunchKernelGGL((convt_c1v2_kernel<true>), grid, dim3(kC1Threads), 0, s, a);
+            return check_launch("conv(c1 transposed, blocked)");
+        }
     }
     const long long wg64 = static_cast<long long>(ceil_div(a.Wo, 64)) * ceil_div(a.Ho, kC1TH) * a.B * (D3 ? a.Do : 1);
     return wg64 >= 256 ? launch_convt_c1_q<D3, 4>(a, s) : launch_convt_c1_q<D3, 2>(a, s);
