@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1_kernel(const esm_conv_des
 // 2 x 2 x 8 output block (2m + q per dim).  Every class of m reads input m + p, p = q - t in {-1, 0, 1}
 // per dim, so per channel the thread reads each of the 3 x 3 input rows around its positions once (6
 // values: one 16-byte and one 8-byte LDS read) and does 256 FMAs with them and 64 wave-uniform weights
-// (16-byte LDS reads; the per-class form above: 16 FMAs per 8 reads).  A workgroup (16 x 16 threads)
+// (16-byte LDS reads; the per-class form above: 16 FMAs per 8 reads), as 128 v_pk_fma_f32 over the x-parity pairs.  A workgroup (16 x 16 threads)
 // owns a 16-row x 64-column input-grid tile of one plane: it stages the 3 planes x 18 rows x 68 columns
 // the tile reads, one channel per chunk, double-buffered (one barrier per chunk, the next chunk's loads
 // in flight during this one's FMAs), and every weight of the layer once, as [c][qz][qy][tz][ty][qx][tx].
@@ -404,9 +404,9 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
         constexpr int WR = WCAP / kC1Threads;
         float rw[WR];
 #pragma unroll
-        for (int k = 0; k < WR; ++k) {  // ws[c][qz][qy][tz][ty][qx][tx] <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
+        for (int k = 0; k < WR; ++k) {  // ws[c][qz][qy][tz][ty][tx][qx] <- packed w[cls = (qz,qy,qx)][tap = (tz,ty,tx)][c][0]
             const int i = tid + k * kC1Threads;
-            const int tx = i & 1, qx = (i >> 1) & 1, ty = (i >> 2) & 1, tz = (i >> 3) & 1, qy = (i >> 4) & 1,
+            const int qx = i & 1, tx = (i >> 1) & 1, ty = (i >> 2) & 1, tz = (i >> 3) & 1, qy = (i >> 4) & 1,
                       qz = (i >> 5) & 1, c = i >> 6;
             const int cls = qz << 2 | qy << 1 | qx, tap = tz << 2 | ty << 1 | tx;
             const bool ok = c < a.Cin;
@@ -421,14 +421,15 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
     __syncthreads();
 
     const int ty = tid / kC2TX, tx = tid % kC2TX;
-    // acc[qz][qy][j][qx]: output (2 mz + qz, 2 (my0 + ty) + qy, 2 (mx0 + 4 tx + j) + qx)
-    float acc[2][2][kC2MX][2];
+    // acc[qz][qy][j] = the qx pair of outputs (2 mz + qz, 2 (my0 + ty) + qy, 2 (mx0 + 4 tx + j) + {0, 1}), one
+    // v_pk_fma_f32 per (j, tx): (w[qx = 0][tx], w[qx = 1][tx]) x (x[m_j - tx], x[m_j + 1 - tx])
+    f32x2 acc[2][2][kC2MX];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
-            for (int j = 0; j < kC2MX; ++j) acc[i][k][j][0] = acc[i][k][j][1] = 0.f;
+            for (int j = 0; j < kC2MX; ++j) acc[i][k][j] = f32x2{0.f, 0.f};
     for (int ch = 0; ch < nch; ++ch) {
         const int buf = ch & 1;
         // unconditional: past the last channel the loads return zeros into a buffer nothing reads, and the
@@ -442,9 +443,18 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
             for (int py = 0; py < 3; ++py) {
                 // input row m_y + py - 1 of plane m_z + pz - 1, columns m0 - 1 .. m0 + 4 (m0 = mx0 + 4 tx)
                 const float* row = &xs[buf][(pz * IR + ty + py) * IC + kC2MX * tx];
+                // the column pairs the packed FMAs take, each in an aligned register pair: x[m0 - 1 + 2i, + 1]
+                // (16- and 8-byte reads) and x[m0 + 2i, + 1] (the same row one column on, 4-byte aligned)
                 const floatx4 r4 = *reinterpret_cast<const floatx4*>(row);
-                const f32x2 r2 = *reinterpret_cast<const f32x2*>(row + 4);
-                const float v[6] = {r4[0], r4[1], r4[2], r4[3], r2.x, r2.y};
+                const f32x2 e0 = {r4[0], r4[1]}, e1 = {r4[2], r4[3]};
+                const f32x2 e2 = *reinterpret_cast<const f32x2*>(row + 4);
+                f32x2 o0, o1;
+                o0.x = row[1];
+                o0.y = row[2];
+                o1.x = row[3];
+                o1.y = row[4];
+                // pair for (j, tx): columns m_j - tx, m_j + 1 - tx, i.e. from x[m0 - 1 + (j + 1 - tx)]
+                const f32x2 pr[5] = {e0, o0, e1, o1, e2};  // pr[k] starts at column m0 - 1 + k
 #pragma unroll
                 for (int qz = 0; qz < 2; ++qz) {
                     const int tz = qz - pz + 1;  // input plane m + q - t
@@ -455,12 +465,12 @@ __global__ void __launch_bounds__(kC1Threads) convt_c1v2_kernel(const esm_conv_d
                         if (tyy < 0 || tyy > 1) continue;
                         const floatx4 w4 = *reinterpret_cast<const floatx4*>(wc + (((qz * 2 + qy) * 2 + tz) * 2 + tyy) * 4);
 #pragma unroll
-                        for (int qx = 0; qx < 2; ++qx)
+                        for (int txx = 0; txx < 2; ++txx) {
+                            const f32x2 w2 = {w4[2 * txx], w4[2 * txx + 1]};  // (qx = 0, qx = 1) at this tx
 #pragma unroll
-                            for (int txx = 0; txx < 2; ++txx)
-#pragma unroll
-                                for (int j = 0; j < kC2MX; ++j)  // input m_j + qx - tx at v[j + qx - tx + 1]
-                                    acc[qz][qy][j][qx] = fmaf(w4[qx * 2 + txx], v[j + qx - txx + 1], acc[qz][qy][j][qx]);
+                            for (int j = 0; j < kC2MX; ++j)  // inputs m_j + qx - tx: pair pr[j + 1 - tx]
+                                acc[qz][qy][j] = __builtin_elementwise_fma(w2, pr[j + 1 - txx], acc[qz][qy][j]);
+                        }
                     }
                 }
                 // one input row (and its weights) live at a time: left to itself the scheduler issues every
