@@ -487,6 +487,8 @@ XCD_SLAB_3D = _ab("ESM_XCD_SLAB_3D", "1") != "0"
 # whose 32-channel input each workgroup re-reads with its halo: 15.8 -> 7.8 MB per launch, step time
 # unchanged (round 4, two alternations, profiles/r04_xcd_group_stem_SK.txt)
 XCD_SLAB_MIN_VOX_WIDE = int(_ab("ESM_XCD_SLAB_MIN_VOX_WIDE", "16384"))
+# per-launch hints by op name, "name=0x...,name=0x..." (A/B measurements; replaces the tuned / automatic choice)
+HINT_SET: Dict[str, int] = {k: int(v, 0) for k, v in (t.split("=") for t in _ab("ESM_HINT_SET", "").split(",") if t)}
 # launches (by name, comma-separated) given the slab order whatever their size (A/B measurements)
 XCD_SLAB_OPS = tuple(t for t in _ab("ESM_XCD_SLAB_OPS", "").split(",") if t)
 
@@ -631,7 +633,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         d.out2 = out2.data_ptr()
         d.post_scale2 = float(post_scale2)
     key = conv_key(d, nd)
-    d.hint = int(hint) if hint else TUNED_HINTS.get(key, 0)
+    d.hint = int(hint) if hint else HINT_SET.get(tag, TUNED_HINTS.get(key, 0))
     if (B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX and (nd == 2 or XCD_SLAB_3D)) or \
             (nd == 3 and XCD_SLAB_3D and pc.cin >= 32 and B * Do * Ho * Wo >= XCD_SLAB_MIN_VOX_WIDE) or \
             tag in XCD_SLAB_OPS:
