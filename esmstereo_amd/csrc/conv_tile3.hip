@@ -55,13 +55,9 @@ struct T3Geo {
 
 // NS: input sources (a channel concat of up to 3, 4-channel aligned splits; 1x1x1 only): every k-step
 // lies inside one source, whose descriptor and offsets are selected per k-step (wave-uniform)
-// TPW > 1: the workgroup runs TPW consecutive 16-column tiles along x through one k-step pipeline (the
-// next tile's first k-step is in flight during this tile's last one), for layers with so few k-steps that
-// every tile otherwise waits out its first staging (`agg`, `conv1.0`: 2); hint bits 12-13 = 3.
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false, int TPW = 1>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false>
 __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
-    static_assert(TPW == 1 || (NS == 1 && !D2), "multi-tile workgroups: one source, 3-D");
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
     constexpr int XR = G::XR, WR = G::WR, NR = G::NR;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
@@ -72,7 +68,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int zw = wave % WZ, yw = wave / WZ;
     const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
-    const int xo0 = bk_.x * TPW * 16, yo0 = bk_.y * G::YB;
+    const int xo0 = bk_.x * 16, yo0 = bk_.y * G::YB;
     const int nzb = (a.Do + G::ZB - 1) / G::ZB;
     const int zz = bk_.z;
     const int mg = zz % ncg;
@@ -214,131 +210,6 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         for (int mt = 0; mt < NCO; ++mt) acc[nt][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int nchunk = (a.Cin + 3) >> 2;
-    if constexpr (TPW > 1) {
-        const int ntile = min(TPW, (a.Wo + 15) / 16 - bk_.x * TPW);
-        auto replan = [&](int xb) __attribute__((always_inline)) {  // staging offsets of the tile at input column xb
-#pragma unroll
-            for (int k = 0; k < XR; ++k) {
-                const int e = tid + k * kT3Threads;
-                const int ix = e % IX, iy = (e / IX) % IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
-                const int zi = zi0 + iz, yi = yi0 + iy, xi = xb + ix;
-                const bool ok = e < G::XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
-                xoff[0][k] = ok ? 4u * static_cast<unsigned>(ci * sc0 + zi * sd0 + yi * sh0 + xi) : kOOB;
-            }
-        };
-        auto mstep = [&](int buf) __attribute__((always_inline)) {
-            const float* xw = &xs[buf][g * CS + (yw * NT * S) * IX + n * S];
-            if constexpr (PZ) {
-                const float* wp = &ws[buf][g * 16 + n];
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) {
-                        float br[NR];
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
-#pragma unroll
-                        for (int dy = 0; dy < 3; ++dy) {
-                            const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
-#pragma unroll
-                            for (int nt = 0; nt < NT; ++nt)
-                                acc[nt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt][0], 0, 0, 0);
-                        }
-                    }
-            } else {
-                const float* wp = &ws[buf][g * WCS + n];
-#pragma unroll
-                for (int dz = 0; dz < G::KD; ++dz)
-#pragma unroll
-                    for (int dx = 0; dx < K; ++dx) {
-                        float br[NR];
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) br[r] = xw[(zw * S + dz) * PLANE + r * IX + dx];
-#pragma unroll
-                        for (int dy = 0; dy < K; ++dy) {
-                            float av[MT];
-#pragma unroll
-                            for (int mt = 0; mt < MT; ++mt) av[mt] = wp[((dz * K + dy) * K + dx) * 4 * WCS + mt * 16];
-#pragma unroll
-                            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                                for (int mt = 0; mt < MT; ++mt)
-                                    acc[nt][mt] =
-                                        __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], br[nt * S + dy], acc[nt][mt], 0, 0, 0);
-                        }
-                    }
-            }
-        };
-        auto epi = [&](int xt) __attribute__((always_inline)) {
-        // ---- epilogue: lane (g, n) holds rows 4g + j of each tile, column n
-        const int x = xt + n;
-        const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
-            a.out + b * a.ob, static_cast<short>(0),
-            4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
-                 (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
-            0x00020000);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const int y = yo0 + yw * NT + nt;
-#pragma unroll
-            for (int mt = 0; mt < NCO; ++mt)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int m = 4 * g + j;
-                    const int co = PZ ? (m & 7) : mg * MT * 16 + mt * 16 + m;
-                    const int z = PZ ? zo0 + 2 * zw + (m >> 3) : zo0 + zw;
-                    const bool ok = co < a.Cout && z < a.Do && y < a.Ho && x < a.Wo;
-                    float v = acc[nt][mt][j];
-                    v = a.scale ? v * scl[mt][j] + shf[mt][j] : v + shf[mt][j];
-                    v = act_t<ACT>(v, a.act);
-                    if constexpr (PLAIN) {
-                        const unsigned o = ok ? 4u * static_cast<unsigned>(co * static_cast<int>(a.oc) +
-                                                                           z * static_cast<int>(a.od) +
-                                                                           y * static_cast<int>(a.oh) + x)
-                                              : kOOB;
-                        store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0);
-                    } else {
-                        if (!ok) continue;
-                        if (a.mul) v = v * a.mul[b * a.mb + co * a.mc + static_cast<long long>(y) * a.mh + x];
-                        if (a.res)
-                            v = v + a.res[b * a.rb + co * a.rc + static_cast<long long>(z) * a.rd +
-                                          static_cast<long long>(y) * a.rh + x];
-                        const long long o = b * a.ob + co * a.oc + static_cast<long long>(z) * a.od +
-                                            static_cast<long long>(y) * a.oh + x;
-                        a.out[o] = v * a.post_scale;
-                        if (a.out2) a.out2[o] = v * a.post_scale2;
-                    }
-                }
-        }
-        };
-        stage_load(0);
-        stage_store(0);
-        __syncthreads();
-        const int nsteps = ntile * nchunk;
-        int ch = 0, t = 0;
-        for (int st = 0; st < nsteps; ++st) {
-            const int buf = st & 1;
-            const bool last = ch + 1 == nchunk;  // the tile's last k-step
-            if (st + 1 < nsteps) {
-                if (last) replan(xi0 + (t + 1) * 16 * S);
-                stage_load(last ? 0 : 4 * (ch + 1));
-            }
-            __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the MFMAs
-            mstep(buf);
-            if (last) {
-                epi(xo0 + t * 16);
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int mt = 0; mt < NCO; ++mt) acc[nt][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-                ++t;
-            }
-            if (st + 1 < nsteps) stage_store(buf ^ 1);
-            __syncthreads();
-            ch = last ? 0 : ch + 1;
-        }
-        return;
-    }
     stage_load(0);
     stage_store(0);
     __syncthreads();
@@ -662,35 +533,28 @@ int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
     return arg_error("conv(tile3 transposed): at most 96 output channels");
 }
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false, int TPW = 1>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false>
 int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
     const long long gy = ceil_div(a.Ho, G::YB);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3): grid too large");
-    const dim3 grid(ceil_div(ceil_div(a.Wo, 16), TPW), static_cast<unsigned>(gy), static_cast<unsigned>(z));
+    const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
     const bool plain = a.act == ESM_ACT_GELU && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2, TPW>), grid, dim3(kT3Threads),
-                           0, s, a, ncg);
-    else if constexpr (TPW == 1)
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2>), grid, dim3(kT3Threads), 0, s,
+                           a, ncg);
+    else
         hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2>), grid, dim3(kT3Threads), 0, s, a, ncg);
-    else  // the multi-tile form is built for the plain epilogue only
-        return launch_t3<S, K, MT, NT, WZ, PZ, NS, D2, 1>(a, s, ncg);
     return check_launch("conv(tile3)");
 }
 
 // cout tiles per workgroup (MT) and cout groups (ncg) for Cout: MT * 16 * ncg >= Cout
-template <int S, int K, int NT, int WZ, int NS = 1, bool D2 = false, int TPW = 1>
+template <int S, int K, int NT, int WZ, int NS = 1, bool D2 = false>
 int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
     const int tiles = (a.Cout + 15) / 16;
-    if constexpr (TPW > 1) {  // one or two cout tiles (conv1.0: 24 couts)
-        if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false, NS, D2, TPW>(a, s, 1);
-        if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false, NS, D2, TPW>(a, s, 1);
-        return launch_t3_mt<S, K, NT, WZ, NS, D2, 1>(a, s);
-    }
     if (tiles <= 3) {
         if (tiles == 1) return launch_t3<S, K, 1, NT, WZ, false, NS, D2>(a, s, 1);
         if (tiles == 2) return launch_t3<S, K, 2, NT, WZ, false, NS, D2>(a, s, 1);
@@ -789,13 +653,11 @@ bool tile3_auto(const esm_conv_desc& a) {
     return vox >= (1LL << 16);
 }
 
-// hint bits 26-27 with TILE3 (bit 23): rows per wave 1 / 2 / 4 (0 = automatic); bits 12-13 = 3: four 16-column
-// tiles per workgroup in one k-step pipeline (the stride-2 one-row form and the plane-pair forms)
+// hint bits 26-27 with TILE3 (bit 23): rows per wave 1 / 2 / 4 (0 = automatic)
 int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     if (!tile3_ok(a)) return arg_error("conv: tile3-form hint not applicable");
     const int rsel = (a.hint >> 26) & 3;
     const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
-    const bool tpw4 = ((a.hint >> 12) & 3) == 3 && a.nsrc == 1;
     if (a.transposed) {
         if (rsel == 1) return launch_tt3_mt<1>(a, s);
         if (rsel == 3) return launch_tt3_mt<4>(a, s);
@@ -809,14 +671,12 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     if (a.stride == 2) {  // one row per wave unless asked (r04 probe, L-K B = 4: conv1.0 274 -> 226 us, conv2.0 92 -> 86)
         if (rsel == 2) return launch_t3_mt<2, 3, 2, 2>(a, s);
         if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
-        if (tpw4) return launch_t3_mt<2, 3, 1, 2, 1, false, 4>(a, s);
         return launch_t3_mt<2, 3, 1, 2>(a, s);
     }
     if (a.Cout <= 8) {  // plane pairs
         if (rsel == 1) return launch_t3<1, 3, 1, 1, 4, true>(a, s, 1);
-        if (rsel == 2 || (rsel == 0 && vox < (1LL << 20)))
-            return tpw4 ? launch_t3<1, 3, 1, 2, 4, true, 1, false, 4>(a, s, 1) : launch_t3<1, 3, 1, 2, 4, true>(a, s, 1);
-        return tpw4 ? launch_t3<1, 3, 1, 4, 4, true, 1, false, 4>(a, s, 1) : launch_t3<1, 3, 1, 4, 4, true>(a, s, 1);
+        if (rsel == 2 || (rsel == 0 && vox < (1LL << 20))) return launch_t3<1, 3, 1, 2, 4, true>(a, s, 1);
+        return launch_t3<1, 3, 1, 4, 4, true>(a, s, 1);
     }
     if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
     if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);
