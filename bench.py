@@ -525,10 +525,17 @@ def standin_cpu(args, world: int, rank: int) -> None:
 
     elapsed = D.timed_steps(step, args.steps, args.warmup, torch.device("cpu"))
     if rank == 0:
+        # the gathered buffer holds rank r's shard at [r] (rank order): every rank's input is regenerated here
+        order_ok = True
+        for r in range(world):
+            gr = torch.Generator().manual_seed(100 + r)
+            lr_, rr_ = torch.randn(b, 3, 8, 16, generator=gr), torch.randn(b, 3, 8, 16, generator=gr)
+            order_ok = order_ok and torch.equal(gather.buf[r], (lr_ - rr_).abs().sum(1) * 4)
         print(json.dumps({"metric": METRIC, "value": round(total * args.steps / elapsed, 2), "unit": "pairs/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "scaling": scaling,
                           "standin": "cpu gloo (no GPU work)", "global_batch": total,
-                          "gathered_shape": list(gather.buf.shape)}), flush=True)
+                          "gathered_shape": list(gather.buf.shape), "gather_rank_order_ok": bool(order_ok)}),
+              flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

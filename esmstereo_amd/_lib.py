@@ -114,6 +114,7 @@ SIGNATURES = {
     "esm_shuffle_tail_f32": (c_int, [POINTER(EsmShuffleTailDesc), c_void_p]),
     "esm_shuffle_conv_f32": (c_int, [POINTER(EsmShuffleConvDesc), c_void_p]),
     "esm_conv_pair2_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
+    "esm_convt_1x1_f32": (c_int, [POINTER(EsmConvDesc), POINTER(EsmConvDesc), c_void_p]),
     "esm_conf_f32": (c_int, [POINTER(EsmConfDesc), c_void_p]),
     "esm_dwconv_f32": (c_int, [POINTER(EsmDwconvDesc), c_void_p]),
     "esm_preprocess_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
@@ -127,6 +128,7 @@ SIGNATURES = {
     "esm_plan_add_shuffle_tail": (c_int, [c_void_p, POINTER(EsmShuffleTailDesc)]),
     "esm_plan_add_shuffle_conv": (c_int, [c_void_p, POINTER(EsmShuffleConvDesc)]),
     "esm_plan_add_conv_pair2": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
+    "esm_plan_add_convt_1x1": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_gwc_stem": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),

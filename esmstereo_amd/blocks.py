@@ -23,10 +23,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, SC11_ENABLED, Ctx, PackedConv, eager_emit, pack_conv, pack_shuffle_tail,
-                     pair2_auto, param_token,
-                     run_conv, run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_pre_supported,
-                     shuffle_conv_supported)
+from .engine import (ACT_GELU, ACT_NONE, CONVT1X1_PAIRED, SC11_ENABLED, Ctx, PackedConv, convt_1x1_supported,
+                     eager_emit, pack_conv, pack_shuffle_tail, pair2_auto, param_token, run_conv, run_convt_1x1,
+                     run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_pre_supported, shuffle_conv_supported)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -151,17 +150,31 @@ class _Hourglass(nn.Module):
             c1 = _pair(ctx, self.conv1[0], [x], self.conv1[1])
         c2 = _pair(ctx, self.conv2[0], [c1], self.conv2[1])
         c3 = _pair(ctx, self.conv3[0], [c2], self.conv3[1])
-        u3 = self.conv3_up.emit(ctx, [c3])
-        a0 = _pair(ctx, self.agg_0[0], [_crop_like(u3, c2), c2, *extra0], self.agg_0[1])
-        u2 = self.conv2_up.emit(ctx, [a0])
-        if crop1:
-            u2 = _crop_like(u2, c1)
-        elif u2.shape[2:] != c1.shape[2:]:
+        a0 = self._up_agg(ctx, self.conv3_up, c3, self.agg_0, [c2, *extra0], True)
+        a1 = self._up_agg(ctx, self.conv2_up, a0, self.agg_1, [c1, *extra1], crop1)
+        return self.conv1_up.emit(ctx, [a1], **last)
+
+    def _up_agg(self, ctx: Ctx, up: BasicConv, x: torch.Tensor, agg: nn.Sequential, skip: Sequence[torch.Tensor],
+                crop: bool) -> torch.Tensor:
+        """``agg(cat(crop(up(x)), *skip))`` (ESMStereo.py:163-177, 226-234): the transposed conv and agg[0] in
+        one launch where conv_up1.hip has the shape (and agg[0] + agg[1] would not run as one pair), else
+        the transposed conv, then agg[0] + agg[1] (one pair2 launch or two)."""
+        ref = skip[0]
+        if not crop and tuple(2 * v for v in x.shape[2:]) != tuple(ref.shape[2:]):
             # the reference concat at ESMStereo.py:234 does not crop and raises here
             raise RuntimeError(f"Sizes of tensors must match except in dimension 1. Expected size "
-                               f"{u2.shape[2]} but got size {c1.shape[2]} for tensor number 1 in the list.")
-        a1 = _pair(ctx, self.agg_1[0], [u2, c1, *extra1], self.agg_1[1])
-        return self.conv1_up.emit(ctx, [a1], **last)
+                               f"{2 * x.shape[2]} but got size {ref.shape[2]} for tensor number 1 in the list.")
+        pa, pb = up.packed(), agg[0].packed()
+        u_shape = tuple(2 * v for v in x.shape[2:])
+        paired = pair2_auto(pb, agg[1].packed(), [ref]) if not self.is_3d else False
+        if convt_1x1_supported(pa, pb, skip) and all(u >= r for u, r in zip(u_shape, ref.shape[2:])) and \
+                (CONVT1X1_PAIRED or not paired):
+            n0 = getattr(up, "_esm_name", "convT")
+            n1 = getattr(agg[0], "_esm_name", "agg.0")
+            h = run_convt_1x1(ctx, pa, [x], pb, skip, tags=(n0, n1))
+            return agg[1].emit(ctx, [h])
+        u = _crop_like(up.emit(ctx, [x]), ref)
+        return _pair(ctx, agg[0], [u, *skip], agg[1])
 
 
 class aggregation(_Hourglass):

@@ -22,7 +22,7 @@
 //     deterministic); then every thread finishes one (cout, pixel) element: BN scale/shift,
 //     activation, optional residual, * post_scale (+ the second copy), one coalesced store.
 // Plain epilogues only (no `* mul`, bilinear add or PixelShuffle): the launcher falls back otherwise.
-#include "conv_direct.h"
+#include "conv_up1.h"
 
 namespace esm {
 namespace conv {
@@ -41,8 +41,10 @@ inline unsigned magic_for(int d) {
 
 // NW = 4 or 8 waves splitting the K reduction (8: layers with more than 4 channel groups, so that no
 // wave walks two groups one after the other; the epilogue runs on the first 256 threads)
-template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN, int NW = 4>
-__global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
+// XB > 0 (transposed, MT = 1): the 1x1 BasicConv behind it fused (conv_up1.h; bp: its descriptor, up to XB
+// extra 4-channel k-steps): wave 0 finishes the 16 x 16 tile, the conv's output never leaves its registers
+template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN, int NW, int XB>
+__device__ __forceinline__ void lconv_body(const esm_conv_desc& a, unsigned m_ds, unsigned m_b, const esm_conv_desc* bp) {
     constexpr int KT = TR ? 2 : K;  // taps per dim (per parity class when transposed)
     constexpr int KDT = D3 ? KT : 1;
     constexpr int TAPS = KDT * KT * KT;
@@ -79,6 +81,26 @@ __global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, u
         const int co = min(cob + 16 * mt + 4 * kq + ej, a.Cout - 1);
         scl[mt] = a.scale ? a.scale[co] : 1.f;
         shf[mt] = a.shift ? a.shift[co] : 0.f;
+    }
+
+    // fused 1x1: its weights, BN and the extra sources at this lane's output pixel, loaded up front by wave 0
+    Up1Ops<(XB > 0 ? XB : 1)> u1;
+    float bx1[(XB > 0 ? XB : 1)];
+    float s1[4], h1[4];
+    if constexpr (XB > 0) {
+        static_assert(TR && MT == 1, "fused 1x1: transposed conv, one cout tile");
+        if (wave == 0) {
+            const esm_conv_desc& bb = *bp;
+            up1_weights(u1, bb, a.Cout, lane);
+            const Up1Src us = up1_src(bb, b, D3);
+            up1_extra(bx1, us, bb, a.Cout, lane, D3 ? 2 * zs + qd : 0, 2 * ys + qh, 2 * (x0 + n16) + qw);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = min(4 * kq + r, a.Cout - 1);
+                s1[r] = a.scale[co];
+                h1[r] = a.shift[co];
+            }
+        }
     }
 
     // per-lane column byte offsets per horizontal tap (kOOB: outside the input or past the map)
@@ -173,6 +195,31 @@ __global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, u
         return v;
     };
 
+    if constexpr (XB > 0) {
+        // wave 0: y = GELU(BN(conv)) in the D layout (lane (n16, kq): channels 4 kq + r), then the 1x1
+        if (wave != 0) return;
+        const esm_conv_desc& bb = *bp;
+        float y[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = gelu_erf(reduced(r * 64 + lane) * s1[r] + h1[r]);
+        const floatx4 o = up1_finish(u1, y, bx1);
+        const int ox = 2 * (x0 + n16) + qw, oy = 2 * ys + qh, oz = D3 ? 2 * zs + qd : 0;
+        const bool pok = ox < bb.Wo && oy < bb.Ho && oz < bb.Do;
+        const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+            bb.out + b * bb.ob, static_cast<short>(0),
+            4 * ((bb.Cout - 1) * static_cast<int>(bb.oc) + (D3 ? (bb.Do - 1) * static_cast<int>(bb.od) : 0) +
+                 (bb.Ho - 1) * static_cast<int>(bb.oh) + bb.Wo),
+            0x00020000);
+        const int orow = 4 * ((D3 ? oz * static_cast<int>(bb.od) : 0) + oy * static_cast<int>(bb.oh));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = 4 * kq + r;
+            const unsigned vo = (pok && co < bb.Cout) ? 4u * static_cast<unsigned>(co * static_cast<int>(bb.oc) + ox) : kOOB;
+            store_b32(__float_as_uint(o[r]), ro_, static_cast<int>(vo), orow);
+        }
+        return;
+    }
+
     const int xsub = x0 + ecol;
     const int oz = TR ? 2 * zs + qd : zs;
     const int oy = TR ? 2 * ys + qh : ys;
@@ -214,6 +261,18 @@ __global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, u
     }
 }
 
+template <bool D3, int K, int S, bool TR, int MT, int ACT, bool PLAIN, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) lconv_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b) {
+    lconv_body<D3, K, S, TR, MT, ACT, PLAIN, NW, 0>(a, m_ds, m_b, nullptr);
+}
+
+// ConvTranspose + crop + cat + 1x1 (conv_up1.h)
+template <bool D3, int NW, int XB>
+__global__ void __launch_bounds__(64 * NW) lconv_up1_kernel(const esm_conv_desc a, unsigned m_ds, unsigned m_b,
+                                                           const esm_conv_desc b) {
+    lconv_body<D3, 4, 2, true, 1, ESM_ACT_GELU, true, NW, XB>(a, m_ds, m_b, &b);
+}
+
 template <bool D3, int K, int S, bool TR>
 int launch_small_m(const esm_conv_desc& a, hipStream_t s) {
     constexpr int NCLS = TR ? (D3 ? 8 : 4) : 1;
@@ -248,7 +307,37 @@ int launch_small_m(const esm_conv_desc& a, hipStream_t s) {
     return check_launch("conv(small)");
 }
 
+template <bool D3, int NW>
+int launch_small_up1_x(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s, const dim3& grid, unsigned mds,
+                       unsigned mb) {
+    const int xb = (b.Cin - a.Cout) >> 2;
+    if (xb <= 3) hipLaunchKernelGGL((lconv_up1_kernel<D3, NW, 3>), grid, dim3(64 * NW), 0, s, a, mds, mb, b);
+    else if (xb <= 4) hipLaunchKernelGGL((lconv_up1_kernel<D3, NW, 4>), grid, dim3(64 * NW), 0, s, a, mds, mb, b);
+    else if (xb <= 8) hipLaunchKernelGGL((lconv_up1_kernel<D3, NW, 8>), grid, dim3(64 * NW), 0, s, a, mds, mb, b);
+    else if (xb <= 10) hipLaunchKernelGGL((lconv_up1_kernel<D3, NW, 10>), grid, dim3(64 * NW), 0, s, a, mds, mb, b);
+    else hipLaunchKernelGGL((lconv_up1_kernel<D3, NW, 12>), grid, dim3(64 * NW), 0, s, a, mds, mb, b);
+    return check_launch("conv(small, transposed + 1x1)");
+}
+
 }  // namespace
+
+bool small_ok(const esm_conv_desc& a);
+
+// ConvTranspose k4 s2 (<= 16 couts) + crop + cat + 1x1 (<= 16 couts, <= 48 extra channels) in the lean form
+// (conv_up1.h); a and b validated by the caller (launch_convt_1x1)
+int launch_small_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
+    if (!small_ok(a) || !a.transposed) return arg_error("convt_1x1: the lean form cannot run this transposed conv");
+    const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || a.kd == 4;
+    const int ncls = d3 ? 8 : 4;
+    const int Ds = d3 ? a.Di : 1;
+    const long long z = static_cast<long long>(Ds) * a.B * ncls;
+    if (a.Hi > 65535 || z > 65535) return arg_error("convt_1x1(small): grid too large");
+    const dim3 grid(ceil_div(a.Wi, 16), static_cast<unsigned>(a.Hi), static_cast<unsigned>(z));
+    const unsigned mds = magic_for(Ds), mb = magic_for(a.B);
+    const bool w8 = (a.hint & (1 << 29)) && (a.Cin + 3) / 4 > 4;
+    if (d3) return w8 ? launch_small_up1_x<true, 8>(a, b, s, grid, mds, mb) : launch_small_up1_x<true, 4>(a, b, s, grid, mds, mb);
+    return w8 ? launch_small_up1_x<false, 8>(a, b, s, grid, mds, mb) : launch_small_up1_x<false, 4>(a, b, s, grid, mds, mb);
+}
 
 // Whether the lean form can run this layer: plain epilogue, 4-channel aligned source splits, spans
 // addressable by 32-bit buffer offsets (conv_direct.h direct_ok), a kernel shape it instantiates.

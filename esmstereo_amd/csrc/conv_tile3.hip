@@ -22,7 +22,7 @@
 //     output is one fixed-order sum (deterministic, independent of the tiling).
 // Epilogue as the other forms: folded BN scale / shift, activation, optional * mul, + res, * post_scale
 // and the second copy, write-through (sc1) buffer stores.
-#include "conv_direct.h"
+#include "conv_up1.h"
 
 namespace esm {
 namespace conv {
@@ -312,8 +312,10 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
 // a lane holds the two adjacent output columns 2m, 2m + 1 and stores them as one 8-byte write.
 // D2: ConvTranspose2d k4 s2 p1 (the refinement hourglasses' conv3_up / conv2_up): one qh class per
 // workgroup, the 4 waves along y (NT rows each), 4 taps per class
-template <int MT, int NT, int ACT, bool PLAIN, bool D2 = false>
-__global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc a, int ncg) {
+// XB > 0 (MT = 1, ncg = 1): the 1x1 BasicConv behind it fused (conv_up1.h; bp: its descriptor, up to XB extra
+// 4-channel k-steps): each wave finishes its tiles through the 1x1, the conv's output never leaves registers
+template <int MT, int NT, int ACT, bool PLAIN, bool D2, int XB, bool PAIR = false>
+__device__ __forceinline__ void tconvt3_body(const esm_conv_desc& a, int ncg, const esm_conv_desc* bp) {
     constexpr int ZB = D2 ? 1 : 4, YB = D2 ? 4 * NT : NT;
     constexpr int NTAP = D2 ? 4 : 8;  // taps per class
     constexpr int IZ = D2 ? 1 : ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
@@ -402,6 +404,25 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
             scl[mt][j] = a.scale ? a.scale[cc] : 1.f;
             shf[mt][j] = a.shift ? a.shift[cc] : 0.f;
         }
+    // fused 1x1: weights, BN and the extra sources at this lane's output pixels, in flight during the K loop
+    Up1Ops<(XB > 0 ? XB : 1)> u1;
+    float bx1[2][NT][(XB > 0 ? XB : 1)];
+    if constexpr (XB > 0) {
+        static_assert(MT == 1, "fused 1x1: one cout tile");
+        const esm_conv_desc& bb = *bp;
+        up1_weights(u1, bb, a.Cout, lane);
+        const Up1Src us = up1_src(bb, b, !D2);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int oz = D2 ? 0 : 2 * (zm0 + zw) + qd, oy = 2 * (ym0 + yw * NT + nt) + qh, ox = 2 * (xm0 + n);
+            if constexpr (PAIR) {
+                up1_extra2(bx1[0][nt], bx1[1][nt], us, bb, a.Cout, lane, oz, oy, ox);
+            } else {
+#pragma unroll
+                for (int qw = 0; qw < 2; ++qw) up1_extra(bx1[qw][nt], us, bb, a.Cout, lane, oz, oy, ox + qw);
+            }
+        }
+    }
     floatx4 acc[2][NT][MT];
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -456,6 +477,54 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
     // ---- epilogue: lane (g, n) holds output columns 2m, 2m + 1 (m = xm0 + n) of rows 4g + j
     const int x = 2 * (xm0 + n);
     const int z = D2 ? 0 : 2 * (zm0 + zw) + qd;
+    if constexpr (XB > 0) {
+        const esm_conv_desc& bb = *bp;
+        const __amdgpu_buffer_rsrc_t rb_ = __builtin_amdgcn_make_buffer_rsrc(
+            bb.out + b * bb.ob, static_cast<short>(0),
+            4 * ((bb.Cout - 1) * static_cast<int>(bb.oc) + (D2 ? 0 : (bb.Do - 1) * static_cast<int>(bb.od)) +
+                 (bb.Ho - 1) * static_cast<int>(bb.oh) + bb.Wo),
+            0x00020000);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int y = 2 * (ym0 + yw * NT + nt) + qh;
+            const int orow = 4 * ((D2 ? 0 : z * static_cast<int>(bb.od)) + y * static_cast<int>(bb.oh));
+            const bool rok = y < bb.Ho && z < bb.Do;
+            floatx4 o[2];
+#pragma unroll
+            for (int qw = 0; qw < 2; ++qw) {
+                float yv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) yv[j] = gelu_erf(acc[qw][nt][0][j] * scl[0][j] + shf[0][j]);
+                o[qw] = up1_finish(u1, yv, bx1[qw][nt]);
+            }
+            if constexpr (PAIR) {  // 8-byte pair stores (b's output rows 8-byte aligned, even width: launcher)
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const bool pok = rok && x < bb.Wo;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g + j;
+                    const unsigned vo =
+                        (pok && co < bb.Cout) ? 4u * static_cast<unsigned>(co * static_cast<int>(bb.oc) + x) : kOOB;
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[0][j]), __float_as_uint(o[1][j])}, rb_,
+                                                          static_cast<int>(vo), rok ? orow : 0, kStoreAux);
+                }
+            } else {
+#pragma unroll
+                for (int qw = 0; qw < 2; ++qw) {
+                    const bool pok = rok && x + qw < bb.Wo;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int co = 4 * g + j;
+                        const unsigned vo = (pok && co < bb.Cout)
+                                                ? 4u * static_cast<unsigned>(co * static_cast<int>(bb.oc) + x + qw)
+                                                : kOOB;
+                        store_b32(__float_as_uint(o[qw][j]), rb_, static_cast<int>(vo), rok ? orow : 0);
+                    }
+                }
+            }
+        }
+        return;
+    }
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
         4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
@@ -501,6 +570,42 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
                 }
             }
     }
+}
+
+template <int MT, int NT, int ACT, bool PLAIN, bool D2 = false>
+__global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc a, int ncg) {
+    tconvt3_body<MT, NT, ACT, PLAIN, D2, 0>(a, ncg, nullptr);
+}
+
+// ConvTranspose + crop + cat + 1x1 (conv_up1.h); PAIR: 8-byte extra-source loads and output stores
+template <int NT, bool D2, int XB, bool PAIR>
+__global__ void __launch_bounds__(kT3Threads) tconvt3_up1_kernel(const esm_conv_desc a, const esm_conv_desc b) {
+    tconvt3_body<1, NT, ESM_ACT_GELU, true, D2, XB, PAIR>(a, 1, &b);
+}
+
+template <int NT, bool D2>
+int launch_tt3_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
+    const long long z = D2 ? static_cast<long long>(a.B) * 2 : static_cast<long long>(a.B) * ((a.Di + 3) / 4) * 4;
+    const long long gy = ceil_div(a.Hi, D2 ? 4 * NT : NT);
+    if (z > 65535 || gy > 65535) return arg_error("convt_1x1(tile): grid too large");
+    const dim3 grid(ceil_div(a.Wi, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
+    const int xb = (b.Cin - a.Cout) >> 2;
+    // pairs: b's output rows / channels / batch items 8-byte aligned and every extra source likewise
+    const bool pair = up1_pairs_ok(b) && !(b.Wo & 1) && !(reinterpret_cast<uintptr_t>(b.out) & 7) && !(b.ob & 1) &&
+                      !(b.oc & 1) && !(b.oh & 1) && !(b.od & 1);
+#define ESM_UP1(X)                                                                                   \
+    do {                                                                                             \
+        if (pair)                                                                                    \
+            hipLaunchKernelGGL((tconvt3_up1_kernel<NT, D2, X, true>), grid, dim3(kT3Threads), 0, s, a, b); \
+        else                                                                                         \
+            hipLaunchKernelGGL((tconvt3_up1_kernel<NT, D2, X, false>), grid, dim3(kT3Threads), 0, s, a, b); \
+    } while (0)
+    if (xb <= 4) ESM_UP1(4);
+    else if (xb <= 8) ESM_UP1(8);
+    else if (xb <= 10) ESM_UP1(10);
+    else ESM_UP1(12);
+#undef ESM_UP1
+    return check_launch("conv(tile3 transposed + 1x1)");
 }
 
 template <int MT, int NT, bool D2 = false>
@@ -624,6 +729,20 @@ int launch_tile2(const esm_conv_desc& a, hipStream_t s) {
     if (a.kh == 1) return launch_t2_nt<1, 1>(a, s);
     if (a.stride == 2) return launch_t2_nt<2, 3>(a, s);
     return launch_t2_nt<1, 3>(a, s);
+}
+
+bool tile2_ok(const esm_conv_desc& a);
+bool tile3_ok(const esm_conv_desc& a);
+
+// ConvTranspose k4 s2 (<= 16 couts) + crop + cat + 1x1 (<= 16 couts, <= 48 extra channels) in the LDS-tiled
+// form (conv_up1.h); a and b validated by the caller (launch_convt_1x1).  Rows per wave from a's hint bits
+// 26-27 (1 / 2; default 2)
+int launch_tile_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
+    const bool d3 = a.kd == 4;
+    if (!(d3 ? tile3_ok(a) : tile2_ok(a))) return arg_error("convt_1x1: the tiled form cannot run this transposed conv");
+    const int rsel = (a.hint >> 26) & 3;
+    if (d3) return rsel == 1 ? launch_tt3_up1<1, false>(a, b, s) : launch_tt3_up1<2, false>(a, b, s);
+    return rsel == 1 ? launch_tt3_up1<1, true>(a, b, s) : launch_tt3_up1<2, true>(a, b, s);
 }
 
 // 3-D, one source, 3x3x3 stride 1 / 2 padding 1 or 1x1x1 stride 1 padding 0, <= 96 couts, spans within

@@ -77,13 +77,14 @@ int launch_dwconv(const esm_dwconv_desc* d, hipStream_t s) {
     const esm_dwconv_desc& a = *d;
     if (!a.x || !a.w || !a.out) return arg_error("dwconv: null pointer");
     if (a.B <= 0 || a.C <= 0 || a.H <= 0 || a.W <= 0) return arg_error("dwconv: bad size");
+    if (a.stride <= 0 || a.K <= 0) return arg_error("dwconv: stride and K must be positive");
     if (a.pad < 0 || a.pad >= a.K) return arg_error("dwconv: bad padding");
     if (a.Ho != (a.H + 2 * a.pad - a.K) / a.stride + 1 || a.Wo != (a.W + 2 * a.pad - a.K) / a.stride + 1 || a.Ho <= 0 ||
         a.Wo <= 0)
         return arg_error("dwconv: output extent inconsistent with K / stride / pad");
     if (a.xh < a.W || a.xc < static_cast<long long>(a.H) * a.xh || a.oh < a.Wo || a.oc < static_cast<long long>(a.Ho) * a.oh)
         return arg_error("dwconv: strides inconsistent with the extents");
-    if (static_cast<long long>(a.B) * a.C > 0x7fffffffLL || ceil_div(a.Ho, kDwTY) > 65535u)
+    if (static_cast<long long>(a.B) * a.C > 65535 || ceil_div(a.Ho, kDwTY) > 65535u)  // grid z / y limits
         return arg_error("dwconv: grid too large");
     if (a.K == 3 && a.stride == 1) return launch_dw<3, 1>(a, s);
     if (a.K == 3 && a.stride == 2) return launch_dw<3, 2>(a, s);

@@ -20,6 +20,7 @@ int launch_shuffle_tail(const esm_shuffle_tail_desc*, hipStream_t);
 int launch_shuffle_conv(const esm_shuffle_conv_desc*, hipStream_t);
 namespace conv {
 int launch_pair2(const esm_conv_desc&, const esm_conv_desc&, hipStream_t);
+int launch_convt_1x1(const esm_conv_desc&, const esm_conv_desc&, hipStream_t);  // conv_up1.hip
 int gwc_stem_check(const esm_conv_desc&, const float*, const float*, int, int);                // gwc_stem.hip
 int launch_gwc_stem(const esm_conv_desc&, const float*, const float*, int, int, hipStream_t);  // gwc_stem.hip
 }
@@ -38,7 +39,7 @@ void set_error(const std::string& msg) {
 
 namespace {
 
-enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12, kPair2 = 13, kGwcStem = 14 };
+enum OpKind { kConv = 1, kSmix = 2, kGwc = 3, kConcat = 4, kNormcorr = 5, kRegression = 6, kShuffleTail = 7, kFmnet = 9, kConf = 10, kShuffleConv = 12, kPair2 = 13, kGwcStem = 14, kConvt1x1 = 15 };
 
 struct VolArgs {
     const float* L;
@@ -78,6 +79,7 @@ int run_op(const Op& op, hipStream_t s) {
         case kShuffleTail: return esm::launch_shuffle_tail(&op.st, s);
         case kShuffleConv: return esm::launch_shuffle_conv(&op.sc, s);
         case kPair2: return esm::conv::launch_pair2(op.conv, op.conv2, s);
+        case kConvt1x1: return esm::conv::launch_convt_1x1(op.conv, op.conv2, s);
         case kConf: return esm::launch_conf(&op.cf, s);
         case kGwcStem: return esm::conv::launch_gwc_stem(op.conv, op.vol.L, op.vol.R, op.vol.C, op.vol.G, s);
         case kGwc:
@@ -230,7 +232,8 @@ struct esm_plan {
         Op& op = ops[i];
         switch (op.kind) {
             case kConv: return rb.conv(op.conv);
-            case kPair2: return rb.conv(op.conv) + rb.conv(op.conv2);
+            case kPair2:
+            case kConvt1x1: return rb.conv(op.conv) + rb.conv(op.conv2);
             case kGwcStem: return rb.conv(op.conv) + rb(op.vol.L) + rb(op.vol.R);
             case kSmix: {
                 int n = rb(op.smix.x) + rb(op.smix.out) + rb(op.smix.res) + rb(op.smix.dw_w) + rb(op.smix.dw_b);
@@ -392,6 +395,15 @@ int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_co
     if (!a || !b) return esm::arg_error("plan: null conv pair desc");
     Op op;
     op.kind = kPair2;
+    op.conv = *a;
+    op.conv2 = *b;
+    return add_op(plan, std::move(op));
+}
+
+int esm_plan_add_convt_1x1(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b) {
+    if (!a || !b) return esm::arg_error("plan: null convt_1x1 desc");
+    Op op;
+    op.kind = kConvt1x1;
     op.conv = *a;
     op.conv2 = *b;
     return add_op(plan, std::move(op));

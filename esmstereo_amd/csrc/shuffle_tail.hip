@@ -971,46 +971,64 @@ __global__ void __launch_bounds__(64 * L) shuffle_conv4_kernel(const esm_shuffle
 }
 
 // The 4x stage's spx_4x[1] + upsampling4 + tail4x + ref4x.conv1[0] + ref4x.conv1[1] in ONE launch (round 5,
-// esm_shuffle_conv_desc.w2): shuffle_conv4_kernel's low-res tile (8 rows x 16 pixels) grown by the second conv's
-// one-pixel halo, which the low-res window already covers: the shuffled map on the WHOLE 10 x 18 window by MFMA
-// (rows Y0 - 4 .. Y0 + 35, no VALU ring), x on 37 x 69, the first conv (c1) on its 18 x 34 tile + halo by MFMA into
-// LDS (zero outside the map: the second conv's padding), then the second conv (3x3 16 -> 16, K = 144 in 36
-// k-steps) by MFMA with BN + GELU, stored.  c1 never leaves LDS: the second conv's own launch (10 us at S-K,
-// 0.33 of the fp32 MFMA peak) becomes ~2 us of matrix-core time here.  Arithmetic: the pre-conv, shuffled map
-// and tail as shuffle_conv4_kernel; the convs in MFMA k-step order (relative 1e-5 vs fp64).
+// esm_shuffle_conv_desc.w2): shuffle_conv4_kernel's low-res tile (L rows x 16 pixels) grown by the second conv's
+// one-pixel halo, which the low-res window already covers: the shuffled map on the WHOLE (L + 2) x 18 window by MFMA
+// (rows Y0 - 4 .. Y0 + 4L + 3, no VALU ring), x on (4L + 5) x 69, the first conv (c1) on its (2L + 2) x 34 tile + halo
+// by MFMA into LDS (zero outside the map: the second conv's padding), then the second conv (3x3 16 -> 16, K = 144 in
+// 36 k-steps) by MFMA with BN + GELU, stored.  c1 never leaves LDS.  Arithmetic: the pre-conv, shuffled map and tail
+// as shuffle_conv4_kernel; the convs in MFMA k-step order (relative 1e-5 vs fp64).
+// Round 6: L = 4 rows on 256 threads (4 waves).  The three weight images the MFMA phases read as A operands (the
+// pre-conv, upsampling's 1x1, the second conv: 5632 floats) are staged through LDS once and then held in registers
+// (each lane's 36 + 2 x (8 / L) + 36 values), so the workgroup needs ~66 KB of LDS and two fit on a CU: 480
+// workgroups on 256 CUs at S-K, one workgroup's VALU / LDS phases (shuffle, tail, c1) overlapping the other's
+// matrix-core phases (pre-conv, second conv).  L = 8 (512 threads, ~111 KB, one per CU) stays selectable
+// (esm_shuffle_tail_desc.flags bit 3) for A/B measurements.
+template <int L_, int NW_>
 struct Sc7Geo {
-    static constexpr int NF = 8, C = 16, L = 8, NT = 64 * L;
+    static constexpr int NF = 8, C = 16, L = L_, NW = NW_, NT = 64 * NW;
+    // the second conv's A image in LDS for the whole kernel (8 waves on 4 rows: two workgroups per CU need
+    // <= 128 VGPRs, so it cannot stay in registers), else in registers
+    static constexpr bool W2LDS = NW == 8 && L == 4;
+    static constexpr int pad16(int v) { return v + ((16 - v % 32) + 32) % 32; }  // = 16 (mod 32)
     static constexpr int LH = L + 2, LW = 18, LP0 = LH * LW;           // low-res window: rows ly0 - 1 .., cols lx0 - 1 ..
-    static constexpr int LP = LP0 + ((16 - LP0 % 32) + 32) % 32;
-    static constexpr int LNT = (LP0 + 15) / 16;                         // window N-tiles (12)
+    static constexpr int LP = pad16(LP0);
+    static constexpr int LNT = (LP0 + 15) / 16;                         // window N-tiles
     static constexpr int SR = 4 * LH, SC = 72;                          // shuffled map: row 0 = Y0 - 4, col 0 = X0 - 4
     static constexpr int XR = 4 * L + 5, XC = 72;                       // x: row 0 = Y0 - 3, col 0 = X0 - 4
     static constexpr int TQ = 18, TITEMS = XR * TQ;                      // tail items (x row, column quad)
     static constexpr int QR = 2 * L + 2, QW = 34, QWP = 36;             // c1: row 0 = oy0 - 1, col 0 = ox0 - 1
-    static constexpr int QS0 = QR * QWP, QS = QS0 + ((16 - QS0 % 32) + 32) % 32;  // c1 channel stride (16 mod 32)
-    static constexpr int QP = QR * QW, QNT = (QP + 15) / 16;            // c1 pixels, N-tiles (39)
-    static constexpr int OW_UB = 128 * NF, OW_TW = OW_UB + 128, OW_TB = OW_TW + NF * 9, OW_CW = (OW_TB + 1 + 3) / 4 * 4,
+    static constexpr int QS = pad16(QR * QWP);                          // c1 channel stride (16 mod 32)
+    static constexpr int QP = QR * QW, QNT = (QP + 15) / 16;            // c1 pixels, N-tiles
+    // small per-channel constants, in LDS for the whole kernel
+    static constexpr int OW_UB = 0, OW_TW = OW_UB + 16 * NF, OW_TB = OW_TW + NF * 9, OW_CW = (OW_TB + 1 + 3) / 4 * 4,
                          OW_SC = OW_CW + 9 * C, OW_SH = OW_SC + C, OW_PS = OW_SH + C, OW_PH = OW_PS + NF,
-                         OW_PW = OW_PH + NF, OW_W2 = OW_PW + 9 * 16 * 16, OW_S2 = OW_W2 + 9 * C * C, OW_H2 = OW_S2 + C,
-                         WN = OW_H2 + C;
-    static constexpr int PR = L + 4, PW = 20, PCS = PR * PW, PXN = 16 * PCS;  // pre-conv window (PCS = 240: 16 mod 32)
+                         OW_S2 = OW_PH + NF, OW_H2 = OW_S2 + C, OW_W2 = OW_H2 + C,
+                         WN = OW_W2 + (W2LDS ? 9 * C * C : 0);
+    // the MFMA A images, staged in `un` behind the pre-conv window, read once into registers
+    static constexpr int PR = L + 4, PW = 20, PCS = pad16(PR * PW), PXN = 16 * PCS;  // pre-conv window [16][PCS]
+    static constexpr int BW = PXN, BU = 0, BP = BU + 16 * NF * NF, B2 = BP + 9 * 16 * 16, BWN = B2 + 9 * C * C;
     static constexpr int POST = NF * SR * SC + XR * XC;
-    static constexpr int UN = POST > PXN ? POST : PXN;
-    static_assert(PCS % 32 == 16 && 16 * QS <= NF * SR * SC, "layout");
+    static constexpr int UN = POST > BW + BWN ? POST : BW + BWN;
+    static_assert(PCS % 32 == 16 && 16 * QS <= NF * SR * SC && NF % NW == 0, "layout");
 };
 
-template <bool PRE>
-__global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_conv_desc d) {
-    using G = Sc7Geo;
-    constexpr int NF = G::NF, C = G::C, NT = G::NT, L = G::L, LW = G::LW, LP = G::LP, LP0 = G::LP0;
+// L low-res rows, NW waves: (4, 8) two workgroups per CU at <= 128 VGPRs (min 4 waves per SIMD), (4, 4) two at
+// <= 256, (8, 8) one (its LDS)
+template <int L, int NW>
+__global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_kernel(const esm_shuffle_conv_desc d) {
+    using G = Sc7Geo<L, NW>;
+    constexpr int NF = G::NF, C = G::C, NT = G::NT, LW = G::LW, LP = G::LP, LP0 = G::LP0;
     constexpr int SR = G::SR, SC = G::SC, XC = G::XC, WN = G::WN;
+    constexpr int CPW = NF / NW;  // shuffled-map channels per wave (phase 3)
+    constexpr bool W2LDS = G::W2LDS;
     const esm_shuffle_tail_desc& a = d.st;
     __shared__ __attribute__((aligned(16))) float wsh[WN];
     __shared__ __attribute__((aligned(16))) float lr[NF * LP];
     __shared__ __attribute__((aligned(16))) float un[G::UN];
     float* const sh = un;                    // [NF][SR][SC]
     float* const xs = un + NF * SR * SC;     // [XR][XC]
-    float* const pxs = un;                   // [16][PCS]  (PRE, until lr is built)
+    float* const pxs = un;                   // [16][PCS]  (until lr is built)
+    float* const bw = un + G::BW;            // A images (until read into registers)
     float* const qs = un;                    // c1 [C][QS] (over sh, once x is built)
 
     const int tid = threadIdx.x;
@@ -1024,142 +1042,155 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
     const int Y0 = 4 * ly0, X0 = 4 * lx0, oy0 = Y0 / 2, ox0 = X0 / 2;
     SC4_STAMP(0);
 
-    // ---- 1. stage (one round trip): every weight and the pre-conv window (or the low-res window)
-    constexpr int WRN = (WN + NT - 1) / NT;
-    float rw[WRN];
+    // ---- 1. stage (one round trip): every weight and the pre-conv window
+    constexpr int WRN = (WN + NT - 1) / NT, BRN = (G::BWN + NT - 1) / NT, PXR = (G::PXN + NT - 1) / NT;
+    float rw[WRN], rb[BRN], rp[PXR];
 #pragma unroll
     for (int k = 0; k < WRN; ++k) {
         const int i = tid + k * NT;
         const float* p;
         int off;
         float dflt = 0.f;
-        if (i < G::OW_UB) { p = a.up_w; off = i; }
-        else if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
+        if (i < G::OW_TW) { p = a.up_b; off = i - G::OW_UB; }
         else if (i < G::OW_TB) { p = a.tail_w; off = i - G::OW_TW; }
         else if (i == G::OW_TB) { p = a.tail_b; off = 0; }
         else if (i < G::OW_CW) { p = nullptr; off = 0; }
         else if (i < G::OW_SC) { p = d.w; off = (i - G::OW_CW) / C * d.cin_pad * d.cout_pad + (i - G::OW_CW) % C; }
         else if (i < G::OW_SH) { p = d.scale; off = i - G::OW_SC; dflt = 1.f; }
         else if (i < G::OW_PS) { p = d.shift; off = i - G::OW_SH; }
-        else if (i < G::OW_PH) { p = PRE ? d.pre_scale : nullptr; off = i - G::OW_PS; dflt = 1.f; }
-        else if (i < G::OW_PW) { p = PRE ? d.pre_shift : nullptr; off = i - G::OW_PH; }
-        else if (i < G::OW_W2) {  // pre-conv A image [tap][ci][co 16] (co >= nf: zero rows)
-            const int j = i - G::OW_PW, co = j & 15, ci = (j >> 4) & 15, tap = j >> 8;
-            const bool ok = PRE && ci < d.pre_cin && co < NF;
-            p = ok ? d.pre_w : nullptr;
-            off = ok ? (tap * d.pre_cin_pad + ci) * d.pre_cout_pad + co : 0;
-        } else if (i < G::OW_S2) {  // second conv A image [tap][ci][co]
+        else if (i < G::OW_PH) { p = d.pre_scale; off = i - G::OW_PS; dflt = 1.f; }
+        else if (i < G::OW_S2) { p = d.pre_shift; off = i - G::OW_PH; }
+        else if (i < G::OW_H2) { p = d.scale2; off = i - G::OW_S2; dflt = 1.f; }
+        else if (i < G::OW_W2) { p = d.shift2; off = i - G::OW_H2; }
+        else {  // (W2LDS) the second conv's A image [tap][ci][co]
             const int j = i - G::OW_W2, co = j & 15, ci = (j >> 4) & 15, tap = j >> 8;
             p = d.w2;
             off = (tap * d.cin_pad2 + ci) * d.cout_pad2 + co;
-        } else if (i < G::OW_H2) { p = d.scale2; off = i - G::OW_S2; dflt = 1.f; }
-        else { p = d.shift2; off = i - G::OW_H2; }
+        }
         const bool ok = i < WN && p != nullptr;
         const float v = (ok ? p : a.up_w)[ok ? off : 0];
         rw[k] = ok ? v : dflt;
     }
-    constexpr int PXR = PRE ? (G::PXN + NT - 1) / NT : 1;
-    constexpr int XRN = PRE ? 1 : (NF * LP + NT - 1) / NT;
-    float rp[PXR], rx[XRN];
-    if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < BRN; ++k) {
+        const int i = tid + k * NT;
+        const float* p;
+        int off;
+        bool ok = i < G::BWN;
+        if (i < G::BP) {  // upsampling's 1x1 [NF * 16 out][NF in]
+            p = a.up_w;
+            off = i;
+        } else {  // pre-conv / second conv A images [tap][ci][co 16] (pre: co >= nf zero rows)
+            const bool two = i >= G::B2;
+            const int j = i - (two ? G::B2 : G::BP), co = j & 15, ci = (j >> 4) & 15, tap = j >> 8;
+            p = two ? d.w2 : d.pre_w;
+            ok = ok && (two || (ci < d.pre_cin && co < NF));
+            off = two ? (tap * d.cin_pad2 + ci) * d.cout_pad2 + co : (tap * d.pre_cin_pad + ci) * d.pre_cout_pad + co;
+        }
+        const float v = (ok ? p : a.up_w)[ok ? off : 0];
+        rb[k] = ok ? v : 0.f;
+    }
+    {
         const float* pb = d.pre_x + b * d.pb;
 #pragma unroll
         for (int k = 0; k < PXR; ++k) {
             const int i = tid + k * NT;
             const int c = i / G::PCS, rem = i - c * G::PCS;
             const int yy = ly0 - 2 + rem / G::PW, xx = lx0 - 2 + rem % G::PW;
-            const bool ok = i < G::PXN && c < d.pre_cin && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const bool ok = i < G::PXN && c < d.pre_cin && rem < G::PR * G::PW && yy >= 0 && yy < H && xx >= 0 && xx < W;
             const float v = pb[ok ? c * d.pc + yy * d.ph + xx : 0];
             rp[k] = ok ? v : 0.f;
-        }
-    } else {
-        const float* xb = a.x + b * a.xb;
-#pragma unroll
-        for (int k = 0; k < XRN; ++k) {
-            const int i = tid + k * NT;
-            const int c = i / LP, rem = i - c * LP;
-            const int yy = ly0 - 1 + rem / LW, xx = lx0 - 1 + rem % LW;
-            const bool ok = i < NF * LP && rem < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            const float v = xb[ok ? c * a.xc + yy * a.xh + xx : 0];
-            rx[k] = ok ? v : 0.f;
         }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < WRN; ++k)
         if (tid + k * NT < WN) wsh[tid + k * NT] = rw[k];
-    if constexpr (PRE) {
 #pragma unroll
-        for (int k = 0; k < PXR; ++k)
-            if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
-    } else {
+    for (int k = 0; k < BRN; ++k)
+        if (tid + k * NT < G::BWN) bw[tid + k * NT] = rb[k];
 #pragma unroll
-        for (int k = 0; k < XRN; ++k)
-            if (tid + k * NT < NF * LP) lr[tid + k * NT] = rx[k];
-    }
+    for (int k = 0; k < PXR; ++k)
+        if (tid + k * NT < G::PXN) pxs[tid + k * NT] = rp[k];
     __syncthreads();
+    // this lane's A operands: lane (g, n) holds row n, k = g of each k-step (W2LDS: the pre-conv's are read from
+    // the staged image in phase 2, the second conv's from wsh in phase 6)
+    float pa[W2LDS ? 1 : 9][4], ua[CPW][2], wa[W2LDS ? 1 : 9][4];
+    if constexpr (!W2LDS) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                pa[tap][ks] = bw[G::BP + (tap * 16 + 4 * ks + g) * 16 + n];
+                wa[tap][ks] = bw[G::B2 + (tap * 16 + 4 * ks + g) * 16 + n];
+            }
+    }
+#pragma unroll
+    for (int cc = 0; cc < CPW; ++cc)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ua[cc][kk] = bw[G::BU + ((wave + NW * cc) * 16 + n) * NF + 4 * kk + g];
     SC4_STAMP(1);
 
     // ---- 2. pre-conv on the low-res window (shuffle_conv4_kernel's MFMA form)
-    if constexpr (PRE) {
-        for (int nt = wave; nt < G::LNT; nt += L) {
-            const int p = nt * 16 + n;
-            const int pp = p < LP0 ? p : 0;
-            const int py = pp / LW, px = pp - (pp / LW) * LW;
-            conv::floatx4 acc2[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+    for (int nt = wave; nt < G::LNT; nt += NW) {
+        const int p = nt * 16 + n;
+        const int pp = p < LP0 ? p : 0;
+        const int py = pp / LW, px = pp - (pp / LW) * LW;
+        conv::floatx4 acc2[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int dy = tap / 3, dx = tap % 3;
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dy = tap / 3, dx = tap % 3;
 #pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    const int ci = 4 * ks + g;
-                    acc2[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        wsh[G::OW_PW + (tap * 16 + ci) * 16 + n], pxs[ci * G::PCS + (py + dy) * G::PW + px + dx],
-                        acc2[ks & 1], 0, 0, 0);
-                }
-            }
-            const conv::floatx4 acc = acc2[0] + acc2[1];
-            const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
-            const bool in = p < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            if (g < 2 && p < LP0) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int co = 4 * g + j;
-                    const float v = gelu_erf(acc[j] * wsh[G::OW_PS + co] + wsh[G::OW_PH + co]);
-                    lr[co * LP + p] = in ? v : 0.f;
-                }
+            for (int ks = 0; ks < 4; ++ks) {
+                const int ci = 4 * ks + g;
+                const float av = W2LDS ? bw[G::BP + (tap * 16 + ci) * 16 + n] : pa[W2LDS ? 0 : tap][ks];
+                acc2[ks & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pxs[ci * G::PCS + (py + dy) * G::PW + px + dx],
+                                                                    acc2[ks & 1], 0, 0, 0);
             }
         }
-        __syncthreads();  // lr complete; the pre-conv window (aliased by sh) is dead
+        const conv::floatx4 acc = acc2[0] + acc2[1];
+        const int yy = ly0 - 1 + py, xx = lx0 - 1 + px;
+        const bool in = p < LP0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        if (g < 2 && p < LP0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 4 * g + j;
+                const float v = gelu_erf(acc[j] * wsh[G::OW_PS + co] + wsh[G::OW_PH + co]);
+                lr[co * LP + p] = in ? v : 0.f;
+            }
+        }
     }
+    __syncthreads();  // lr complete; the pre-conv window and the A images (aliased by sh) are dead
     SC4_STAMP(2);
 
-    // ---- 3. shuffled map on the whole window: item (window tile, channel), 16x16x4 MFMA
-    for (int it = wave; it < G::LNT * NF; it += L) {
-        const int wt = it >> 3, c = it & 7;
+    // ---- 3. shuffled map on the whole window: wave w takes channels w + L cc of every window tile, 16x16x4 MFMA
+    for (int wt = 0; wt < G::LNT; ++wt) {
         const int p = wt * 16 + n;
         const int pp = p < LP0 ? p : 0;
         const int py = pp / LW, px = pp - (pp / LW) * LW;
-        conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wsh[(c * 16 + n) * NF + 4 * kk + g], lr[(4 * kk + g) * LP + pp],
-                                                      acc, 0, 0, 0);
+        const float b0 = lr[g * LP + pp], b1 = lr[(4 + g) * LP + pp];
         const int row = 4 * py + g;  // sh row: Y0 - 4 + row
         const int Y = Y0 - 4 + row, X = X0 - 4 + 4 * px;
         const bool yok = Y >= 0 && Y < HO;
-        conv::floatx4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
-            o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+        for (int cc = 0; cc < CPW; ++cc) {
+            const int c = wave + NW * cc;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cc][0], b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cc][1], b1, acc, 0, 0, 0);
+            conv::floatx4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = silu_fast(acc[j] + wsh[G::OW_UB + c * 16 + 4 * g + j]);
+                o[j] = (yok && X + j >= 0 && X + j < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+            }
+            if (p < LP0) *reinterpret_cast<conv::floatx4*>(&sh[(c * SR + row) * SC + 4 * px]) = o;
         }
-        if (p < LP0) *reinterpret_cast<conv::floatx4*>(&sh[(c * SR + row) * SC + 4 * px]) = o;
     }
     __syncthreads();
     SC4_STAMP(3);
 
-    // ---- 4. tail -> x rows Y0 - 3 .. Y0 + 33, cols X0 - 4 + 4q .. + 3 (q = 0 .. 17; cols X0 - 3 .. X0 + 65 used)
+    // ---- 4. tail -> x rows Y0 - 3 .. Y0 + 4L + 1, cols X0 - 4 + 4q .. + 3 (q = 0 .. 17; cols X0 - 3 .. X0 + 65 used)
     {
         const float tb = a.tail_b ? wsh[G::OW_TB] : 0.f;
         for (int it = tid; it < G::TITEMS; it += NT) {
@@ -1199,8 +1230,8 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
     __syncthreads();
     SC4_STAMP(4);
 
-    // ---- 5. c1 = GELU(BN(conv 3x3 s2 (x))) on rows oy0 - 1 .. oy0 + 16, cols ox0 - 1 .. ox0 + 32 (612 pixels in 16-
-    //         pixel N-tiles), zero outside the map (the second conv's padding) -> LDS
+    // ---- 5. c1 = GELU(BN(conv 3x3 s2 (x))) on rows oy0 - 1 .. oy0 + 2L, cols ox0 - 1 .. ox0 + 32 (in 16-pixel
+    //         N-tiles), zero outside the map (the second conv's padding) -> LDS
     {
         float ca[3], sc[4], shf[4];
 #pragma unroll
@@ -1213,7 +1244,7 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
             sc[j] = wsh[G::OW_SC + 4 * g + j];
             shf[j] = wsh[G::OW_SH + 4 * g + j];
         }
-        for (int nt = wave; nt < G::QNT; nt += L) {
+        for (int nt = wave; nt < G::QNT; nt += NW) {
             const int p = nt * 16 + n;
             const int pp = p < G::QP ? p : 0;
             const int qa = pp / G::QW, qb = pp - (pp / G::QW) * G::QW;
@@ -1240,7 +1271,7 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
     __syncthreads();
     SC4_STAMP(5);
 
-    // ---- 6. the second conv (3x3 16 -> 16, BN, GELU) on the 16 x 32 output tile: N-tile = 16 pixels of one row,
+    // ---- 6. the second conv (3x3 16 -> 16, BN, GELU) on the 2L x 32 output tile: N-tile = 16 pixels of one row,
     //         two tiles per wave iteration on independent accumulators; lane (g, n): k-step (tap, ks) reads channel
     //         4ks + g of pixel n; C lane (g, n): couts 4g .. 4g + 3
     {
@@ -1253,7 +1284,7 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
             sc[j] = wsh[G::OW_S2 + 4 * g + j];
             shf[j] = wsh[G::OW_H2 + 4 * g + j];
         }
-        for (int nt = 2 * wave; nt < 4 * L; nt += 2 * L) {
+        for (int nt = 2 * wave; nt < 4 * L; nt += 2 * NW) {
             conv::floatx4 acc[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
@@ -1261,11 +1292,11 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const int ci = 4 * ks + g;
-                    const float av = wsh[G::OW_W2 + (tap * 16 + ci) * 16 + n];
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const int t2 = nt + u;
                         const int oyl = t2 >> 1, oxl = 16 * (t2 & 1) + n;
+                        const float av = W2LDS ? wsh[G::OW_W2 + (tap * 16 + ci) * 16 + n] : wa[W2LDS ? 0 : tap][ks];
                         acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                             av, qs[ci * G::QS + (oyl + dy) * G::QWP + oxl + dx], acc[u], 0, 0, 0);
                     }
@@ -1294,13 +1325,18 @@ __global__ void __launch_bounds__(512) shuffle_conv11_kernel(const esm_shuffle_c
 #endif
 }
 
+// flags bits 3-4: 0 = 4 low-res rows on 8 waves (two workgroups per CU; the default), 1 = 8 rows on 8 waves (one per
+// CU; the round-5 tile), 2 = 4 rows on 4 waves
 int launch_sc11(const esm_shuffle_conv_desc& a, hipStream_t s) {
-    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, Sc7Geo::L), a.st.B);
+    const int sel = (a.st.flags >> 3) & 3;
+    const dim3 grid(ceil_div(a.st.W, 16), ceil_div(a.st.H, sel == 1 ? 8 : 4), a.st.B);
     if (grid.y > 65535u || grid.z > 65535u) return arg_error("shuffle_conv: grid too large");
-    if (a.pre_x)
-        hipLaunchKernelGGL((shuffle_conv11_kernel<true>), grid, dim3(Sc7Geo::NT), 0, s, a);
+    if (sel == 1)
+        hipLaunchKernelGGL((shuffle_conv11_kernel<8, 8>), grid, dim3(Sc7Geo<8, 8>::NT), 0, s, a);
+    else if (sel == 2)
+        hipLaunchKernelGGL((shuffle_conv11_kernel<4, 4>), grid, dim3(Sc7Geo<4, 4>::NT), 0, s, a);
     else
-        hipLaunchKernelGGL((shuffle_conv11_kernel<false>), grid, dim3(Sc7Geo::NT), 0, s, a);
+        hipLaunchKernelGGL((shuffle_conv11_kernel<4, 8>), grid, dim3(Sc7Geo<4, 8>::NT), 0, s, a);
     return check_launch("shuffle_conv");
 }
 
@@ -1368,9 +1404,9 @@ int launch_shuffle_conv(const esm_shuffle_conv_desc* d, hipStream_t s) {
     const long long Ho2 = (static_cast<long long>(t.H) * t.r + 1) / 2, Wo2 = (static_cast<long long>(t.W) * t.r + 1) / 2;
     if (a.oh < Wo2 || a.oc < Ho2 * a.oh || a.ob < a.C * a.oc) return arg_error("shuffle_conv: output strides");
     if (4 * (a.C * a.oc) >= 0x7fffffffLL) return arg_error("shuffle_conv: output too large");
-    if (a.w2) {  // the second conv fused (the row form only)
-        if (!(t.nf == 8 && t.r == 4 && a.C == 16) || (t.flags >> 1 & 3) == 1)
-            return arg_error("shuffle_conv: the second conv needs nf 8, r 4, C 16 and the row form");
+    if (a.w2) {  // the second conv fused (the row form with its pre-conv only)
+        if (!(t.nf == 8 && t.r == 4 && a.C == 16) || (t.flags >> 1 & 3) == 1 || !a.pre_x)
+            return arg_error("shuffle_conv: the second conv needs nf 8, r 4, C 16, the row form and the pre-conv");
         if (a.cin_pad2 < a.C || a.cout_pad2 < a.C || a.cin_pad2 % 16 || a.cout_pad2 % 32)
             return arg_error("shuffle_conv: bad second-conv weight padding");
         return launch_sc11(a, s);

@@ -27,7 +27,8 @@ from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_RELU6, ACT_SIGMOID, ACT_SIL
                    EsmShuffleTailDesc, EsmSmixDesc, check, lib)
 
 __all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_fmnet", "run_shuffle_tail", "pack_shuffle_tail",
-           "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID", "ACT_RELU6", "run_dwconv", "cached_pack"]
+           "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID", "ACT_RELU6", "run_dwconv", "cached_pack", "run_convt_1x1",
+           "convt_1x1_supported"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -726,6 +727,55 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     return pb.k == 1 or (light <= 25 and pa.stride == 1) or (pa.k == 1 and B * Ho * Wo <= 8192)
 
 
+# A ConvTranspose BasicConv + crop + cat + the 1x1 BasicConv after it as one launch (esm_convt_1x1_f32,
+# conv_up1.hip): the hourglasses' conv3_up -> agg_0[0] and conv2_up -> agg_1[0].  ESM_CONVT_1X1=0 keeps two
+# launches; ESM_CONVT_1X1_PAIRED=0 keeps agg_N[0] + agg_N[1] as one pair2 launch where pair2_auto takes it
+# (A/B measurements).  S-K, three alternations on one box (round 6): 0.3202-0.3214 ms with two launches,
+# 0.3127-0.3140 fused where agg_N[0] is not paired, 0.3077-0.3080 fused everywhere (the default)
+CONVT1X1_ENABLED = _ab("ESM_CONVT_1X1", "1") != "0"
+CONVT1X1_PAIRED = _ab("ESM_CONVT_1X1_PAIRED", "1") == "1"
+CONVT1X1_MAX_EXTRA = 48  # extra channels the fused kernels instantiate (conv_up1.hip kUp1MaxXB * 4)
+
+
+def convt_1x1_supported(pa: PackedConv, pb: PackedConv, extra: Sequence[torch.Tensor]) -> bool:
+    """Python mirror of conv_up1.h up1_check (plus the on/off switch)."""
+    if not CONVT1X1_ENABLED or not pa.transposed or pb.transposed or (pa.k, pa.stride, pa.pad) != (4, 2, 1):
+        return False
+    if pa.act != ACT_GELU or pa.scale is None or pa.shift is None or pa.cout > 16 or pa.cout % 4:
+        return False
+    if (pb.k, pb.stride, pb.pad) != (1, 1, 0) or pb.act != ACT_GELU or pb.cout > 16 or pb.nd != pa.nd:
+        return False
+    cx = sum(int(t.shape[1]) for t in extra)
+    return 1 <= len(extra) <= 2 and all(int(t.shape[1]) % 4 == 0 for t in extra) and 4 <= cx <= CONVT1X1_MAX_EXTRA
+
+
+def run_convt_1x1(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv, extra: Sequence[torch.Tensor],
+                  tags: Tuple[str, str] = ("convT", "conv1x1")) -> torch.Tensor:
+    """``pb(cat(crop(pa(srcs)), *extra))`` (models/ESMStereo.py:163-175, 221-234) as one launch: the transposed
+    conv's output is cropped to the extra sources' extent and never written."""
+    da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
+    nd = pa.nd
+    e0 = extra[0]
+    geo = (int(e0.shape[0]), pa.cout) + tuple(int(v) for v in e0.shape[2:])
+    virt = srcs[0].as_strided(geo, (0,) * (len(geo) - 1) + (1,))  # the crop's geometry only, never read
+    db, out, mb = _conv_desc(ctx, pb, [virt, *extra], tag=tags[1])
+    db.hint = 0
+    B = int(e0.shape[0])
+    vox = math.prod(int(v) for v in e0.shape[2:])
+    full = 4 * B * pa.cout * int(da.Ho) * int(da.Wo) * (int(da.Do) if nd == 3 else 1)
+    name = f"{tags[0]}+{'.'.join(tags[1].split('.')[-2:])}"
+    ctx.meta.append(dict(name=name, kind="conv_up1", flops=ma["flops"] + mb["flops"],
+                         bytes=ma["bytes"] - full + mb["bytes"] - 4 * B * pa.cout * vox,
+                         shape=f"{ma['shape']} + {mb['shape']}", reads=ma["reads"] + _spans(*extra), writes=mb["writes"],
+                         key=ma["key"] + " | " + mb["key"], hint=da.hint))
+    if ctx._submit():
+        if ctx.plan:
+            check(lib.esm_plan_add_convt_1x1(ctx.plan, ctypes.byref(da), ctypes.byref(db)), "plan_add_convt_1x1")
+        else:
+            check(lib.esm_convt_1x1_f32(ctypes.byref(da), ctypes.byref(db), ctx.stream), "convt_1x1")
+    return out
+
+
 # the hot path's disparity_regression folded into the upsampler's first pair (conv_pair2.hip hint bit 29):
 # one launch less on the S / M chains; ESM_PAIR_REGRESS=0 keeps the separate launch (A/B)
 PAIR_REGRESS_ENABLED = _ab("ESM_PAIR_REGRESS", "1") != "0"
@@ -1017,6 +1067,9 @@ SHUFFLE_PRE_ENABLED = _ab("ESM_SHUFFLE_PRE", "1") != "0"
 # the refinement's conv1[1] inside the same launch as well (esm_shuffle_conv_desc.w2, the whole conv1 of the 4x
 # stage in one launch; ESM_SC11=0: conv1[1] as its own launch, A/B measurements)
 SC11_ENABLED = _ab("ESM_SC11", "1") != "0"
+# tile of that launch (esm_shuffle_tail_desc.flags bits 3-4; A/B knob): 0 = 4 low-res rows on 8 waves, two
+# workgroups per CU (round 6, the default); 1 = 8 rows on 8 waves (round 5); 2 = 4 rows on 4 waves
+SC11_TILE = int(_ab("ESM_SC11_TILE", "0"))
 
 
 def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: PackedConv) -> bool:
@@ -1097,6 +1150,7 @@ def run_shuffle_conv(ctx: Ctx, x: torch.Tensor, p: PackedShuffleTail, conv: Pack
         d.scale2 = conv2.scale.data_ptr() if conv2.scale is not None else None
         d.shift2 = conv2.shift.data_ptr() if conv2.shift is not None else None
         d.cin_pad2, d.cout_pad2 = conv2.cin_pad, conv2.cout_pad
+        t.flags |= (SC11_TILE & 3) << 3
         ctx.hold(conv2.w, conv2.scale, conv2.shift)
     npix = B * H * W * r * r
     flops = 2 * npix * nf * (nf + 9) + 2 * B * Ho2 * Wo2 * conv.cout * 9  # head as shuffle_tail + the 1 -> C 3x3

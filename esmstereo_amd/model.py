@@ -326,6 +326,12 @@ class ForwardGraph:
 
     def __init__(self, model: "ESMStereo", left: torch.Tensor, right: torch.Tensor, train_status: bool):
         self.device = left.device
+        # capture, streams and the torch ops of prefix() on the input's device, whatever device is current
+        # (torch.cuda.graph() makes its capture stream on the current device)
+        with torch.cuda.device(self.device):
+            self._build(model, left, right, train_status)
+
+    def _build(self, model: "ESMStereo", left: torch.Tensor, right: torch.Tensor, train_status: bool) -> None:
         B = int(left.shape[0])
         self.both = torch.cat((left, right), 0)  # the static image buffer: [left; right], the backbone's batch
         self.left, self.right = self.both[:B], self.both[B:]
@@ -346,11 +352,12 @@ class ForwardGraph:
         self.hp.bind(self.ml, self.mr, self.att, self.up)
 
     def run(self, left: torch.Tensor, right: torch.Tensor) -> List[torch.Tensor]:
-        self.left.copy_(left)
-        self.right.copy_(right)
-        self.graph.replay()
-        self.hp.launch()
-        return [o.clone() for o in self.hp.outputs]
+        with torch.cuda.device(self.device):
+            self.left.copy_(left)
+            self.right.copy_(right)
+            self.graph.replay()
+            self.hp.launch()
+            return [o.clone() for o in self.hp.outputs]
 
     def close(self) -> None:
         self.hp.close()
@@ -374,6 +381,7 @@ class ESMStereo(nn.Module):
     """ESMStereo stereo network with the HIP hot path (reference models/ESMStereo.py:511-745)."""
 
     _HOT_MODULES = ("group_stem", "corr_stem", "agg", "aggregation_out", "upsample_module")
+    FORWARD_GRAPHS = 4  # captured whole-forward graphs kept (input shapes), as the hot-path plan cache
 
     def __init__(self, maxdisp: int, gwc: bool = False, norm_correlation: bool = True,
                  backbone: str = "efficientnet_b2", cv_scale: int = 4, *, feature_cls=None) -> None:
@@ -635,10 +643,17 @@ class ESMStereo(nn.Module):
         if fg is None:
             for k in [k for k in graphs if k[-1] != key[-1]]:  # captured under older weights: never hit again
                 graphs.pop(k).close()
+            # a caller cycling through more input shapes than the cache holds would re-capture (two warm-up
+            # forwards, a capture and a new plan) on every call: after that many evictions, shapes not in the
+            # cache take the eager backbone + cached plan instead
+            if self.__dict__.get("_fwd_evictions", 0) >= self.FORWARD_GRAPHS:
+                ml, mr, att, up = self.prefix(left, right)
+                return self.hot_path(ml, mr, att, up, train_status)
             fg = ForwardGraph(self, left, right, train_status)
             graphs[key] = fg
-            while len(graphs) > 2:
+            while len(graphs) > self.FORWARD_GRAPHS:
                 graphs.popitem(last=False)[1].close()
+                self.__dict__["_fwd_evictions"] = self.__dict__.get("_fwd_evictions", 0) + 1
         else:
             graphs.move_to_end(key)
         return fg.run(left, right)

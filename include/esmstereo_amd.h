@@ -321,6 +321,16 @@ int esm_shuffle_conv_f32(const esm_shuffle_conv_desc* desc, void* stream);
  * (models/ESMStereo.py:185-259: the refinement hourglasses' conv2 / conv3 pairs and the upsampler
  * stages' dm<t> / spx_<t> pairs.) */
 int esm_conv_pair2_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
+/* A ConvTranspose BasicConv and the 1x1 BasicConv over [its output cropped to b's extent, further sources]
+ * in one launch; replaces the decoder steps of models/ESMStereo.py:163-175 (aggregation: conv3_up ->
+ * cat(crop, conv2) -> agg_0[0], conv2_up -> cat(crop, conv1) -> agg_1[0]) and :221-234 (up_refinement, with
+ * left_f1x / left_f2x as the third source).  out_b = GELU(BN_b(conv1x1_b(cat(crop(GELU(BN_a(convT_a(a->src)))),
+ * b->src[1..])))).  a: k4 s2 p1, one source, 4 / 8 / 12 / 16 outputs, BN + GELU, plain epilogue; a->out is
+ * not written (may be NULL).  b: 1x1 stride 1, b->src[0].C = a->Cout (its ptr is not read; b's input extent
+ * is the crop, at most a's output extent), b->src[1..2]: 4-channel multiples, at most 48 channels together;
+ * <= 16 outputs, BN + GELU, plain epilogue.  a->hint picks the transposed conv's form (bit 23: LDS-tiled,
+ * bits 26-27 rows per wave 1 / 2; bit 21: lean), 0 = automatic.  ESM_ERR_ARG outside that set. */
+int esm_convt_1x1_f32(const esm_conv_desc* a, const esm_conv_desc* b, void* stream);
 /* Confidence-head stages (models/ESMStereo_confidence.py), fp32 NCHW, contiguous:
  *   ESM_CONF_COST_FEATURES  x[0] = cost [B,D,H,W] (D >= 7) -> out [B,7,H,W]: the 7 largest of
  *                           softmax(-100 * cost / sqrt(sum_d cost^2 + 1e-6)) over D, descending (:647-654)
@@ -375,6 +385,7 @@ int esm_plan_add_fmnet(esm_plan* plan, const esm_fmnet_desc* desc);
 int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc);
 int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc);
 int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
+int esm_plan_add_convt_1x1(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_gwc_stem(esm_plan* plan, const esm_conv_desc* stem, const float* L, const float* R, int C, int G);

@@ -72,6 +72,27 @@ def flip_masked(name: str, got: torch.Tensor, ref: torch.Tensor, flips: torch.Te
     return rep
 
 
+def init_nonflip(name: str, got: torch.Tensor, ref: torch.Tensor, flips: torch.Tensor, margin: torch.Tensor
+                 ) -> Dict[str, float]:
+    """ESMStereo-L ``init_pred`` (regression_topk at low resolution, per pixel): a top-2 flip changes that
+    pixel only, so every low-res pixel whose top-2 set matches the reference's is checked, with no
+    dilation: EPE <= 1e-3 px over them, and every flip must sit on a reference margin
+    <= TOPK_MARGIN_TOL.  got / ref / flips / margin: [B, h, w]."""
+    got = got.detach().double().cpu()
+    ref = torch.as_tensor(ref).double().cpu()
+    flips = flips.cpu()
+    bad = flips & (margin.cpu().double() > TOPK_MARGIN_TOL)
+    assert not bad.any(), (name, "top-2 flip where the reference margin exceeds the tolerance",
+                           margin.cpu()[bad][:8].tolist())
+    keep = ~flips
+    d = (got - ref).abs()
+    rep = {"flips": int(flips.sum()), "lowres_px": int(flips.numel()), "checked_frac": float(keep.double().mean()),
+           "epe_nonflip": float(d[keep].mean()) if keep.any() else 0.0,
+           "max_err_nonflip": float(d[keep].max()) if keep.any() else 0.0, "epe_all": float(d.mean())}
+    assert rep["epe_nonflip"] <= EPE_TOL, (name, rep)
+    return rep
+
+
 def rel(a, b) -> float:
     a = torch.as_tensor(a).detach().double().cpu()
     b = torch.as_tensor(b).double().cpu()
@@ -99,7 +120,8 @@ def check_fullsize(name: str, m: dict, g: Dict[str, np.ndarray], cost: torch.Ten
                    disp0: torch.Tensor, disp0_from_ref_init: Optional[torch.Tensor] = None) -> Dict[str, float]:
     """cost [B, D, h, w], init [B, 1, h, w], disp0 [B, H, W] from the path under test vs the
     reference fixture.  S (continuous disparity_regression): EPE <= 1e-3 on init and on the
-    subsampled disp_0; L: the flip-masked metric on both.  ``disp0_from_ref_init`` [B, H, W]: the
+    subsampled disp_0; L: init at every low-res pixel whose top-2 set did not flip (no dilation), the
+    flip-masked metric on disp_0.  ``disp0_from_ref_init`` [B, H, W]: the
     upsampler under test run on the REFERENCE's own init_pred (g["init_pred"]), which carries every
     top-2 decision the reference made, so it must match disp_0 at EVERY pixel (EPE <= 1e-3, no mask):
     this pins the upsampler where the flip mask would hide it."""
@@ -125,7 +147,9 @@ def check_fullsize(name: str, m: dict, g: Dict[str, np.ndarray], cost: torch.Ten
         flips = (top2_sets(cost) != torch.sort(torch.from_numpy(g["top3_idx"][:, :2]).long(), 1)[0]).any(1)
         tv = torch.from_numpy(g["top3_val"])
         margin = tv[:, 1] - tv[:, 2]
-        rep["init"] = flip_masked(name + ":init", init[:, 0], g["init_pred"][:, 0], flips, margin, 4)
+        # init: every pixel that did not flip, no dilation; disp_0: the dilated flip mask (a flip moves the
+        # upsampler's output over its receptive field)
+        rep["init"] = init_nonflip(name + ":init", init[:, 0], g["init_pred"][:, 0], flips, margin)
         rep["disp0"] = flip_masked(name + ":disp0", sub, ref_sub, flips, margin, 4)
     else:
         rep["init_epe"] = float((init.detach().double().cpu() - torch.from_numpy(g["init_pred"]).double()).abs().mean())

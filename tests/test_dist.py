@@ -170,6 +170,21 @@ def test_bench_launches_its_own_ranks(extra, want):
     line = lines[0]
     assert line["n_gpus"] == 2 and line["global_batch"] == want[0]
     assert line["gathered_shape"] == want[1] and line["scaling"] == want[2]
+    assert line["gather_rank_order_ok"] is True
+    assert line["value"] > 0
+
+
+def test_bench_world8_configs3_strong_scaling():
+    """configs[3]'s shape at world size 8: `bench.py --gpus 8 --global-batch 32` starts 8 gloo
+    ranks with 4 pairs each, gathers [8, 4, H, W] every step in rank order, and counts all 32 pairs."""
+    rc, lines, err = _bench("--gpus", "8", "--cpu-standin", "--global-batch", "32", "--steps", "3", "--warmup", "1",
+                            timeout=300)
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    line = lines[0]
+    assert line["n_gpus"] == 8 and line["global_batch"] == 32 and line["scaling"] == "strong"
+    assert line["gathered_shape"] == [8, 4, 8, 16]
+    assert line["gather_rank_order_ok"] is True
     assert line["value"] > 0
 
 

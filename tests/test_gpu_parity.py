@@ -761,10 +761,20 @@ def test_shuffle_conv_pre(cp, H, W):
     conv2, bn2 = _mk(2, 16, 16, 3, 1, 1, seed=H + 2)
     ref2 = _ref_conv([ref.double()], conv2, bn2, ACT_GELU)
     pc2 = pk(conv2, bn2, ACT_GELU)
-    y2 = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp, conv2=pc2)
-    assert y2.shape == ref2.shape
-    assert rel(y2, ref2) < 1e-5
-    assert rel(y2, run_conv(ctx, pc2, [y])) < 1e-5
+    from esmstereo_amd import engine as EN
+    rows0 = EN.SC11_TILE
+    try:
+        for rows in (0, 1, 2):  # round 6: 4 low-res rows on 8 / 4 waves (two workgroups per CU); the round-5 8-row tile
+            EN.SC11_TILE = rows
+            y2 = run_shuffle_conv(ctx, c.to(DEV), p, pc, pre=pp, conv2=pc2)
+            assert y2.shape == ref2.shape
+            assert rel(y2, ref2) < 1e-5, rows
+            assert rel(y2, run_conv(ctx, pc2, [y])) < 1e-5, rows
+    finally:
+        EN.SC11_TILE = rows0
+    # the fused second conv needs the pre-conv: a descriptor with w2 and no pre_x is an argument error
+    with pytest.raises((ValueError, RuntimeError)):
+        run_shuffle_conv(ctx, x.to(DEV), p, pc, conv2=pc2)
 
 
 PAIR2_CASES = [  # (cins, kA, sA, pA, kB, pB, coutB, H, W): the shapes the hot paths use, then ragged ones
@@ -823,6 +833,69 @@ def test_conv_pair2_regress(B, D, H, W):
     assert torch.equal(y, two)
     ref = (cost * torch.arange(D, dtype=torch.float32).view(1, D, 1, 1)).sum(1, keepdim=True)
     assert rel(init, ref) < 1e-6
+
+
+UP1_CASES = [  # (nd, cin, cy, extra channels, coutb, input grid, crop, B, hint of the transposed conv)
+    (3, 24, 16, (16,), 16, (2, 3, 10), (3, 6, 20), 1, 0),              # S aggregation conv3_up -> agg_0.0
+    (3, 16, 12, (12,), 12, (3, 6, 20), (6, 12, 39), 1, 0),             # S aggregation conv2_up -> agg_1.0
+    (2, 16, 16, (16, 24), 16, (48, 156), (96, 312), 1, 0x4800000),     # S ref4x conv3_up -> agg_0.0, tiled rows 1
+    (2, 16, 16, (16, 24), 16, (96, 312), (192, 624), 1, 0x4800000),    # S ref4x conv2_up -> agg_1.0, tiled rows 1
+    (2, 16, 16, (16, 24), 16, (96, 312), (192, 624), 1, 0x8800000),    # ... tiled rows 2
+    (2, 16, 16, (16, 24), 16, (96, 312), (192, 624), 1, 0),            # ... automatic (lean)
+    (2, 16, 16, (16, 32), 16, (12, 39), (24, 78), 1, 0),               # S ref2x conv3_up -> agg_0.0
+    (2, 16, 16, (16, 32), 16, (24, 78), (48, 156), 1, 0),              # S ref2x conv2_up -> agg_1.0
+    (3, 24, 8, (4,), 12, (3, 7, 9), (5, 13, 17), 2, 0x20200000),       # ragged crops, 8-wave lean, batch 2
+    (3, 20, 16, (8, 4), 8, (3, 5, 10), (6, 9, 20), 2, 0x4800000),      # 3-D tiled rows 1, three sources
+    (2, 12, 12, (16, 32), 16, (11, 19), (21, 37), 2, 0x8800000),       # 2-D tiled, odd crop, batch 2
+    (2, 12, 4, (48,), 5, (11, 19), (22, 37), 2, 0),                    # 4 couts, 48 extra channels
+]
+
+
+@pytest.mark.parametrize("nd,cin,cy,cxs,coutb,grid,crop,B,hint", UP1_CASES)
+def test_convt_1x1(nd, cin, cy, cxs, coutb, grid, crop, B, hint):
+    """ConvTranspose BasicConv + crop + cat + 1x1 BasicConv in one launch (conv_up1.hip) vs fp64 torch of the
+    reference layers and vs the two separate launches (relative 1e-5), in the lean and LDS-tiled forms."""
+    from esmstereo_amd.engine import convt_1x1_supported, run_convt_1x1
+    ca, ba = _mk(nd, cin, cy, 4, 2, 1, transposed=True, seed=51 + cin)
+    cb, bb = _mk(nd, cy + sum(cxs), coutb, 1, 1, 0, seed=52 + coutb)
+    x = torch.randn(B, cin, *grid)
+    xs = [torch.randn(B, c, *crop) for c in cxs]
+    u = _ref_conv([x], ca, ba, ACT_GELU)
+    u = u[(slice(None), slice(None)) + tuple(slice(0, n) for n in crop)]
+    ref = _ref_conv([u, *xs], cb, bb, ACT_GELU)
+    pa_, pb_ = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
+    xd, xsd = x.to(DEV), [t.to(DEV) for t in xs]
+    assert convt_1x1_supported(pa_, pb_, xsd)
+    ctx = Ctx(DEV)
+    from esmstereo_amd import engine as EN
+    old = dict(EN.HINT_SET)
+    EN.HINT_SET["convT"] = hint
+    try:
+        y = run_convt_1x1(ctx, pa_, [xd], pb_, xsd)
+    finally:
+        EN.HINT_SET.clear()
+        EN.HINT_SET.update(old)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-5
+    ud = run_conv(ctx, pa_, [xd])
+    two = run_conv(ctx, pb_, [ud[(slice(None), slice(None)) + tuple(slice(0, n) for n in crop)], *xsd])
+    assert rel(y, two) < 1e-5
+
+
+def test_convt_1x1_rejects():
+    """Shapes outside the fused form raise the library's argument error (no silent fallback)."""
+    from esmstereo_amd.engine import run_convt_1x1
+    ca, ba = _mk(2, 16, 24, 4, 2, 1, transposed=True, seed=61)  # 24 outputs: more than one cout tile
+    cb, bb = _mk(2, 40, 16, 1, 1, 0, seed=62)
+    with pytest.raises(E.EsmError):
+        run_convt_1x1(Ctx(DEV), pk(ca, ba, ACT_GELU), [torch.randn(1, 16, 8, 8, device=DEV)], pk(cb, bb, ACT_GELU),
+                      [torch.randn(1, 16, 16, 16, device=DEV)])
+    ca, ba = _mk(2, 16, 16, 4, 2, 1, transposed=True, seed=63)
+    cb, bb = _mk(2, 16 + 64, 16, 1, 1, 0, seed=64)  # 64 extra channels: more than the kernels hold
+    with pytest.raises(E.EsmError):
+        run_convt_1x1(Ctx(DEV), pk(ca, ba, ACT_GELU), [torch.randn(1, 16, 8, 8, device=DEV)], pk(cb, bb, ACT_GELU),
+                      [torch.randn(1, 64, 16, 16, device=DEV)])
 
 
 def test_conv_multisource_crop_and_epilogues():

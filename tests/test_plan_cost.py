@@ -32,7 +32,7 @@ CASES = {  # name: (variant, backbone, cv_scale, B, H, W, maxdisp)
     "L-K B4": ("L", "efficientnet_b2", 4, 4, 384, 1248, 192),
     "Mid": ("L", "efficientnet_b2", 4, 1, 1024, 1504, 256),
 }
-CONV_KINDS = ("conv", "conv_pair", "shuffle_tail", "shuffle_conv", "fmnet", "gwc_stem")
+CONV_KINDS = ("conv", "conv_pair", "shuffle_tail", "shuffle_conv", "fmnet", "gwc_stem", "conv_up1")
 
 
 def _plan(case):
@@ -124,6 +124,19 @@ def test_plan_per_op_cost(case):
                 ba += 4 * B * D * h * w  # the D cost planes read; the map is written instead of read
             assert op["flops"] == fa + fb, name
             assert op["bytes"] == ba + bb - 2 * 4 * mid, name  # the intermediate map never reaches HBM
+        elif kind == "conv_up1":  # round 6: transposed conv + crop + cat + 1x1, the conv's output never written
+            sa, sb = shape.split(" + ")
+            na = name.split("+")[0]
+            nb = na.rsplit(".", 1)[0] + "." + name.split("+")[1]
+            ga, gb = re.search(r"in (\S+) out (\S+)", sa), re.search(r"in (\S+) out (\S+)", sb)
+            la, lb = _layer(m, na), _layer(m, nb)
+            fa, ba, wa, nout = _conv_cost(la, B, _ext(ga.group(1)), _ext(ga.group(2)))
+            fb, bb, wb, _ = _conv_cost(lb, B, _ext(gb.group(1)), _ext(gb.group(2)))
+            cy = la.weight.shape[1]
+            crop = _ext(gb.group(1))[-la.weight.dim() + 2:]
+            assert all(c <= u for c, u in zip(crop, wa)), name
+            assert op["flops"] == fa + fb, name
+            assert op["bytes"] == ba + bb - 4 * nout - 4 * B * cy * math.prod(crop), name
         elif kind in ("shuffle_tail", "shuffle_conv"):
             g = re.search(r"nf(\d+) r(\d+) in (\d+)x(\d+)", shape)
             nf, r, hi, wi = (int(v) for v in g.groups())
