@@ -35,17 +35,9 @@ inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned
 // library form branches per value under an exec mask, so the four values a lane finishes in an
 // MFMA epilogue run one after the other as serial dependency chains; branch-free, they interleave
 // (profiles/r02_pmc_*: ~2600 VALU per wave and 43 % issue stalls in the pair kernel were mostly erf).
-//
-// Round 6: the two Horner chains run as ONE chain of packed FMAs (v_pk_fma_f32, two fp32 FMAs per lane per
-// instruction at full rate on gfx950): lane pair (s, l) = (x^2 polynomial, |x| polynomial), the shorter x^2 chain
-// led by a zero coefficient (fma(x2, 0, c0) = c0 exactly).  Every FMA is the scalar form's, so the result is
-// bit-identical (ESM_ERF_SCALAR builds the scalar chains for A/B); 7 packed FMAs replace 13 scalar ones in every
-// GELU of every BasicConv epilogue.
-typedef float erf_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float erf_bf(float x) {
     const float ax = fabsf(x);
     const float x2 = x * x;
-#ifdef ESM_ERF_SCALAR
     float s = fmaf(x2, __int_as_float(0xba1345e1), __int_as_float(0x3ba10414));
     s = fmaf(x2, s, __int_as_float(0xbcdac9b8));
     s = fmaf(x2, s, __int_as_float(0x3de703be));
@@ -59,18 +51,6 @@ __device__ __forceinline__ float erf_bf(float x) {
     l = fmaf(ax, l, __int_as_float(0x3f228afd));
     l = fmaf(ax, l, __int_as_float(0x3e03c728));
     l = fmaf(ax, l, ax);
-#else
-    const erf_f2 v = {x2, ax};
-    erf_f2 p = __builtin_elementwise_fma(v, erf_f2{0.f, __int_as_float(0x378e98ab)},
-                                         erf_f2{__int_as_float(0xba1345e1), __int_as_float(0xb9c68948)});
-    p = __builtin_elementwise_fma(v, p, erf_f2{__int_as_float(0x3ba10414), __int_as_float(0x3b7cd369)});
-    p = __builtin_elementwise_fma(v, p, erf_f2{__int_as_float(0xbcdac9b8), __int_as_float(0xbcc618b2)});
-    p = __builtin_elementwise_fma(v, p, erf_f2{__int_as_float(0x3de703be), __int_as_float(0x3dda74e4)});
-    p = __builtin_elementwise_fma(v, p, erf_f2{__int_as_float(0xbec09330), __int_as_float(0x3f228afd)});
-    p = __builtin_elementwise_fma(v, p, erf_f2{__int_as_float(0x3e0375d0), __int_as_float(0x3e03c728)});
-    p = __builtin_elementwise_fma(erf_f2{ax, ax}, p, erf_f2{ax, ax});
-    const float rs = p[0], l = p[1];
-#endif
     // 1 - exp(-l) with the hardware exp2 (v_exp_f32, 1 ulp) instead of the library expf's range reduction:
     // l >= 0.84 here, so exp(-l) <= 0.43 and its rounding moves erf by < 2^-24 relative (the GELU test's
     // 2.5e-7 |x| bound vs fp64 holds); ~10 fewer instructions per GELU in every BasicConv epilogue

@@ -55,13 +55,17 @@ struct T3Geo {
 
 // NS: input sources (a channel concat of up to 3, 4-channel aligned splits; 1x1x1 only): every k-step
 // lies inside one source, whose descriptor and offsets are selected per k-step (wave-uniform)
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false>
+// WREG (plane pairs only, round 6): each lane loads its composite-weight A operands straight into registers (36
+// per k-step, reloaded for the next k-step right after their last MFMA) instead of the workgroup staging them in
+// LDS: 18 KB less LDS per workgroup (agg at L-K: 2 -> 4 workgroups per CU), no weight stores
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false, bool WREG = false>
 __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
+    static_assert(!WREG || PZ, "register weights: plane pairs only");
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
-    constexpr int XR = G::XR, WR = G::WR, NR = G::NR;
+    constexpr int XR = G::XR, WR = WREG ? 1 : G::WR, NR = G::NR;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
-    __shared__ __attribute__((aligned(16))) float ws[2][G::WL];
+    __shared__ __attribute__((aligned(16))) float ws[WREG ? 1 : 2][WREG ? 1 : G::WL];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, g = lane >> 4, n = lane & 15;
@@ -176,8 +180,10 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         } else {
             load_src(std::integral_constant<int, (NS > 2 ? 2 : 0)>{}, c0);
         }
+        if constexpr (!WREG) {
 #pragma unroll
-        for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
+            for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
+        }
     };
     auto stage_store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -185,9 +191,27 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
             const int e = tid + k * kT3Threads;
             if (e < G::XE) xs[buf][e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
         }
+        if constexpr (!WREG) {
 #pragma unroll
-        for (int k = 0; k < WR; ++k)
-            if (wdst[k] >= 0) ws[buf][wdst[k]] = wv[k];
+            for (int k = 0; k < WR; ++k)
+                if (wdst[k] >= 0) ws[buf][wdst[k]] = wv[k];
+        }
+    };
+    // WREG: lane (g, n)'s A operand of (input plane p, tap t9) at the k-step of channel c0 is
+    // W[dz = p - n / 8][t9][c0 + g][n % 8] (zero outside dz 0..2 or past Cout)
+    unsigned wpo[4];
+    float wa[WREG ? 36 : 1];
+    if constexpr (WREG) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int dz = p - (n >> 3), co = n & 7;
+            wpo[p] = (dz >= 0 && dz <= 2 && co < a.Cout)
+                         ? 4u * static_cast<unsigned>((dz * 9 * a.cin_pad + g) * a.cout_pad + co)
+                         : kOOB;
+        }
+    }
+    auto wreg_load = [&](int i, int c0) __attribute__((always_inline)) {
+        if constexpr (WREG) wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + c0) * a.cout_pad);
     };
 
     // epilogue constants, loaded while the first k-step streams in
@@ -211,6 +235,10 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
 
     const int nchunk = (a.Cin + 3) >> 2;
     stage_load(0);
+    if constexpr (WREG) {
+#pragma unroll
+        for (int i = 0; i < 36; ++i) wreg_load(i, 0);
+    }
     stage_store(0);
     __syncthreads();
     for (int ch = 0; ch < nchunk; ++ch) {
@@ -218,7 +246,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
         const float* xw = &xs[buf][g * CS + (yw * NT * S) * IX + n * S];
         if constexpr (PZ) {
-            const float* wp = &ws[buf][g * 16 + n];
+            const float* wp = &ws[WREG ? 0 : buf][g * 16 + n];
 #pragma unroll
             for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -228,10 +256,12 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
                     for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy) {
-                        const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
+                        const float av = WREG ? wa[WREG ? p * 9 + dy * 3 + dx : 0] : wp[((p * 9 + dy * 3 + dx) * 4) * 16];
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt)
                             acc[nt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt][0], 0, 0, 0);
+                        // (a k-step past the last one reads weights no MFMA uses; the range check bounds it)
+                        wreg_load(p * 9 + dy * 3 + dx, 4 * (ch + 1));
                     }
                 }
         } else {
@@ -638,7 +668,7 @@ int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
     return arg_error("conv(tile3 transposed): at most 96 output channels");
 }
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false, bool WREG = false>
 int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
@@ -649,10 +679,11 @@ int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2>), grid, dim3(kT3Threads), 0, s,
-                           a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2, WREG>), grid, dim3(kT3Threads), 0,
+                           s, a, ncg);
     else
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2>), grid, dim3(kT3Threads), 0, s, a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2, WREG>), grid, dim3(kT3Threads), 0, s, a,
+                           ncg);
     return check_launch("conv(tile3)");
 }
 
@@ -792,10 +823,12 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
         if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
         return launch_t3_mt<2, 3, 1, 2>(a, s);
     }
-    if (a.Cout <= 8) {  // plane pairs
-        if (rsel == 1) return launch_t3<1, 3, 1, 1, 4, true>(a, s, 1);
-        if (rsel == 2 || (rsel == 0 && vox < (1LL << 20))) return launch_t3<1, 3, 1, 2, 4, true>(a, s, 1);
-        return launch_t3<1, 3, 1, 4, 4, true>(a, s, 1);
+    if (a.Cout <= 8) {  // plane pairs; hint bit 29: weights staged in LDS (round 5), else in registers (round 6)
+        const bool lw = (a.hint >> 29) & 1;
+        if (rsel == 1) return lw ? launch_t3<1, 3, 1, 1, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 1, 4, true, 1, false, true>(a, s, 1);
+        if (rsel == 2 || (rsel == 0 && vox < (1LL << 20)))
+            return lw ? launch_t3<1, 3, 1, 2, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 2, 4, true, 1, false, true>(a, s, 1);
+        return lw ? launch_t3<1, 3, 1, 4, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 4, 4, true, 1, false, true>(a, s, 1);
     }
     if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
     if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);

@@ -41,14 +41,17 @@ struct GsGeo {
     static_assert(FE < (1 << 15), "packed LDS indices are 15 bits");
 };
 
-template <int NT, int CPG, int ACT, bool PLAIN>
-__global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_desc a, const float* __restrict__ Lf,
-                                                              const float* __restrict__ Rf, int C) {
+// WREG (round 6): every lane loads its composite-weight A operands of a k-step straight into registers
+// (36 per lane, one k-step ahead, from L1 / L2: the 27 x 32 x 8 stem weights), so the weights take no LDS and
+// three workgroups fit on a CU (52.6 KB instead of 71 KB at NT = 4); else they are staged in LDS per k-step
+template <int NT, int CPG, int ACT, bool PLAIN, bool WREG>
+__global__ void __launch_bounds__(kGsThreads, WREG ? 3 : 2) gwc_stem_kernel(const esm_conv_desc a, const float* __restrict__ Lf,
+                                                                            const float* __restrict__ Rf, int C) {
     using G = GsGeo<NT, CPG>;
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, CS0 = G::CS0;
     constexpr int WR = G::WR, LR = G::LR, RR = G::RR, NR = NT + 2;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
-    __shared__ __attribute__((aligned(16))) float ws[2][G::WE];
+    __shared__ __attribute__((aligned(16))) float ws[WREG ? 1 : 2][WREG ? 1 : G::WE];
     __shared__ float fs[2][G::FE];  // [left: FC][IY][IX] then [right: FC][IY][RX]
 
     const int tid = threadIdx.x;
@@ -123,7 +126,23 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
         woff[k] = ok ? 4u * static_cast<unsigned>(((dz * 9 + t9) * a.cin_pad + ci) * a.cout_pad + co) : kOOB;
     }
 
-    float lv[LR], rv[RR], wv[WR];
+    // WREG: lane (g, n)'s A operand of (input plane p, tap t9) at k-step ch is W[dz = p - n / 8][t9][4 ch + g][n % 8]
+    // (zero outside dz 0..2 or past Cout): per-lane offset of plane p, the tap and k-step in soffset
+    unsigned wpo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int dz = p - (n >> 3), co = n & 7;
+        wpo[p] = (dz >= 0 && dz <= 2 && co < a.Cout) ? 4u * static_cast<unsigned>((dz * 9 * a.cin_pad + g) * a.cout_pad + co)
+                                                     : kOOB;
+    }
+    // one register per (p, t9): reloaded with the next k-step's value right after its last MFMA of this k-step
+    // (a k-step past the last one reads weights no MFMA uses; the buffer range check keeps it inside the slab)
+    float wa[WREG ? 36 : 1];
+    auto wreg_load = [&](int i, int ch) __attribute__((always_inline)) {
+        if constexpr (WREG) wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + 4 * ch) * a.cout_pad);
+    };
+
+    float lv[LR], rv[RR], wv[WREG ? 1 : WR];
     auto fload = [&](int ch) __attribute__((always_inline)) {
         const int so = 4 * G::FC * ch * HW;
 #pragma unroll
@@ -144,14 +163,18 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
         }
     };
     auto wload = [&](int ch) __attribute__((always_inline)) {
+        if constexpr (!WREG) {
 #pragma unroll
-        for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * 4 * ch * a.cout_pad);
+            for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * 4 * ch * a.cout_pad);
+        }
     };
     auto wstore = [&](int buf) __attribute__((always_inline)) {
+        if constexpr (!WREG) {
 #pragma unroll
-        for (int k = 0; k < WR; ++k) {
-            const int e = tid + k * kGsThreads;
-            if (e < G::WE) ws[buf][e] = wv[k];
+            for (int k = 0; k < WR; ++k) {
+                const int e = tid + k * kGsThreads;
+                if (e < G::WE) ws[buf][e] = wv[k];
+            }
         }
     };
     // two planes (iz, iz + 1) of one column of a k-step's window from the staged feature windows
@@ -163,24 +186,22 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
 #pragma unroll
             for (int c = 0; c < CPG; ++c) lft[r][c] = fs[fb][cl[r] + c * G::LW];
     };
+    // the two planes as packed fp32 (v_pk_mul_f32 / v_pk_add_f32: per plane the same operations, so the same bits)
+    typedef float f2 __attribute__((ext_vector_type(2)));
     auto volume_pair = [&](int u, int fb, int buf) __attribute__((always_inline)) {
         const int r = u / (IZ / 2), iz = 2 * (u % (IZ / 2));
         const float inv = 1.0f / static_cast<float>(CPG);
-        float s0, s1;
+        f2 sv;
         {
 #pragma clang fp contract(off)
-            s0 = lft[r][0] * fs[fb][cr[r] - iz];
-            s1 = lft[r][0] * fs[fb][cr[r] - iz - 1];
+            sv = f2{lft[r][0], lft[r][0]} * f2{fs[fb][cr[r] - iz], fs[fb][cr[r] - iz - 1]};
 #pragma unroll
-            for (int c = 1; c < CPG; ++c) {
-                s0 = s0 + lft[r][c] * fs[fb][cr[r] + c * G::RW - iz];
-                s1 = s1 + lft[r][c] * fs[fb][cr[r] + c * G::RW - iz - 1];
-            }
-            s0 = s0 * inv;
-            s1 = s1 * inv;
+            for (int c = 1; c < CPG; ++c)
+                sv = sv + f2{lft[r][c], lft[r][c]} * f2{fs[fb][cr[r] + c * G::RW - iz], fs[fb][cr[r] + c * G::RW - iz - 1]};
+            sv = sv * f2{inv, inv};
         }
-        xs[buf][cx[r] + iz * PLANE] = (vm >> (r * IZ + iz)) & 1u ? s0 : 0.f;
-        xs[buf][cx[r] + (iz + 1) * PLANE] = (vm >> (r * IZ + iz + 1)) & 1u ? s1 : 0.f;
+        xs[buf][cx[r] + iz * PLANE] = (vm >> (r * IZ + iz)) & 1u ? sv[0] : 0.f;
+        xs[buf][cx[r] + (iz + 1) * PLANE] = (vm >> (r * IZ + iz + 1)) & 1u ? sv[1] : 0.f;
     };
     constexpr int NU = NRND * IZ / 2;  // plane pairs per thread and k-step
 
@@ -200,6 +221,10 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
     const int nchunk = a.Cin >> 2;
     fload(0);
     wload(0);
+    if constexpr (WREG) {
+#pragma unroll
+        for (int i = 0; i < 36; ++i) wreg_load(i, 0);
+    }
     fstore(0);
     wstore(0);
     fload(1);
@@ -217,7 +242,7 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
         // stores that wait for them, and every k-step then waits out a full memory latency
         __builtin_amdgcn_sched_barrier(0);
         const float* xw = &xs[buf][g * CS + n];
-        const float* wp = &ws[buf][g * 16 + n];
+        const float* wp = &ws[WREG ? 0 : buf][g * 16 + n];
         load_left((ch + 1) & 1);
 #pragma unroll
         for (int it = 0; it < 12; ++it) {
@@ -227,10 +252,11 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
             for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + p) * PLANE + r * IX + dx];
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy) {
-                const float av = wp[((p * 9 + dy * 3 + dx) * 4) * 16];
+                const float av = WREG ? wa[WREG ? p * 9 + dy * 3 + dx : 0] : wp[((p * 9 + dy * 3 + dx) * 4) * 16];
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, br[nt + dy], acc[nt], 0, 0, 0);
+                wreg_load(p * 9 + dy * 3 + dx, ch + 1);
             }
             // k-step ch + 1's volume window, spread over the MFMA stream
 #pragma unroll
@@ -275,7 +301,7 @@ __global__ void __launch_bounds__(kGsThreads) gwc_stem_kernel(const esm_conv_des
     }
 }
 
-template <int NT, int CPG>
+template <int NT, int CPG, bool WREG>
 int launch_gs(const esm_conv_desc& a, const float* L, const float* R, int C, hipStream_t s) {
     using G = GsGeo<NT, CPG>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB);
@@ -284,9 +310,9 @@ int launch_gs(const esm_conv_desc& a, const float* L, const float* R, int C, hip
     const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
     const bool plain = a.act == ESM_ACT_GELU && a.post_scale == 1.f;
     if (plain)
-        hipLaunchKernelGGL((gwc_stem_kernel<NT, CPG, ESM_ACT_GELU, true>), grid, dim3(kGsThreads), 0, s, a, L, R, C);
+        hipLaunchKernelGGL((gwc_stem_kernel<NT, CPG, ESM_ACT_GELU, true, WREG>), grid, dim3(kGsThreads), 0, s, a, L, R, C);
     else
-        hipLaunchKernelGGL((gwc_stem_kernel<NT, CPG, -1, false>), grid, dim3(kGsThreads), 0, s, a, L, R, C);
+        hipLaunchKernelGGL((gwc_stem_kernel<NT, CPG, -1, false, WREG>), grid, dim3(kGsThreads), 0, s, a, L, R, C);
     return check_launch("gwc_stem");
 }
 
@@ -319,8 +345,11 @@ int launch_gwc_stem(const esm_conv_desc& a, const float* L, const float* R, int 
     // rows per wave as the tiled stem's automatic choice (conv_tile3.hip launch_tile3, plane pairs)
     const long long vox = static_cast<long long>(a.B) * a.Do * a.Ho * a.Wo;
     const int rsel = (a.hint >> 26) & 3;
-    if (rsel == 2 || (rsel == 0 && vox < (1LL << 20))) return launch_gs<2, 2>(a, L, R, C, s);
-    return launch_gs<4, 2>(a, L, R, C, s);
+    // hint bit 28: the LDS-staged weights (round 5); default: weights in registers (round 6)
+    const bool lds_w = (a.hint >> 28) & 1;
+    if (rsel == 2 || (rsel == 0 && vox < (1LL << 20)))
+        return lds_w ? launch_gs<2, 2, false>(a, L, R, C, s) : launch_gs<2, 2, true>(a, L, R, C, s);
+    return lds_w ? launch_gs<4, 2, false>(a, L, R, C, s) : launch_gs<4, 2, true>(a, L, R, C, s);
 }
 
 }  // namespace conv

@@ -1131,7 +1131,8 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
         for (int kk = 0; kk < 2; ++kk) ua[cc][kk] = bw[G::BU + ((wave + NW * cc) * 16 + n) * NF + 4 * kk + g];
     SC4_STAMP(1);
 
-    // ---- 2. pre-conv on the low-res window (shuffle_conv4_kernel's MFMA form)
+    // ---- 2. pre-conv on the low-res window (shuffle_conv4_kernel's MFMA form); two tiles interleaved per wave
+#pragma unroll 2
     for (int nt = wave; nt < G::LNT; nt += NW) {
         const int p = nt * 16 + n;
         const int pp = p < LP0 ? p : 0;
@@ -1164,6 +1165,8 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
     SC4_STAMP(2);
 
     // ---- 3. shuffled map on the whole window: wave w takes channels w + L cc of every window tile, 16x16x4 MFMA
+    //         (4 tiles interleaved: their 2-MFMA chains and SiLUs overlap)
+#pragma unroll 4
     for (int wt = 0; wt < G::LNT; ++wt) {
         const int p = wt * 16 + n;
         const int pp = p < LP0 ? p : 0;
@@ -1244,6 +1247,7 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
             sc[j] = wsh[G::OW_SC + 4 * g + j];
             shf[j] = wsh[G::OW_SH + 4 * g + j];
         }
+#pragma unroll 2
         for (int nt = wave; nt < G::QNT; nt += NW) {
             const int p = nt * 16 + n;
             const int pp = p < G::QP ? p : 0;
@@ -1284,8 +1288,12 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
             sc[j] = wsh[G::OW_S2 + 4 * g + j];
             shf[j] = wsh[G::OW_H2 + 4 * g + j];
         }
-        for (int nt = 2 * wave; nt < 4 * L; nt += 2 * NW) {
-            conv::floatx4 acc[2] = {conv::floatx4{0.f, 0.f, 0.f, 0.f}, conv::floatx4{0.f, 0.f, 0.f, 0.f}};
+        // UT output tiles per wave iteration: independent accumulator chains (4 where the tile count allows)
+        constexpr int UT = (4 * L) % (4 * NW) == 0 ? 4 : 2;
+        for (int nt = UT * wave; nt < 4 * L; nt += UT * NW) {
+            conv::floatx4 acc[UT];
+#pragma unroll
+            for (int u = 0; u < UT; ++u) acc[u] = conv::floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 const int dy = tap / 3, dx = tap % 3;
@@ -1293,7 +1301,7 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
                 for (int ks = 0; ks < 4; ++ks) {
                     const int ci = 4 * ks + g;
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
+                    for (int u = 0; u < UT; ++u) {
                         const int t2 = nt + u;
                         const int oyl = t2 >> 1, oxl = 16 * (t2 & 1) + n;
                         const float av = W2LDS ? wsh[G::OW_W2 + (tap * 16 + ci) * 16 + n] : wa[W2LDS ? 0 : tap][ks];
@@ -1303,7 +1311,7 @@ __global__ void __launch_bounds__(64 * NW, L == 4 ? NW / 2 : 2) shuffle_conv11_k
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < UT; ++u) {
                 const int t2 = nt + u;
                 const int oy = oy0 + (t2 >> 1), ox = ox0 + 16 * (t2 & 1) + n;
                 const bool ok = oy < Ho2 && ox < Wo2;

@@ -659,6 +659,9 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
 # The gwc volume and group_stem as one launch (esm_gwc_stem_f32, gwc_stem.hip) on the volumes the LDS-tiled
 # stem takes (ESMStereo-L / -M); ESM_GWC_STEM=0 keeps the two launches (A/B measurements)
 GWC_STEM_ENABLED = _ab("ESM_GWC_STEM", "1") != "0"
+# its composite weights staged in LDS per k-step (round 5; gwc_stem.hip hint bit 28) instead of loaded into
+# registers (round 6): A/B knob
+GWC_STEM_WLDS = _ab("ESM_GWC_STEM_WLDS", "0") == "1"
 
 
 def gwc_stem_supported(pc: PackedConv, L: torch.Tensor, G: int, D: int, att) -> bool:
@@ -682,7 +685,11 @@ def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, G: 
         raise ValueError("gwc_stem: L and R must be contiguous tensors of one shape")
     virt = L.as_strided((B, G, D, H, W), (0, 0, 0, 0, 1))  # the volume's geometry only, never read
     d, out, meta = _conv_desc(ctx, pc, [virt], tag=tag, hint=hint)
-    d.hint &= HINT_XCD_SLAB | (3 << 26)  # tile order and rows per wave; a standalone stem's form bits do not apply
+    # tile order and rows per wave (+ the weight form when the caller passes a hint); a standalone stem's
+    # tuned form bits do not apply
+    d.hint &= HINT_XCD_SLAB | (3 << 26) | ((1 << 28) if hint else 0)
+    if GWC_STEM_WLDS:
+        d.hint |= 1 << 28
     vol_flops = 2 * B * C * D * H * W
     meta.update(kind="gwc_stem", flops=meta["flops"] + vol_flops,
                 bytes=4 * B * 2 * C * H * W + 4 * B * pc.cout * D * H * W + 4 * pc.cin * pc.cout * 27,
@@ -1069,7 +1076,7 @@ SHUFFLE_PRE_ENABLED = _ab("ESM_SHUFFLE_PRE", "1") != "0"
 SC11_ENABLED = _ab("ESM_SC11", "1") != "0"
 # tile of that launch (esm_shuffle_tail_desc.flags bits 3-4; A/B knob): 0 = 4 low-res rows on 8 waves, two
 # workgroups per CU (round 6, the default); 1 = 8 rows on 8 waves (round 5); 2 = 4 rows on 4 waves
-SC11_TILE = int(_ab("ESM_SC11_TILE", "0"))
+SC11_TILE = int(_ab("ESM_SC11_TILE", "1"))
 
 
 def shuffle_conv_pre_supported(p: PackedShuffleTail, conv: PackedConv, pre: PackedConv) -> bool:

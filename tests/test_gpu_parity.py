@@ -293,9 +293,15 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
     x = torch.randn(B, cin, *shape)
     ref = _ref_conv([x], conv, bn, ACT_GELU)
     p = pk(conv, bn, ACT_GELU)
-    for hint in (0, 1 << 26, 2 << 26, 3 << 26, 3 << 26 | 1 << 28):  # automatic, rows 1 / 2 / 4, rows 8 (bit 28)
+    outs = {}
+    # automatic, rows 1 / 2 / 4, rows 8 (bit 28); plane pairs (<= 8 couts): bit 29 stages the weights in LDS
+    # (round 5) instead of registers (round 6) -- the same products in the same order, bitwise equal
+    for hint in (0, 1 << 26, 2 << 26, 3 << 26, 3 << 26 | 1 << 28, 1 << 29, 2 << 26 | 1 << 29):
         y = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | hint)
         assert rel(y, ref) < 1e-5, hex(hint)
+        outs[hint] = y
+    if cout <= 8 and k == 3 and s == 1:
+        assert torch.equal(outs[1 << 29], outs[0]) and torch.equal(outs[2 << 26 | 1 << 29], outs[2 << 26])
     res = torch.randn(ref.shape)
     mul = torch.rand(B, cout, ref.shape[3], ref.shape[4]) + 0.5
     want = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res)
@@ -320,7 +326,7 @@ def test_gwc_stem_fused(B, G, D, H, W):
     p = pk(conv, bn, ACT_GELU)
     V = E.build_gwc_volume(Ld, Rd, D, G)
     two = run_conv(Ctx(DEV), p, [V], hint=HINT_TILE3)
-    for hint in (0, 2 << 26, 3 << 26):
+    for hint in (0, 2 << 26, 3 << 26, 1 << 28, (2 << 26) | (1 << 28)):  # bit 28: LDS-staged weights (round 5)
         y = run_gwc_stem(Ctx(DEV), p, Ld, Rd, G, D, hint=hint)
         assert torch.equal(y, two), (hex(hint), float((y - two).abs().max()))
     if B * D * H * W <= 1 << 16:
