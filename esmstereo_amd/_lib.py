@@ -44,6 +44,7 @@ class EsmConvDesc(Structure):
         ("up", c_void_p), ("up_h", c_int32), ("up_w", c_int32), ("up_f", c_int32), ("hint", c_int32),
         ("ub", c_int64), ("uh", c_int64),
         ("post_scale", c_float), ("post_scale2", c_float), ("out2", c_void_p),
+        ("pre", c_void_p), ("prb", c_int64), ("prc", c_int64), ("prh", c_int64),
     ]
 
 
@@ -129,6 +130,8 @@ SIGNATURES = {
     "esm_plan_add_shuffle_conv": (c_int, [c_void_p, POINTER(EsmShuffleConvDesc)]),
     "esm_plan_add_conv_pair2": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
     "esm_plan_add_convt_1x1": (c_int, [c_void_p, POINTER(EsmConvDesc), POINTER(EsmConvDesc)]),
+    "esm_plan_set_branch": (c_int, [c_void_p, c_int, c_int]),
+    "esm_plan_set_join": (c_int, [c_void_p, c_int, c_int]),
     "esm_plan_add_gwc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6),
     "esm_plan_add_gwc_stem": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "esm_plan_add_concat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 5),

@@ -23,9 +23,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .engine import (ACT_GELU, ACT_NONE, CONVT1X1_PAIRED, SC11_ENABLED, Ctx, PackedConv, convt_1x1_supported,
-                     eager_emit, pack_conv, pack_shuffle_tail, pair2_auto, param_token, run_conv, run_convt_1x1,
-                     run_pair2, run_shuffle_conv, run_shuffle_tail, shuffle_conv_pre_supported, shuffle_conv_supported)
+from .engine import (ACT_GELU, ACT_NONE, CONVT1X1_PAIRED, FORK_ENABLED, SC11_ENABLED, Ctx, PackedConv,
+                     convt_1x1_supported, eager_emit, forked_packs, pack_conv, pack_shuffle_tail, pair2_auto,
+                     param_token, run_conv, run_conv_forked, run_convt_1x1, run_pair2, run_shuffle_conv,
+                     run_shuffle_tail, run_side_partial, shuffle_conv_pre_supported, shuffle_conv_supported)
 from .mixer import FMBlock
 
 __all__ = ["BasicConv", "Conv2x", "aggregation", "up_refinement", "upsample4", "upsample8", "upsample16"]
@@ -166,11 +167,27 @@ class _Hourglass(nn.Module):
                                f"{2 * x.shape[2]} but got size {ref.shape[2]} for tensor number 1 in the list.")
         pa, pb = up.packed(), agg[0].packed()
         u_shape = tuple(2 * v for v in x.shape[2:])
+        n0 = getattr(up, "_esm_name", "convT")
+        n1 = getattr(agg[0], "_esm_name", "agg.0")
         paired = pair2_auto(pb, agg[1].packed(), [ref]) if not self.is_3d else False
+        # the fork-join: up_refinement's image features (the last source) as a partial sum on the side branch
+        fork = FORK_ENABLED and not self.is_3d and len(skip) == 2 and agg[0].use_bn and int(skip[0].shape[1]) % 4 == 0
+        if fork:
+            cm = pa.cout + int(skip[0].shape[1])
+            p_side, p_main = forked_packs(agg[0], agg[0].conv, agg[0].bn, ACT_GELU if agg[0].gelu else ACT_NONE, cm,
+                                          int(skip[1].shape[1]))
+            if convt_1x1_supported(pa, p_main, skip[:1]) and all(u >= r for u, r in zip(u_shape, ref.shape[2:])):
+                part = run_side_partial(ctx, p_side, skip[1], n1, cm)
+                h = run_convt_1x1(ctx, pa, [x], p_main, skip[:1], tags=(n0, n1), pre=part)
+                ctx.meta[-1]["split"] = (0, cm)
+                return agg[1].emit(ctx, [h])
+            u = _crop_like(up.emit(ctx, [x]), ref)
+            part = run_side_partial(ctx, p_side, skip[1], n1, cm)
+            h = run_conv(ctx, p_main, [u, skip[0]], pre=part, tag=n1)
+            ctx.meta[-1].update(layer=n1, split=(0, cm))
+            return agg[1].emit(ctx, [h])
         if convt_1x1_supported(pa, pb, skip) and all(u >= r for u, r in zip(u_shape, ref.shape[2:])) and \
                 (CONVT1X1_PAIRED or not paired):
-            n0 = getattr(up, "_esm_name", "convT")
-            n1 = getattr(agg[0], "_esm_name", "agg.0")
             h = run_convt_1x1(ctx, pa, [x], pb, skip, tags=(n0, n1))
             return agg[1].emit(ctx, [h])
         u = _crop_like(up.emit(ctx, [x]), ref)
@@ -286,11 +303,15 @@ class _ESMUpsampler(nn.Module):
             # spx_<t>[1] inside the row-form head + ref conv launch where it fits (stages after the first;
             # the first one's c feeds to_feat and the FMBlocks), else the pair / two launches
             pre = None
-            if i > 0 and not pair2_auto(spx[0].packed(), p[f"spx1_{tag}"], [d, feats[cat_i]]) and \
+            paired = pair2_auto(spx[0].packed(), p[f"spx1_{tag}"], [d, feats[cat_i]])
+            if i > 0 and not paired and \
                     shuffle_conv_pre_supported(p[f"up_{tag}"], ref.conv1[0].packed(), p[f"spx1_{tag}"]) and \
                     shuffle_conv_supported(p[f"up_{tag}"], ref.conv1[0].packed(), d):
-                c = run_conv(ctx, spx[0].packed(), [d, feats[cat_i]], tag=getattr(spx[0], "_esm_name", "spx.0"))
+                c = self._spx0(ctx, spx[0], d, feats[cat_i])
                 pre = p[f"spx1_{tag}"]
+            elif not paired:
+                c = run_conv(ctx, p[f"spx1_{tag}"], [self._spx0(ctx, spx[0], d, feats[cat_i])],
+                             tag=f"{getattr(spx[0], '_esm_name', 'spx.0')[:-2]}.1")
             else:
                 c = _pair(ctx, spx[0], [d, feats[cat_i]], spx[1], p[f"spx1_{tag}"])
             x = c
@@ -328,6 +349,16 @@ class _ESMUpsampler(nn.Module):
         outs.reverse()
         copies.reverse()
         return (outs, copies) if scaled_copies is not None else outs
+
+    def _spx0(self, ctx: Ctx, spx0: BasicConv, d: torch.Tensor, feat: torch.Tensor) -> torch.Tensor:
+        """spx_<t>[0](cat(d, feat)) (ESMStereo.py:488, 501): with the fork-join, feat's part of the 3x3 sum runs on
+        the plan's side branch (it depends on the backbone features only) and the chain's conv covers d's
+        channels from it; else one conv over the concat."""
+        name = getattr(spx0, "_esm_name", "spx.0")
+        if FORK_ENABLED and spx0.use_bn and int(d.shape[1]) % 4 == 0:
+            return run_conv_forked(ctx, spx0, spx0.conv, spx0.bn, ACT_GELU if spx0.gelu else ACT_NONE, [d], feat,
+                                   tag=name)
+        return run_conv(ctx, spx0.packed(), [d, feat], tag=name)
 
     def forward(self, *args: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         *feats, init = args

@@ -24,6 +24,7 @@ int launch_widet(const esm_conv_desc& a, hipStream_t s);  // conv_widet.hip
 bool tile3_auto(const esm_conv_desc& a);                 // conv_tile3.hip
 int launch_tile3(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
 bool tile2_auto(const esm_conv_desc& a);                 // conv_tile3.hip
+bool tile2_ok(const esm_conv_desc& a);                   // conv_tile3.hip
 int launch_tile2(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
 }  // namespace conv
 
@@ -62,6 +63,8 @@ int conv_check(const esm_conv_desc& a) {
     if (a.shuffle > 1 && (d3 || a.transposed)) return arg_error("conv: pixel shuffle only for 2-D convs");
     if (a.up && (a.Cout != 1 || d3 || a.up_f <= 0)) return arg_error("conv: bilinear add needs 2-D, Cout == 1");
     if (a.Hi <= 0 || a.Wi <= 0 || a.Di <= 0) return arg_error("conv: empty input");
+    if (a.pre && (d3 || a.transposed || a.shuffle > 1 || a.up || a.prh < a.Wo || a.prc < 0 || a.prb < 0))
+        return arg_error("conv: a partial sum (pre) only for 2-D, non-transposed, unshuffled convs");
     if (a.transposed) {
         if (a.kh != 4 || a.stride != 2 || a.ph != 1 || a.pw != 1 || (d3 && a.pd != 1))
             return arg_error("conv: transposed conv supports k=4, s=2, p=1 only");
@@ -86,6 +89,13 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
     const int form = a.hint & ~(kHintXcd | kHintNoTile);  // the form / tile bits (bit 30 only orders the tiles)
     const bool tile_auto = form == 0 && !(a.hint & kHintNoTile);
+    if (a.pre) {  // the forms that start their accumulators from a partial sum (round 6)
+        if ((a.hint & kHintWide) && conv::wide_ok(a)) return conv::launch_wide(a, s);
+        if (((a.hint & kHintTile3) || (tile_auto && conv::tile2_auto(a))) && conv::tile2_ok(a)) return conv::launch_tile2(a, s);
+        if (conv::small_ok(a)) return conv::launch_small(a, s);
+        if (conv::wide_ok(a)) return conv::launch_wide(a, s);
+        return arg_error("conv: a partial sum (pre) needs the lean, register-weight or tiled 2-D form");
+    }
     if (a.transposed) {
         if (a.hint & kHintWideT) return conv::launch_widet(a, s);
         if (a.hint & kHintTile3) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);

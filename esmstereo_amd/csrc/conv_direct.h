@@ -58,6 +58,21 @@ __device__ __forceinline__ float buf_load_s(__amdgpu_buffer_rsrc_t r, unsigned v
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), soff, 0));
 }
 
+// The partial conv sum esm_conv_desc.pre (2-D, [B, Cout, Ho, Wo]) at the D-layout elements of lane (n, q) of the
+// 16-cout tile from cout c0: rows c0 + 4q + j, output row y, column x -- the accumulator's starting value (0
+// past Cout / the map, or without `pre`).
+__device__ __forceinline__ floatx4 pre_tile(const esm_conv_desc& a, int b, int c0, int q, int y, int x) {
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (!a.pre || y >= a.Ho || x >= a.Wo) return v;
+    const float* p = a.pre + b * a.prb + static_cast<long long>(y) * a.prh + x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int co = c0 + 4 * q + j;
+        if (co < a.Cout) v[j] = p[co * a.prc];
+    }
+    return v;
+}
+
 template <bool D3, int K, int S, bool TR, int MT, int NT, int KS, int CK, bool MS>
 __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_desc a) {
     constexpr int KT = TR ? 2 : K;  // taps per dim (per parity class for transposed)
@@ -343,6 +358,9 @@ __global__ void __launch_bounds__(kDirectThreads) dconv_kernel(const esm_conv_de
 
 // Whether the direct form can run this layer: every multi-source split on a 4-channel
 // boundary, and each source's per-batch span addressable by a 32-bit buffer offset.
+// whether a form without `pre` support may run this desc
+inline bool no_pre(const esm_conv_desc& a) { return a.pre == nullptr; }
+
 inline bool direct_ok(const esm_conv_desc& a) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1;
     for (int s = 0; s < a.nsrc; ++s) {

@@ -136,6 +136,12 @@ __device__ __forceinline__ void lconv_body(const esm_conv_desc& a, unsigned m_ds
     for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[c][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (!TR && !D3) {  // the partial sum `pre` (2-D) starts wave 0's accumulator
+        if (wave == 0) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[0][mt] = pre_tile(a, b, cob + 16 * mt, kq, ys, x0 + n16);
+        }
+    }
 
     const int G = (a.Cin + 3) >> 2;
     const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
@@ -202,7 +208,8 @@ __device__ __forceinline__ void lconv_body(const esm_conv_desc& a, unsigned m_ds
         float y[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = gelu_erf(reduced(r * 64 + lane) * s1[r] + h1[r]);
-        const floatx4 o = up1_finish(u1, y, bx1);
+        const floatx4 o = up1_finish(u1, y, bx1, D3 ? floatx4{0.f, 0.f, 0.f, 0.f}
+                                                    : pre_tile(bb, b, 0, kq, 2 * ys + qh, 2 * (x0 + n16) + qw));
         const int ox = 2 * (x0 + n16) + qw, oy = 2 * ys + qh, oz = D3 ? 2 * zs + qd : 0;
         const bool pok = ox < bb.Wo && oy < bb.Ho && oz < bb.Do;
         const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(

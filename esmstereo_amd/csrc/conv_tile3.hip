@@ -231,7 +231,9 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int mt = 0; mt < NCO; ++mt) acc[nt][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < NCO; ++mt)  // 2-D: the partial sum `pre` (or 0) starts the accumulator
+            acc[nt][mt] = (D2 && !PZ) ? pre_tile(a, b, mg * MT * 16 + mt * 16, g, yo0 + yw * NT + nt, xo0 + n)
+                                      : floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int nchunk = (a.Cin + 3) >> 2;
     stage_load(0);
@@ -331,6 +333,211 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
                 }
             }
     }
+}
+
+// Cout = 16 MF + 8 (24, 40: the L hourglass's conv1.1 / agg_1.1 / conv2.1 / agg_0.1, 3x3x3 stride 1), round 6.
+// The MT form pads such a layer to 16 (MF + 1) MFMA rows, a quarter (24) or a sixth (40) of the matrix work on
+// zero weights.  Here a wave owns a PLANE PAIR: the first 16 MF couts run as full tiles for each of the two
+// planes, and the last 8 couts of both planes share one 16-row tile through the plane-pair composite weights
+// A_p[(h, co)][ci] = W[p - h][ci][co] over the four input planes p (conv_tile3 PZ; 6 of its 8 half-blocks
+// carry weights): 90 instead of 108 MFMAs per plane pair, row and k-step at 24 couts, 144 instead of 162 at 40.
+// Each input plane's rows are read from LDS once for both.  The composite A operands sit in registers (36 per
+// lane, reloaded for the next k-step after their last use, as WREG), the full tiles' weights are staged in LDS.
+// Per output the products and their order (dz, dx, dy within a k-step, k-steps in channel order) are the MT
+// form's, so the result is bit-identical to it.  Plain BasicConv epilogue only (BN + GELU).
+template <int MF, int NT>
+struct HzGeo {
+    static constexpr int ZB = 8, IZ = ZB + 2, IY = NT + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
+    static constexpr int CS = CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;  // channel stride = 16 mod 32 banks
+    static constexpr int XE = 4 * CS0, XL = 4 * CS, XR = (XE + kT3Threads - 1) / kT3Threads;
+    static constexpr int WCS = MF % 2 ? 16 * MF : 16 * MF + 16;      // weight row stride = 16 mod 32
+    static constexpr int WE = 27 * 4 * 16 * MF, WL = 27 * 4 * WCS, WR = (WE + kT3Threads - 1) / kT3Threads;
+    static constexpr int NR = NT + 2;
+};
+
+template <int MF, int NT>
+__global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_desc a) {
+    using G = HzGeo<MF, NT>;
+    constexpr int IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS, XR = G::XR, WR = G::WR, NR = G::NR;
+    __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
+    __shared__ __attribute__((aligned(16))) float ws[2][G::WL];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+    const int zw = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
+    const int xo0 = bk_.x * 16, yo0 = bk_.y * NT;
+    const int nzb = (a.Do + G::ZB - 1) / G::ZB;
+    const int b = bk_.z / nzb;
+    const int zo0 = (bk_.z - b * nzb) * G::ZB;
+    const int zi0 = zo0 - 1, yi0 = yo0 - 1, xi0 = xo0 - 1;
+
+    const esm_src& s0 = a.src[0];
+    const int sc = static_cast<int>(s0.sc), sd = static_cast<int>(s0.sd), sh = static_cast<int>(s0.sh);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s0.ptr + b * s0.sb), static_cast<short>(0),
+        4 * ((s0.C - 1) * sc + (a.Di - 1) * sd + (a.Hi - 1) * sh + a.Wi), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), static_cast<short>(0), 4 * 27 * a.cin_pad * a.cout_pad, 0x00020000);
+
+    unsigned xoff[XR];
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+        const int e = tid + k * kT3Threads;
+        const int ix = e % IX, iy = (e / IX) % G::IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
+        const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
+        const bool ok = e < G::XE && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+        xoff[k] = ok ? 4u * static_cast<unsigned>(ci * sc + zi * sd + yi * sh + xi) : kOOB;
+    }
+    unsigned woff[WR];
+    int wdst[WR];
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {  // the full tiles' weights: e = (tap * 4 + ci) * 16 MF + m
+        const int e = tid + k * kT3Threads;
+        const int m = e % (16 * MF), ci = (e / (16 * MF)) & 3, tap = e / (64 * MF);
+        woff[k] = e < G::WE ? 4u * static_cast<unsigned>((tap * a.cin_pad + ci) * a.cout_pad + m) : kOOB;
+        wdst[k] = e < G::WE ? (tap * 4 + ci) * WCS + m : -1;
+    }
+    // the last 8 couts' composite A operand of (input plane p, tap t9): lane (g, n) holds W[p - n / 8][t9][c0 + g][16 MF + n % 8]
+    unsigned wpo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int dz = p - (n >> 3), co = 16 * MF + (n & 7);
+        wpo[p] = (dz >= 0 && dz <= 2 && co < a.Cout) ? 4u * static_cast<unsigned>((dz * 9 * a.cin_pad + g) * a.cout_pad + co)
+                                                     : kOOB;
+    }
+    float wa[36];
+    auto wreg_load = [&](int i, int c0) __attribute__((always_inline)) {
+        wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + c0) * a.cout_pad);
+    };
+    float xv[XR], wv[WR];
+    auto stage_load = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int ci = (tid + k * kT3Threads) / G::CS0;
+            xv[k] = buf_load_s(rs, c0 + ci < a.Cin ? xoff[k] : kOOB, 4 * c0 * sc);
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k) wv[k] = buf_load_s(wrs, woff[k], 4 * c0 * a.cout_pad);
+    };
+    auto stage_store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < XR; ++k) {
+            const int e = tid + k * kT3Threads;
+            if (e < G::XE) xs[buf][e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < WR; ++k)
+            if (wdst[k] >= 0) ws[buf][wdst[k]] = wv[k];
+    };
+    floatx4 accf[2][NT][MF], acch[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        acch[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int pz = 0; pz < 2; ++pz)
+#pragma unroll
+            for (int mf = 0; mf < MF; ++mf) accf[pz][nt][mf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    const int nchunk = (a.Cin + 3) >> 2;
+    stage_load(0);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) wreg_load(i, 0);
+    stage_store(0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
+        const float* xw = &xs[buf][g * CS + n];
+        const float* wp = &ws[buf][g * WCS + n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                float br[NR];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) br[r] = xw[(2 * zw + q) * PLANE + r * IX + dx];
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+#pragma unroll
+                    for (int pz = 0; pz < 2; ++pz) {  // full tiles of output plane pz: dz = q - pz
+                        const int dz = q - pz;
+                        if (dz < 0 || dz > 2) continue;
+                        float av[MF];
+#pragma unroll
+                        for (int mf = 0; mf < MF; ++mf) av[mf] = wp[((dz * 3 + dy) * 3 + dx) * 4 * WCS + mf * 16];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                            for (int mf = 0; mf < MF; ++mf)
+                                accf[pz][nt][mf] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(av[mf], br[nt + dy], accf[pz][nt][mf], 0, 0, 0);
+                    }
+                    const int i = q * 9 + dy * 3 + dx;
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acch[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[i], br[nt + dy], acch[nt], 0, 0, 0);
+                    wreg_load(i, 4 * (ch + 1));  // (past the last k-step: weights no MFMA uses, range-checked)
+                }
+            }
+        if (ch + 1 < nchunk) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue (BN + GELU, buffer stores): lane (g, n) holds rows 4g + j of each tile, column n; the BN
+    //      constants are loaded here (one round trip at the end) rather than held through the K loop
+    float scl[MF + 1][4], shf[MF + 1][4];
+#pragma unroll
+    for (int mf = 0; mf <= MF; ++mf)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = mf < MF ? mf * 16 + 4 * g + j : 16 * MF + ((4 * g + j) & 7);
+            scl[mf][j] = a.scale[co];
+            shf[mf][j] = a.shift[co];
+        }
+    const int x = xo0 + n;
+    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + b * a.ob, static_cast<short>(0),
+        4 * ((a.Cout - 1) * static_cast<int>(a.oc) + (a.Do - 1) * static_cast<int>(a.od) +
+             (a.Ho - 1) * static_cast<int>(a.oh) + a.Wo),
+        0x00020000);
+    auto store = [&](float v, int co, int z, int y) __attribute__((always_inline)) {
+        const bool ok = co < a.Cout && z < a.Do && y < a.Ho && x < a.Wo;
+        const unsigned o = ok ? 4u * static_cast<unsigned>(co * static_cast<int>(a.oc) + z * static_cast<int>(a.od) +
+                                                           y * static_cast<int>(a.oh) + x)
+                              : kOOB;
+        store_b32(__float_as_uint(v), ro_, static_cast<int>(o), 0);
+    };
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int y = yo0 + nt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int pz = 0; pz < 2; ++pz)
+#pragma unroll
+                for (int mf = 0; mf < MF; ++mf) {
+                    float v = accf[pz][nt][mf][j];  // (the MT form's epilogue expression: the same rounding)
+                    v = a.scale ? v * scl[mf][j] + shf[mf][j] : v + shf[mf][j];
+                    store(act_t<ESM_ACT_GELU>(v, a.act), mf * 16 + 4 * g + j, zo0 + 2 * zw + pz, y);
+                }
+            const int m = 4 * g + j;
+            float v = acch[nt][j];
+            v = a.scale ? v * scl[MF][j] + shf[MF][j] : v + shf[MF][j];
+            store(act_t<ESM_ACT_GELU>(v, a.act), 16 * MF + (m & 7), zo0 + 2 * zw + (m >> 3), y);
+        }
+    }
+}
+
+template <int MF, int NT>
+int launch_hz(const esm_conv_desc& a, hipStream_t s) {
+    const long long z = static_cast<long long>(a.B) * ((a.Do + 7) / 8);
+    const long long gy = ceil_div(a.Ho, NT);
+    if (z > 65535 || gy > 65535) return arg_error("conv(tile3 hz): grid too large");
+    const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
+    hipLaunchKernelGGL((tconv3hz_kernel<MF, NT>), grid, dim3(kT3Threads), 0, s, a);
+    return check_launch("conv(tile3 hz)");
 }
 
 // ConvTranspose3d k4 s2 p1 (the hourglass decoder steps conv3_up 72 -> 40 and conv2_up 40 -> 24,
@@ -525,7 +732,7 @@ __device__ __forceinline__ void tconvt3_body(const esm_conv_desc& a, int ncg, co
                 float yv[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) yv[j] = gelu_erf(acc[qw][nt][0][j] * scl[0][j] + shf[0][j]);
-                o[qw] = up1_finish(u1, yv, bx1[qw][nt]);
+                o[qw] = up1_finish(u1, yv, bx1[qw][nt], D2 ? pre_tile(bb, b, 0, g, y, x + qw) : floatx4{0.f, 0.f, 0.f, 0.f});
             }
             if constexpr (PAIR) {  // 8-byte pair stores (b's output rows 8-byte aligned, even width: launcher)
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -829,6 +1036,16 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
         if (rsel == 2 || (rsel == 0 && vox < (1LL << 20)))
             return lw ? launch_t3<1, 3, 1, 2, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 2, 4, true, 1, false, true>(a, s, 1);
         return lw ? launch_t3<1, 3, 1, 4, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 4, 4, true, 1, false, true>(a, s, 1);
+    }
+    // 24 / 40 couts, plain BasicConv: the plane-pair hybrid (hint bit 29: the padded MT form, A/B); rows per wave
+    // 2 / 4 for rsel 1 / 2-3, automatic 4 (2 on small volumes)
+    const bool plain = a.act == ESM_ACT_GELU && a.scale && a.shift && !a.res && !a.out2 && !a.mul && a.post_scale == 1.f &&
+                       a.nsrc == 1 && static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
+                                              static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
+    if (plain && !((a.hint >> 29) & 1) && (a.Cout == 24 || a.Cout == 40)) {
+        const int nt = rsel == 1 ? 2 : rsel >= 2 ? 4 : (vox < (1LL << 19) ? 2 : 4);
+        if (a.Cout == 24) return nt == 2 ? launch_hz<1, 2>(a, s) : launch_hz<1, 4>(a, s);  // (8 rows spill)
+        return launch_hz<2, 2>(a, s);  // 40 couts: 2 rows per wave (4 and 8 exceed the register file)
     }
     if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
     if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);

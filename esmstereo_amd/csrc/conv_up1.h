@@ -128,8 +128,8 @@ inline bool up1_pairs_ok(const esm_conv_desc& b) {
 // channel 4q + r (after its BN + GELU), bx the extra channels.  The XB k-steps run unconditionally: those past the
 // layer's extra channels meet zero weights and zero inputs (kOOB loads), so no branch splits the MFMA chain.
 template <int XB>
-__device__ __forceinline__ floatx4 up1_finish(const Up1Ops<XB>& u, const float (&y)[4], const float (&bx)[XB]) {
-    floatx4 d{0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ floatx4 up1_finish(const Up1Ops<XB>& u, const float (&y)[4], const float (&bx)[XB],
+                                              floatx4 d /* the 1x1's partial sum `pre`, or 0 */) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) d = __builtin_amdgcn_mfma_f32_16x16x4f32(u.wy[r], y[r], d, 0, 0, 0);
 #pragma unroll
@@ -153,6 +153,7 @@ inline int up1_check(const esm_conv_desc& a, const esm_conv_desc& b, int xb_max)
     if (b.act != ESM_ACT_GELU || !b.out || !b.scale || !b.shift || b.mul || b.res || b.up || b.out2 ||
         b.post_scale != 1.f || b.shuffle > 1)
         return arg_error("convt_1x1: b must be a BasicConv (BN + GELU, plain epilogue)");
+    if (b.pre && d3) return arg_error("convt_1x1: a partial sum (pre) for the 2-D form only");
     if (b.nsrc < 2 || b.src[0].C != a.Cout || b.Cout < 1 || b.Cout > 16 || b.B != a.B)
         return arg_error("convt_1x1: b.src[0] must be a's output, b.Cout <= 16");
     if (b.Hi > a.Ho || b.Wi > a.Wo || b.Di > a.Do || b.Ho != b.Hi || b.Wo != b.Wi || b.Do != b.Di ||

@@ -130,7 +130,8 @@ __global__ void __launch_bounds__(kWideThreads) wconv_kernel(const esm_conv_desc
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[r][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt)  // the partial sum `pre` (one wave of a K split) or 0
+            acc[r][mt] = kh == 0 ? pre_tile(a, b, cob + 16 * mt, kq, y0 + r, xo) : floatx4{0.f, 0.f, 0.f, 0.f};
 
     // output through a buffer descriptor over this batch item: per-lane voffset (cout, column) fixed
     // for the whole wave, the row in soffset; a cout past Cout / column past Wo / row past Ho carries

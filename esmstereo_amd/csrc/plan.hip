@@ -69,6 +69,8 @@ struct Op {
     RegArgs reg{};
     esm_conf_desc cf{};
     int repeat = 1;  // launches per replay (esm_plan_set_repeat: 0 drops the op, 2 doubles it)
+    int branch = 0;  // 0: the main chain; 1: the side branch (esm_plan_set_branch)
+    int join = 0;    // main op: wait for the side ops listed before it (esm_plan_set_join)
 };
 
 int run_op(const Op& op, hipStream_t s) {
@@ -176,7 +178,7 @@ struct Rebase {
         int n = 0;
         for (int i = 0; i < d.nsrc && i < ESM_MAX_SRC; ++i) n += (*this)(d.src[i].ptr);
         n += (*this)(d.w) + (*this)(d.scale) + (*this)(d.shift) + (*this)(d.mul) + (*this)(d.res);
-        return n + (*this)(d.out) + (*this)(d.up) + (*this)(d.out2);
+        return n + (*this)(d.out) + (*this)(d.up) + (*this)(d.out2) + (*this)(d.pre);
     }
     int stage(esm_smix_stage& t) const {
         return (*this)(t.ln_w) + (*this)(t.fc0_w) + (*this)(t.fc0_b) + (*this)(t.fc2_w) + (*this)(t.fc2_b);
@@ -193,6 +195,9 @@ struct esm_plan {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     hipStream_t cap_stream = nullptr;
+    // the side branch: its stream and the fork / join events (created on first use)
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // probe
     int probe_index = -1;
     int ring = 0;
@@ -226,7 +231,40 @@ struct esm_plan {
         clear_graph();
         clear_probe();
         if (last_launch) hipEventDestroy(last_launch);
+        if (ev_fork) hipEventDestroy(ev_fork);
+        if (ev_join) hipEventDestroy(ev_join);
+        if (side_stream) hipStreamDestroy(side_stream);
         if (cap_stream) hipStreamDestroy(cap_stream);
+    }
+    bool has_side() const {
+        for (const Op& op : ops)
+            if (op.branch && op.repeat) return true;
+        return false;
+    }
+    int side_setup() {
+        if ((!side_stream && hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking) != hipSuccess) ||
+            (!ev_fork && hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess) ||
+            (!ev_join && hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess)) {
+            esm::set_error("plan: cannot create the side-branch stream / events");
+            return ESM_ERR_RUNTIME;
+        }
+        return ESM_OK;
+    }
+    // fork: the side stream continues from s's current point; join: s continues after the side stream's
+    // last launch.  Under stream capture these are dependency edges, not nodes.
+    int fork(hipStream_t s) {
+        if (hipEventRecord(ev_fork, s) != hipSuccess || hipStreamWaitEvent(side_stream, ev_fork, 0) != hipSuccess) {
+            esm::set_error("plan: side-branch fork failed");
+            return ESM_ERR_RUNTIME;
+        }
+        return ESM_OK;
+    }
+    int joined(hipStream_t s) {
+        if (hipEventRecord(ev_join, side_stream) != hipSuccess || hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) {
+            esm::set_error("plan: side-branch join failed");
+            return ESM_ERR_RUNTIME;
+        }
+        return ESM_OK;
     }
     int patch(int i, const Rebase& rb) {
         Op& op = ops[i];
@@ -303,7 +341,27 @@ struct esm_plan {
     // Under stream capture the records become event-record graph nodes (hipEventRecordExternal).
     int launch_all(hipStream_t s, int slot, bool capture = false) {
         const unsigned flags = capture ? hipEventRecordExternal : 0u;
+        const bool side = has_side();
+        bool pending = false;  // side launches not yet joined
+        if (side) {
+            int rc = side_setup();
+            if (rc == ESM_OK) rc = fork(s);
+            if (rc != ESM_OK) return rc;
+        }
         for (int i = 0; i < static_cast<int>(ops.size()); ++i) {
+            if (ops[i].branch) {
+                for (int r = 0; r < ops[i].repeat; ++r) {
+                    const int rc = run_op(ops[i], side_stream);
+                    if (rc != ESM_OK) return rc;
+                }
+                pending = pending || ops[i].repeat > 0;
+                continue;
+            }
+            if (ops[i].join && pending) {
+                const int rc = joined(s);
+                if (rc != ESM_OK) return rc;
+                pending = false;
+            }
             if (i == probe_index && slot >= 0) {
                 const hipError_t e = hipEventRecordWithFlags(ev0[slot], s, flags);
                 if (e != hipSuccess) {
@@ -323,7 +381,7 @@ struct esm_plan {
                 }
             }
         }
-        return ESM_OK;
+        return side ? joined(s) : ESM_OK;  // (the side stream always rejoins: the run ends on s)
     }
 };
 
@@ -492,6 +550,26 @@ int esm_plan_set_conv_hint(esm_plan* plan, int index, int hint) {
     return prev & ~esm::kHintXcd;
 }
 
+int esm_plan_set_branch(esm_plan* plan, int index, int branch) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (index < 0 || index >= static_cast<int>(plan->ops.size())) return esm::arg_error("plan: op index out of range");
+    if (branch != 0 && branch != 1) return esm::arg_error("plan: branch must be 0 (main) or 1 (side)");
+    if (branch && index == plan->probe_index) return esm::arg_error("plan: the probed op must be on the main chain");
+    plan->clear_graph();
+    const int prev = plan->ops[index].branch;
+    plan->ops[index].branch = branch;
+    return prev;
+}
+
+int esm_plan_set_join(esm_plan* plan, int index, int join) {
+    if (!plan) return esm::arg_error("plan: null");
+    if (index < 0 || index >= static_cast<int>(plan->ops.size())) return esm::arg_error("plan: op index out of range");
+    plan->clear_graph();
+    const int prev = plan->ops[index].join;
+    plan->ops[index].join = join ? 1 : 0;
+    return prev;
+}
+
 int esm_plan_set_repeat(esm_plan* plan, int index, int repeat) {
     if (!plan) return esm::arg_error("plan: null");
     if (index < 0 || index >= static_cast<int>(plan->ops.size())) return esm::arg_error("plan: op index out of range");
@@ -534,15 +612,39 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
     }
     // Capture the launch list; around the probed op remember the capture frontier so the
     // event-record nodes can be spliced in after capture (records inside capture are refused).
+    // Side-branch ops are captured on the side stream, forked from the capture's start and joined where a
+    // main op asks (and at the end); each op's kernel nodes are found from its own stream's frontiers.
     std::vector<hipGraphNode_t> before, after;
-    std::vector<std::vector<hipGraphNode_t>> frontiers;  // capture frontier after each op
-    int rc = ESM_OK;
+    std::vector<std::vector<hipGraphNode_t>> frontiers;  // capture frontier (of the op's stream) after each op
+    std::vector<std::vector<hipGraphNode_t>> prev_of;    // ... and before it
+    const bool side = plan->has_side();
+    int rc = side ? plan->side_setup() : ESM_OK;
+    if (rc == ESM_OK && side) rc = plan->fork(plan->cap_stream);
+    std::vector<hipGraphNode_t> last_main, last_side = capture_frontier(plan->cap_stream);
+    last_main = last_side;
+    bool pending = false;
     for (int i = 0; i < static_cast<int>(plan->ops.size()) && rc == ESM_OK; ++i) {
+        const Op& op = plan->ops[i];
+        if (op.branch) {
+            prev_of.push_back(last_side);
+            for (int r = 0; r < op.repeat && rc == ESM_OK; ++r) rc = run_op(op, plan->side_stream);
+            last_side = capture_frontier(plan->side_stream);
+            frontiers.push_back(last_side);
+            pending = pending || op.repeat > 0;
+            continue;
+        }
+        if (op.join && pending && rc == ESM_OK) {
+            rc = plan->joined(plan->cap_stream);
+            pending = false;
+        }
+        prev_of.push_back(last_main);
         if (i == plan->probe_index) before = capture_frontier(plan->cap_stream);
-        for (int r = 0; r < plan->ops[i].repeat && rc == ESM_OK; ++r) rc = run_op(plan->ops[i], plan->cap_stream);
-        frontiers.push_back(capture_frontier(plan->cap_stream));
+        for (int r = 0; r < op.repeat && rc == ESM_OK; ++r) rc = run_op(op, plan->cap_stream);
+        last_main = capture_frontier(plan->cap_stream);
+        frontiers.push_back(last_main);
         if (i == plan->probe_index) after = frontiers.back();
     }
+    if (rc == ESM_OK && side) rc = plan->joined(plan->cap_stream);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(plan->cap_stream, &g);
     if (rc != ESM_OK) {
@@ -555,8 +657,7 @@ int esm_plan_graph_build(esm_plan* plan, void* stream) {
     }
     plan->graph = g;
     plan->op_nodes.resize(frontiers.size());
-    for (size_t i = 0; i < frontiers.size(); ++i)
-        plan->op_nodes[i] = chain_between(i ? frontiers[i - 1] : std::vector<hipGraphNode_t>{}, frontiers[i]);
+    for (size_t i = 0; i < frontiers.size(); ++i) plan->op_nodes[i] = chain_between(prev_of[i], frontiers[i]);
     if (plan->probe_index >= 0) {
         if (after.empty()) {
             plan->clear_graph();

@@ -12,6 +12,7 @@ compiled whole-hot-path plan run the very same kernels with the very same fusion
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import json
 import math
@@ -28,7 +29,8 @@ from ._lib import (ACT_GELU, ACT_NONE, ACT_RELU, ACT_RELU6, ACT_SIGMOID, ACT_SIL
 
 __all__ = ["Ctx", "PackedConv", "pack_conv", "run_conv", "run_smix", "run_fmnet", "run_shuffle_tail", "pack_shuffle_tail",
            "ACT_NONE", "ACT_GELU", "ACT_SILU", "ACT_RELU", "ACT_SIGMOID", "ACT_RELU6", "run_dwconv", "cached_pack", "run_convt_1x1",
-           "convt_1x1_supported"]
+           "convt_1x1_supported", "pack_conv_split", "run_conv_forked",
+           "forked_packs", "run_side_partial"]
 
 
 def _rup(x: int, m: int) -> int:
@@ -163,6 +165,21 @@ def pack_conv(conv: torch.nn.Module, bn: Optional[torch.nn.Module] = None, act: 
                       cin_pad, cout_pad)
 
 
+def pack_conv_split(conv: torch.nn.Module, bn: Optional[torch.nn.Module], act: int, lo: int, hi: int) -> PackedConv:
+    """The input channels [lo, hi) of a 2-D Conv2d as their own conv (a partial sum of the layer): with ``bn``
+    the folded BN + ``act`` epilogue (the part that finishes the layer), else a plain sum (no bias, no act)."""
+    W = conv.weight
+    if isinstance(conv, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d)) or W.dim() != 4 or conv.bias is not None:
+        raise ValueError("pack_conv_split: a bias-free Conv2d")
+    P, cin_pad, cout_pad = pack_weight(W[:, lo:hi], False)
+    scale = shift = None
+    if bn is not None:
+        scale, shift = bn_affine(bn)
+    k, s_, p_ = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+    return PackedConv(P, scale, shift, act if bn is not None else ACT_NONE, 2, k, s_, p_, False, hi - lo,
+                      int(W.shape[0]), cin_pad, cout_pad)
+
+
 def cached_pack(owner: torch.nn.Module, name: str, mods: Sequence[Optional[torch.nn.Module]], build, *extra):
     """``build()`` (packed weights of ``mods``) cached on ``owner`` under ``name`` until a tensor of ``mods`` is
     replaced, moved or edited in place (param_token)."""
@@ -219,6 +236,8 @@ class Ctx:
         self.arena_bytes = 0   # bytes carved out of the arena (256-B granules)
         self.arena_chunks = 0
         self.num_ops = 0       # ops submitted (or, dry, recorded)
+        self._branch = 0       # 1 inside side(): ops go to the plan's side branch
+        self._join_next = False
 
     def __enter__(self) -> "Ctx":
         if self.dry:
@@ -230,11 +249,37 @@ class Ctx:
             _DRY.depth = _dry_depth() - 1
 
     def _submit(self) -> bool:
-        """Count one op; True when it is to be handed to the library (not a dry emission)."""
+        """Count one op; True when it is to be handed to the library (not a dry emission).  The op's meta entry
+        (the last one appended) records its branch."""
         self.num_ops += 1
         if self.dry and not _dry_depth():
             raise RuntimeError("a dry Ctx must be used as a context manager")
+        if self.meta:
+            self.meta[-1]["branch"] = self._branch
         return not self.dry
+
+    @contextlib.contextmanager
+    def side(self):
+        """Ops emitted inside run on the plan's side branch (esm_plan_set_branch): they overlap the main chain
+        and may read only the plan's inputs (eagerly they run in place, on the current stream)."""
+        prev, self._branch = self._branch, 1
+        try:
+            yield self
+        finally:
+            self._branch = prev
+
+    def join_next(self) -> None:
+        """The next main-chain op waits for every side op emitted before it (esm_plan_set_join)."""
+        self._join_next = True
+
+    def _placed(self, idx: int) -> int:
+        """Branch / join attributes of the op just added to the native plan at ``idx``."""
+        if self._branch:
+            check(lib.esm_plan_set_branch(self.plan, idx, 1), "plan_set_branch")
+        elif self._join_next:
+            check(lib.esm_plan_set_join(self.plan, idx, 1), "plan_set_join")
+            self._join_next = False
+        return idx
 
     def launch(self, graph: bool = True, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Run a plan context's launch list (as a hipGraph by default) on the current stream."""
@@ -313,7 +358,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_conv(self.plan, ctypes.byref(d)), "plan_add_conv")
+            self._placed(check(lib.esm_plan_add_conv(self.plan, ctypes.byref(d)), "plan_add_conv"))
         else:
             check(lib.esm_conv_f32(ctypes.byref(d), self.stream), "conv")
 
@@ -321,7 +366,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_smix(self.plan, ctypes.byref(d)), "plan_add_smix")
+            self._placed(check(lib.esm_plan_add_smix(self.plan, ctypes.byref(d)), "plan_add_smix"))
         else:
             check(lib.esm_smix_f32(ctypes.byref(d), self.stream), "smix")
 
@@ -329,7 +374,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_fmnet(self.plan, ctypes.byref(d)), "plan_add_fmnet")
+            self._placed(check(lib.esm_plan_add_fmnet(self.plan, ctypes.byref(d)), "plan_add_fmnet"))
         else:
             check(lib.esm_fmnet_f32(ctypes.byref(d), self.stream), "fmnet")
 
@@ -337,7 +382,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail")
+            self._placed(check(lib.esm_plan_add_shuffle_tail(self.plan, ctypes.byref(d)), "plan_add_shuffle_tail"))
         else:
             check(lib.esm_shuffle_tail_f32(ctypes.byref(d), self.stream), "shuffle_tail")
 
@@ -345,7 +390,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_conv_pair2(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair2")
+            self._placed(check(lib.esm_plan_add_conv_pair2(self.plan, ctypes.byref(a), ctypes.byref(b)), "plan_add_conv_pair2"))
         else:
             check(lib.esm_conv_pair2_f32(ctypes.byref(a), ctypes.byref(b), self.stream), "conv_pair2")
 
@@ -353,7 +398,7 @@ class Ctx:
         if not self._submit():
             return
         if self.plan:
-            check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv")
+            self._placed(check(lib.esm_plan_add_shuffle_conv(self.plan, ctypes.byref(d)), "plan_add_shuffle_conv"))
         else:
             check(lib.esm_shuffle_conv_f32(ctypes.byref(d), self.stream), "shuffle_conv")
 
@@ -373,7 +418,7 @@ class Ctx:
             return
         if self.plan:
             self.hold(L, R, att, V)
-            check(lib.esm_plan_add_gwc(self.plan, L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G), "gwc")
+            self._placed(check(lib.esm_plan_add_gwc(self.plan, L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G), "gwc"))
         else:
             check(lib.esm_gwc_volume_f32(L.data_ptr(), R.data_ptr(), a, V.data_ptr(), B, C, H, W, D, G, self.stream),
                   "gwc")
@@ -383,7 +428,7 @@ class Ctx:
             return
         if self.plan:
             self.hold(L, R)
-            check(lib.esm_plan_add_gwc_stem(self.plan, ctypes.byref(d), L.data_ptr(), R.data_ptr(), C, G), "gwc_stem")
+            self._placed(check(lib.esm_plan_add_gwc_stem(self.plan, ctypes.byref(d), L.data_ptr(), R.data_ptr(), C, G), "gwc_stem"))
         else:
             check(lib.esm_gwc_stem_f32(ctypes.byref(d), L.data_ptr(), R.data_ptr(), C, G, self.stream), "gwc_stem")
 
@@ -394,7 +439,7 @@ class Ctx:
             return
         if self.plan:
             self.hold(L, R, V)
-            check(lib.esm_plan_add_concat(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D), "concat")
+            self._placed(check(lib.esm_plan_add_concat(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D), "concat"))
         else:
             check(lib.esm_concat_volume_f32(L.data_ptr(), R.data_ptr(), V.data_ptr(), B, C, H, W, D, self.stream),
                   "concat")
@@ -406,8 +451,8 @@ class Ctx:
             return
         if self.plan:
             self.hold(L, R, V, work)
-            check(lib.esm_plan_add_normcorr(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C,
-                                            H, W, D), "normcorr")
+            self._placed(check(lib.esm_plan_add_normcorr(self.plan, L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C,
+                                            H, W, D), "normcorr"))
         else:
             check(lib.esm_normcorr_volume_f32(L.data_ptr(), R.data_ptr(), V.data_ptr(), work.data_ptr(), B, C, H, W, D,
                                               self.stream), "normcorr")
@@ -429,7 +474,7 @@ class Ctx:
             return
         if self.plan:
             self.hold(*xs, out)
-            check(lib.esm_plan_add_conf(self.plan, ctypes.byref(d)), name)
+            self._placed(check(lib.esm_plan_add_conf(self.plan, ctypes.byref(d)), name))
         else:
             check(lib.esm_conf_f32(ctypes.byref(d), self.stream), name)
 
@@ -444,8 +489,8 @@ class Ctx:
             if samples is not None or (kind and k != 2):
                 raise ValueError("plan regression: disparity_regression or regression_topk(k=2) over arange(D)")
             self.hold(cost, out)
-            check(lib.esm_plan_add_regression(self.plan, kind, cost.data_ptr(), out.data_ptr(), B, D, H, W),
-                  "regression")
+            self._placed(check(lib.esm_plan_add_regression(self.plan, kind, cost.data_ptr(), out.data_ptr(), B, D, H, W),
+                  "regression"))
         elif kind == 0:
             check(lib.esm_disp_regression_f32(cost.data_ptr(), out.data_ptr(), B, D, H, W, self.stream), "regression")
         else:
@@ -520,12 +565,13 @@ def run_conv(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Option
              mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
              up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
              out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
-             hint: int = 0) -> torch.Tensor:
+             hint: int = 0, pre: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One implicit-GEMM conv launch; ``srcs`` are concatenated along channels (each may be a
     cropped view), the epilogue applies BN/bias, activation, ``*mul``, ``+res``,
-    ``+bilinear(up)``, ``*post_scale`` and an optional PixelShuffle(``shuffle``)."""
+    ``+bilinear(up)``, ``*post_scale`` and an optional PixelShuffle(``shuffle``).  ``pre`` (2-D,
+    [B, Cout, Ho, Wo]): a partial conv sum over other input channels, added before BN."""
     d, out, meta = _conv_desc(ctx, pc, srcs, out, mul=mul, res=res, up=up, up_f=up_f, post_scale=post_scale,
-                              shuffle=shuffle, out2=out2, post_scale2=post_scale2, tag=tag, hint=hint)
+                              shuffle=shuffle, out2=out2, post_scale2=post_scale2, tag=tag, hint=hint, pre=pre)
     ctx.meta.append(meta)
     ctx.conv(d)
     return out
@@ -535,7 +581,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
                mul: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
                up: Optional[torch.Tensor] = None, up_f: int = 0, post_scale: float = 1.0, shuffle: int = 1,
                out2: Optional[torch.Tensor] = None, post_scale2: float = 1.0, tag: str = "conv",
-               hint: int = 0, alloc_out: bool = True):
+               hint: int = 0, alloc_out: bool = True, pre: Optional[torch.Tensor] = None):
     """Validate one conv and build its ``esm_conv_desc``; returns (desc, output tensor, meta).
     ``alloc_out=False`` (the first conv of a fused pair) leaves the output pointer NULL."""
     nd = pc.nd
@@ -564,7 +610,7 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         cin += int(s.shape[1])
     if cin != pc.cin:
         raise RuntimeError(f"conv: input has {cin} channels, layer expects {pc.cin}")
-    require_on(dev, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2)
+    require_on(dev, "conv", *srcs, pc.w, pc.scale, pc.shift, out, mul, res, up, out2, pre)
     d.nsrc = max(1, len(srcs))
     d.B, d.Cin = B, cin
     d.Di, d.Hi, d.Wi = Di, Hi, Wi
@@ -633,13 +679,19 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
             raise ValueError("conv: out2 must have the output's shape and strides")
         d.out2 = out2.data_ptr()
         d.post_scale2 = float(post_scale2)
-    key = conv_key(d, nd)
+    if pre is not None:
+        require_device(pre, "conv pre")
+        if nd != 2 or pc.transposed or shuffle > 1 or up is not None or tuple(pre.shape) != (B, pc.cout, Ho, Wo):
+            raise ValueError("conv: a partial sum (pre) is [B, Cout, Ho, Wo] of a 2-D, non-transposed conv")
+        d.pre = pre.data_ptr()
+        d.prb, d.prc, d.prh = pre.stride(0), pre.stride(1), pre.stride(2)
+    key = conv_key(d, nd)  # (a conv with `pre` shares the tuned form of its shape)
     d.hint = int(hint) if hint else HINT_SET.get(tag, TUNED_HINTS.get(key, 0))
     if (B * max(Di * Hi * Wi, Do * Ho * Wo) >= XCD_SLAB_MIN_PIX and (nd == 2 or XCD_SLAB_3D)) or \
             (nd == 3 and XCD_SLAB_3D and pc.cin >= 32 and B * Do * Ho * Wo >= XCD_SLAB_MIN_VOX_WIDE) or \
             tag in XCD_SLAB_OPS:
         d.hint |= HINT_XCD_SLAB
-    ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up)
+    ctx.hold(pc.w, pc.scale, pc.shift, *srcs, out, out2, mul, res, up, pre)
     taps = pc.k ** nd
     if pc.transposed:  # algorithmic ConvT count: every input voxel meets every kernel tap
         macs = B * Di * Hi * Wi * pc.cin * pc.cout * taps
@@ -647,12 +699,12 @@ def _conv_desc(ctx: Ctx, pc: PackedConv, srcs: Sequence[torch.Tensor], out: Opti
         macs = B * Do * Ho * Wo * pc.cin * pc.cout * taps
     in_bytes = 4 * B * cin * Di * Hi * Wi
     out_bytes = 4 * B * pc.cout * Do * Ho * Wo * (2 if out2 is not None else 1)
-    extra = 4 * sum(t.numel() for t in (res, mul, up) if t is not None)
+    extra = 4 * sum(t.numel() for t in (res, mul, up, pre) if t is not None)
     w_bytes = 4 * pc.cin * pc.cout * taps  # the layer's weights (the packed slab's padding is not algorithmic)
     meta = dict(name=tag, kind="conv", flops=2 * macs, bytes=in_bytes + out_bytes + extra + w_bytes,
                 shape=f"{'T' if pc.transposed else ''}{nd}d k{pc.k}s{pc.stride} {cin}->{pc.cout} "
                       f"in {Di}x{Hi}x{Wi} out {Do}x{Ho}x{Wo}",
-                reads=_spans(*srcs, mul, res, up), writes=_spans(out, out2), key=key, hint=d.hint)
+                reads=_spans(*srcs, mul, res, up, pre), writes=_spans(out, out2), key=key, hint=d.hint)
     return d, out, meta
 
 
@@ -743,6 +795,16 @@ CONVT1X1_ENABLED = _ab("ESM_CONVT_1X1", "1") != "0"
 CONVT1X1_PAIRED = _ab("ESM_CONVT_1X1_PAIRED", "1") == "1"
 CONVT1X1_MAX_EXTRA = 48  # extra channels the fused kernels instantiate (conv_up1.hip kUp1MaxXB * 4)
 
+# Fork-join (round 6): the image-feature part of the upsampler stages' concat convs (spx_<t>[0] over
+# cat(disparity features, left features), models/ESMStereo.py:488, 501) as a partial sum on the plan's side
+# branch, overlapping the cost-volume -> hourglass chain; the chain's conv then reads only the disparity
+# features and starts from that sum (esm_conv_desc.pre).  Measured (round 6, three alternations on one box) and
+# NOT taken: a captured hipGraph with a second branch costs far more per replay than the overlap saves (S-K
+# 0.4166-0.4204 ms forked vs 0.3069-0.3072 ms as one chain; L-K B = 4 4.885-4.896 vs 4.685-4.696 ms), so the
+# default keeps one conv over the concat; ESM_FORK=1 forks (A/B; the kernels and the plan's branch API stay
+# tested: test_conv_partial_sum, test_convt_1x1_partial_sum, test_plan_side_branch_matches_eager).
+FORK_ENABLED = _ab("ESM_FORK", "0") == "1"
+
 
 def convt_1x1_supported(pa: PackedConv, pb: PackedConv, extra: Sequence[torch.Tensor]) -> bool:
     """Python mirror of conv_up1.h up1_check (plus the on/off switch)."""
@@ -757,7 +819,7 @@ def convt_1x1_supported(pa: PackedConv, pb: PackedConv, extra: Sequence[torch.Te
 
 
 def run_convt_1x1(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv, extra: Sequence[torch.Tensor],
-                  tags: Tuple[str, str] = ("convT", "conv1x1")) -> torch.Tensor:
+                  tags: Tuple[str, str] = ("convT", "conv1x1"), pre: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``pb(cat(crop(pa(srcs)), *extra))`` (models/ESMStereo.py:163-175, 221-234) as one launch: the transposed
     conv's output is cropped to the extra sources' extent and never written."""
     da, _, ma = _conv_desc(ctx, pa, srcs, tag=tags[0], alloc_out=False)
@@ -765,7 +827,7 @@ def run_convt_1x1(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: Pa
     e0 = extra[0]
     geo = (int(e0.shape[0]), pa.cout) + tuple(int(v) for v in e0.shape[2:])
     virt = srcs[0].as_strided(geo, (0,) * (len(geo) - 1) + (1,))  # the crop's geometry only, never read
-    db, out, mb = _conv_desc(ctx, pb, [virt, *extra], tag=tags[1])
+    db, out, mb = _conv_desc(ctx, pb, [virt, *extra], tag=tags[1], pre=pre)
     db.hint = 0
     B = int(e0.shape[0])
     vox = math.prod(int(v) for v in e0.shape[2:])
@@ -777,9 +839,40 @@ def run_convt_1x1(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: Pa
                          key=ma["key"] + " | " + mb["key"], hint=da.hint))
     if ctx._submit():
         if ctx.plan:
-            check(lib.esm_plan_add_convt_1x1(ctx.plan, ctypes.byref(da), ctypes.byref(db)), "plan_add_convt_1x1")
+            ctx._placed(check(lib.esm_plan_add_convt_1x1(ctx.plan, ctypes.byref(da), ctypes.byref(db)), "plan_add_convt_1x1"))
         else:
             check(lib.esm_convt_1x1_f32(ctypes.byref(da), ctypes.byref(db), ctx.stream), "convt_1x1")
+    return out
+
+
+def forked_packs(owner: torch.nn.Module, conv: torch.nn.Module, bn: Optional[torch.nn.Module], act: int, cm: int,
+                 cs: int) -> Tuple[PackedConv, PackedConv]:
+    """(side part: input channels [cm, cm + cs), plain sum; main part: [0, cm) + BN + act) of a 2-D conv."""
+    def build():
+        return (pack_conv_split(conv, None, act, cm, cm + cs), pack_conv_split(conv, bn, act, 0, cm))
+    return cached_pack(owner, f"fork{cm}", [conv, bn], build)
+
+
+def run_side_partial(ctx: Ctx, p_side: PackedConv, side: torch.Tensor, tag: str, cm: int) -> torch.Tensor:
+    """The side channels' partial sum on the plan's side branch (it reads only plan inputs); the next main op
+    joins it."""
+    with ctx.side():
+        part = run_conv(ctx, p_side, [side], tag=tag + "[side]")
+    ctx.meta[-1].update(layer=tag, split=(cm, cm + p_side.cin))
+    ctx.join_next()
+    return part
+
+
+def run_conv_forked(ctx: Ctx, owner: torch.nn.Module, conv: torch.nn.Module, bn: Optional[torch.nn.Module], act: int,
+                    main: Sequence[torch.Tensor], side: torch.Tensor, tag: str = "conv") -> torch.Tensor:
+    """``conv(cat(*main, side))`` + BN + ``act`` as two launches: the ``side`` channels' partial sum on the plan's
+    side branch, then the ``main`` channels' conv starting from it (esm_conv_desc.pre), on the main chain behind
+    a join.  fp32 reassociation of the channel sum only (tests hold it to 1e-5)."""
+    cm = sum(int(t.shape[1]) for t in main)
+    p_side, p_main = forked_packs(owner, conv, bn, act, cm, int(side.shape[1]))
+    part = run_side_partial(ctx, p_side, side, tag, cm)
+    out = run_conv(ctx, p_main, list(main), pre=part, tag=tag)
+    ctx.meta[-1].update(layer=tag, split=(0, cm))
     return out
 
 

@@ -144,6 +144,13 @@ typedef struct {
     float post_scale;
     float post_scale2;
     float* out2; /* nullable: second copy of the result (same strides as out), x post_scale2 / post_scale */
+    /* nullable (round 6): a partial conv sum over other input channels, [B, Cout, Ho, Wo] (2-D, element strides
+     * prb / prc / prh, W contiguous), added before the BN scale/shift: acc = pre + sum over this conv's sources.
+     * The upsampler stages' concat convs (models/ESMStereo.py:488, 501) split this way: the image-feature part
+     * runs on the plan's side branch (esm_plan_set_branch) while the disparity chain runs.  Lean, register-
+     * weight and LDS-tiled 2-D forms (and esm_convt_1x1_f32's second desc); ESM_ERR_ARG elsewhere. */
+    const float* pre;
+    int64_t prb, prc, prh;
 } esm_conv_desc;
 
 /* ShuffleMixer per-pixel chain on a [B, C, H, W] tensor, C in {8, 16}:
@@ -386,6 +393,13 @@ int esm_plan_add_shuffle_tail(esm_plan* plan, const esm_shuffle_tail_desc* desc)
 int esm_plan_add_shuffle_conv(esm_plan* plan, const esm_shuffle_conv_desc* desc);
 int esm_plan_add_conv_pair2(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
 int esm_plan_add_convt_1x1(esm_plan* plan, const esm_conv_desc* a, const esm_conv_desc* b);
+/* Fork-join (round 6).  Op `index` runs on the plan's second stream (branch 1) instead of the main chain
+ * (branch 0): forked from the start of every run / graph replay, so it overlaps the main chain.  A side op
+ * may read only buffers no main op writes before the join and write only buffers no main op reads before it.
+ * esm_plan_set_join(index, 1): main op `index` first waits for every side op listed before it (the join);
+ * side ops not joined by any op are joined at the end of the plan.  Both return the previous value. */
+int esm_plan_set_branch(esm_plan* plan, int index, int branch);
+int esm_plan_set_join(esm_plan* plan, int index, int join);
 int esm_plan_add_gwc(esm_plan* plan, const float* L, const float* R, const float* att, float* V, int B, int C,
                      int H, int W, int D, int G);
 int esm_plan_add_gwc_stem(esm_plan* plan, const esm_conv_desc* stem, const float* L, const float* R, int C, int G);

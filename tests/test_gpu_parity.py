@@ -302,6 +302,12 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
         outs[hint] = y
     if cout <= 8 and k == 3 and s == 1:
         assert torch.equal(outs[1 << 29], outs[0]) and torch.equal(outs[2 << 26 | 1 << 29], outs[2 << 26])
+    if cout in (24, 40) and k == 3 and s == 1:
+        # round 6: the plane-pair hybrid for 16 MF + 8 couts (default) is bitwise the padded MT form (bit 29)
+        for rows in (1 << 26, 2 << 26):
+            hz = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows)
+            mt = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 29)
+            assert torch.equal(hz, mt), hex(rows)
     res = torch.randn(ref.shape)
     mul = torch.rand(B, cout, ref.shape[3], ref.shape[4]) + 0.5
     want = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res)
@@ -887,6 +893,101 @@ def test_convt_1x1(nd, cin, cy, cxs, coutb, grid, crop, B, hint):
     ud = run_conv(ctx, pa_, [xd])
     two = run_conv(ctx, pb_, [ud[(slice(None), slice(None)) + tuple(slice(0, n) for n in crop)], *xsd])
     assert rel(y, two) < 1e-5
+
+
+PRE_CASES = [  # (main channels, side channels, cout, k, H, W, B, hint): the fork-join partial sums (round 6)
+    (16, 24, 16, 3, 96, 312, 1, 0x18400000),   # spx_4x.0 (S): the register-weight form, K split
+    (16, 32, 16, 3, 24, 78, 1, 0),             # spx_2x.0 (S): automatic (lean)
+    (16, 32, 16, 3, 24, 78, 1, 0x20200000),    # lean, 8 waves
+    (32, 48, 32, 3, 96, 312, 2, 0x8800000),    # spx_2x.0 (L): LDS-tiled, 2 rows
+    (32, 48, 32, 1, 48, 156, 2, 0x800000),     # agg_N.0 (L): LDS-tiled 1x1
+    (16, 24, 16, 1, 37, 70, 2, 0x400000),      # 1x1 register-weight form, ragged
+]
+
+
+@pytest.mark.parametrize("cm,cs,cout,k,H,W,B,hint", PRE_CASES)
+def test_conv_partial_sum(cm, cs, cout, k, H, W, B, hint):
+    """conv(cat(main, side)) as the side channels' plain partial sum + the main channels' conv started from it
+    (esm_conv_desc.pre) vs fp64 torch of the whole layer (relative 1e-5), in the forms that take `pre`."""
+    from esmstereo_amd.engine import pack_conv_split
+    conv, bn = _mk(2, cm + cs, cout, k, 1, k // 2, seed=cm + cs + k)
+    xm, xs = torch.randn(B, cm, H, W), torch.randn(B, cs, H, W)
+    ref = _ref_conv([xm, xs], conv, bn, ACT_GELU)
+    c_, b_ = copy.deepcopy(conv).to(DEV), copy.deepcopy(bn).to(DEV)
+    p_side, p_main = pack_conv_split(c_, None, ACT_GELU, cm, cm + cs), pack_conv_split(c_, b_, ACT_GELU, 0, cm)
+    ctx = Ctx(DEV)
+    part = run_conv(ctx, p_side, [xs.to(DEV)], hint=hint)
+    y = run_conv(ctx, p_main, [xm.to(DEV)], pre=part, hint=hint)
+    assert rel(y, ref) < 1e-5
+    with pytest.raises((ValueError, E.EsmError)):  # a 3-D conv takes no partial sum
+        c3, b3 = _mk(3, 8, 8, 3, 1, 1, seed=5)
+        p3 = pk(c3, b3, ACT_GELU)
+        x3 = torch.randn(1, 8, 4, 6, 20, device=DEV)
+        run_conv(Ctx(DEV), p3, [x3], pre=torch.zeros(1, 8, 4, 6, 20, device=DEV))
+
+
+def test_convt_1x1_partial_sum():
+    """The fused transposed conv + 1x1 with the 1x1's image-feature channels as a side partial sum (b.pre)."""
+    from esmstereo_amd.engine import pack_conv_split, run_convt_1x1
+    for hint in (0x4800000, 0):
+        ca, ba = _mk(2, 16, 16, 4, 2, 1, transposed=True, seed=71)
+        cb, bb = _mk(2, 16 + 16 + 24, 16, 1, 1, 0, seed=72)
+        x = torch.randn(1, 16, 48, 156)
+        skip, feat = torch.randn(1, 16, 96, 312), torch.randn(1, 24, 96, 312)
+        u = _ref_conv([x], ca, ba, ACT_GELU)
+        ref = _ref_conv([u, skip, feat], cb, bb, ACT_GELU)
+        cb_, bb_ = copy.deepcopy(cb).to(DEV), copy.deepcopy(bb).to(DEV)
+        p_side, p_main = pack_conv_split(cb_, None, ACT_GELU, 32, 56), pack_conv_split(cb_, bb_, ACT_GELU, 0, 32)
+        from esmstereo_amd import engine as EN
+        old = dict(EN.HINT_SET)
+        EN.HINT_SET["convT"] = hint
+        try:
+            ctx = Ctx(DEV)
+            part = run_conv(ctx, p_side, [feat.to(DEV)])
+            y = run_convt_1x1(ctx, pk(ca, ba, ACT_GELU), [x.to(DEV)], p_main, [skip.to(DEV)], pre=part)
+        finally:
+            EN.HINT_SET.clear()
+            EN.HINT_SET.update(old)
+        assert rel(y, ref) < 1e-5, hex(hint)
+
+
+def test_plan_side_branch_matches_eager():
+    """A plan with side-branch ops (the fork-join partial sums) gives bitwise the same outputs eagerly, as a graph,
+    and after a zero-copy rebind of its inputs (the side ops read the image features), as the eager modules."""
+    from esmstereo_amd import blocks as BL
+    name = next(k for k in HOT if k.startswith("hot_S_gwc"))
+    model, sd, m = _model_from_manifest(name)
+    fork0 = BL.FORK_ENABLED
+    BL.FORK_ENABLED = True  # (off by default: measured slower as a graph branch, engine.FORK_ENABLED)
+    try:
+        _side_branch_case(model, name)
+    finally:
+        BL.FORK_ENABLED = fork0
+
+
+def _side_branch_case(model, name):
+    g = load_golden(name)
+    up = [cu(g[f"up_{i}"]) for i in range(4) if f"up_{i}" in g]
+    att = cu(g["att"]) if "att" in g else None
+    ml, mr = cu(g["match_left"]), cu(g["match_right"])
+    B, C, h, w = (int(v) for v in ml.shape)
+    hp = E.HotPath(model, B, h, w, 0 if att is None else int(att.shape[1]), [tuple(u.shape) for u in up], DEV,
+                   channels=C, graph=False)
+    assert any(x.get("branch") for x in hp.ctx.meta), "the S plan forks"
+    hp.load_inputs(ml, mr, att, up)
+    hp.launch()
+    torch.cuda.synchronize()
+    eager = [o.clone() for o in hp.outputs]
+    hp.graph = True
+    hp.launch()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(eager, hp.outputs))
+    up2 = [u.clone() for u in up]  # new addresses: rebind moves every op pointer, side ops included
+    hp.bind(ml, mr, att, up2)
+    hp.launch()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(eager, hp.outputs))
+    hp.close()
 
 
 def test_convt_1x1_rejects():

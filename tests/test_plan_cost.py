@@ -73,9 +73,10 @@ def _layer(model, name):
     return mod.conv if isinstance(mod, E.BasicConv) else mod
 
 
-def _conv_cost(conv, B, ein, eout, scale2=False):
-    """(flops, bytes, output extent re-derived from the layer) of one conv launch."""
-    w = conv.weight
+def _conv_cost(conv, B, ein, eout, scale2=False, split=None):
+    """(flops, bytes, output extent re-derived from the layer) of one conv launch; ``split`` = (lo, hi): the
+    launch covers the layer's input channels [lo, hi) only (round 6: the fork-join partial sums)."""
+    w = conv.weight if split is None else conv.weight[:, split[0]:split[1]]
     nd = w.dim() - 2
     taps = math.prod(w.shape[2:])
     tr = isinstance(conv, (torch.nn.ConvTranspose2d, torch.nn.ConvTranspose3d))
@@ -102,7 +103,10 @@ def test_plan_per_op_cost(case):
         if kind == "conv":
             g = re.search(r"in (\S+) out (\S+)", shape)
             ein, eout = _ext(g.group(1)), _ext(g.group(2))
-            f, b, want, nout = _conv_cost(_layer(m, name), B, ein, eout)
+            split = op.get("split")
+            f, b, want, nout = _conv_cost(_layer(m, op.get("layer", name)), B, ein, eout, split=split)
+            if split is not None and split[0] == 0:
+                b += 4 * nout  # the chain's part reads the side branch's partial sum
             assert want == eout[-len(want):], (name, want, eout)
             assert op["flops"] == f, name
             if re.match(r"upsample_module\.ref\d+x\.conv1_up$", name):
@@ -131,7 +135,10 @@ def test_plan_per_op_cost(case):
             ga, gb = re.search(r"in (\S+) out (\S+)", sa), re.search(r"in (\S+) out (\S+)", sb)
             la, lb = _layer(m, na), _layer(m, nb)
             fa, ba, wa, nout = _conv_cost(la, B, _ext(ga.group(1)), _ext(ga.group(2)))
-            fb, bb, wb, _ = _conv_cost(lb, B, _ext(gb.group(1)), _ext(gb.group(2)))
+            split = op.get("split")
+            fb, bb, wb, nb = _conv_cost(lb, B, _ext(gb.group(1)), _ext(gb.group(2)), split=split)
+            if split is not None:
+                bb += 4 * nb  # the fork-join partial sum of the image-feature channels, read
             cy = la.weight.shape[1]
             crop = _ext(gb.group(1))[-la.weight.dim() + 2:]
             assert all(c <= u for c, u in zip(crop, wa)), name
