@@ -26,6 +26,9 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
 bool tile2_auto(const esm_conv_desc& a);                 // conv_tile3.hip
 bool tile2_ok(const esm_conv_desc& a);                   // conv_tile3.hip
 int launch_tile2(const esm_conv_desc& a, hipStream_t s);  // conv_tile3.hip
+bool pw_ok(const esm_conv_desc& a);                       // conv_pw.hip
+bool pw_auto(const esm_conv_desc& a);                     // conv_pw.hip
+int launch_pw(const esm_conv_desc& a, hipStream_t s);     // conv_pw.hip
 }  // namespace conv
 
 constexpr int kHintStem = 1 << 17;    // force the 16-block narrow-output form (conv_stem.hip)
@@ -103,6 +106,11 @@ int launch_conv(const esm_conv_desc* d, hipStream_t s) {
         if (tile_auto && (d3 ? conv::tile3_auto(a) : conv::tile2_auto(a))) return d3 ? conv::launch_tile3(a, s) : conv::launch_tile2(a, s);
         if ((a.hint & kHintSmall) || (form == 0 && conv::small_auto(a))) return conv::launch_small(a, s);
         return d3 ? launch_conv3d(a, s) : launch_conv2d(a, s);
+    }
+    // 1x1 on the large maps / volumes: the pointwise streaming form (round 6); TILE3 | bit 29 forces it, TILE3
+    // alone the LDS-tiled k1 form (A/B)
+    if (((a.hint & kHintTile3) && (a.hint & (1 << 29))) || (tile_auto && conv::pw_auto(a))) {
+        if (conv::pw_ok(a)) return conv::launch_pw(a, s);
     }
     if (a.hint & kHintSmall) return conv::launch_small(a, s);
     if (a.hint & kHintWide) {

@@ -55,13 +55,15 @@ struct T3Geo {
 
 // NS: input sources (a channel concat of up to 3, 4-channel aligned splits; 1x1x1 only): every k-step
 // lies inside one source, whose descriptor and offsets are selected per k-step (wave-uniform)
-// WREG (plane pairs only, round 6): each lane loads its composite-weight A operands straight into registers (36
-// per k-step, reloaded for the next k-step right after their last MFMA) instead of the workgroup staging them in
-// LDS: 18 KB less LDS per workgroup (agg at L-K: 2 -> 4 workgroups per CU), no weight stores
+// WREG (plane pairs and the stride-2 MT form, round 6): each lane loads its (composite-)weight A operands
+// straight into registers (36, or 27 MT, per k-step, reloaded for the next k-step right after their last MFMA)
+// instead of the workgroup staging them in LDS: 18 KB less LDS per workgroup (agg at L-K: 2 -> 4 workgroups per
+// CU), no weight stores
 template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false, bool WREG = false>
-__global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc a, int ncg) {
+__global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) tconv3_kernel(const esm_conv_desc a, int ncg) {
     using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
-    static_assert(!WREG || PZ, "register weights: plane pairs only");
+    static_assert(!WREG || PZ || (K == 3 && !D2 && NS == 1), "register weights: plane pairs or 3x3x3 MT");
+    constexpr int NWA = PZ ? 36 : G::TAPS * MT;  // register A operands per k-step (WREG)
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
     constexpr int XR = G::XR, WR = WREG ? 1 : G::WR, NR = G::NR;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
@@ -198,34 +200,47 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
         }
     };
     // WREG: lane (g, n)'s A operand of (input plane p, tap t9) at the k-step of channel c0 is
-    // W[dz = p - n / 8][t9][c0 + g][n % 8] (zero outside dz 0..2 or past Cout)
-    unsigned wpo[4];
-    float wa[WREG ? 36 : 1];
+    // W[dz = p - n / 8][t9][c0 + g][n % 8] (zero outside dz 0..2 or past Cout); the MT form (round 6, the stride-2
+    // downsamplers): operand (tap, mt) is W[tap][c0 + g][mg MT 16 + 16 mt + n], 27 MT registers
+    constexpr int NWP = PZ ? 4 : MT;
+    unsigned wpo[NWP];
+    float wa[WREG ? NWA : 1];
     if constexpr (WREG) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int dz = p - (n >> 3), co = n & 7;
-            wpo[p] = (dz >= 0 && dz <= 2 && co < a.Cout)
-                         ? 4u * static_cast<unsigned>((dz * 9 * a.cin_pad + g) * a.cout_pad + co)
-                         : kOOB;
+        for (int p = 0; p < NWP; ++p) {
+            if constexpr (PZ) {
+                const int dz = p - (n >> 3), co = n & 7;
+                wpo[p] = (dz >= 0 && dz <= 2 && co < a.Cout)
+                             ? 4u * static_cast<unsigned>((dz * 9 * a.cin_pad + g) * a.cout_pad + co)
+                             : kOOB;
+            } else {
+                const int co = mg * MT * 16 + p * 16 + n;
+                wpo[p] = co < a.cout_pad ? 4u * static_cast<unsigned>(g * a.cout_pad + co) : kOOB;
+            }
         }
     }
     auto wreg_load = [&](int i, int c0) __attribute__((always_inline)) {
-        if constexpr (WREG) wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + c0) * a.cout_pad);
+        if constexpr (WREG && PZ) wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + c0) * a.cout_pad);
+        if constexpr (WREG && !PZ) wa[i] = buf_load_s(wrs, wpo[i % MT], 4 * ((i / MT) * a.cin_pad + c0) * a.cout_pad);
     };
 
-    // epilogue constants, loaded while the first k-step streams in
+    // epilogue constants, loaded while the first k-step streams in (the register-weight MT form: in the
+    // epilogue, 16 registers it needs for the weights)
     constexpr int NCO = PZ ? 1 : MT;
+    constexpr bool LATE_BN = WREG && !PZ;
     float scl[NCO][4], shf[NCO][4];
+    auto load_bn = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int mt = 0; mt < NCO; ++mt)
+        for (int mt = 0; mt < NCO; ++mt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = PZ ? ((4 * g + j) & 7) : mg * MT * 16 + mt * 16 + 4 * g + j;
-            const int cc = min(co, a.Cout - 1);
-            scl[mt][j] = a.scale ? a.scale[cc] : 1.f;
-            shf[mt][j] = a.shift ? a.shift[cc] : 0.f;
-        }
+            for (int j = 0; j < 4; ++j) {
+                const int co = PZ ? ((4 * g + j) & 7) : mg * MT * 16 + mt * 16 + 4 * g + j;
+                const int cc = min(co, a.Cout - 1);
+                scl[mt][j] = a.scale ? a.scale[cc] : 1.f;
+                shf[mt][j] = a.shift ? a.shift[cc] : 0.f;
+            }
+    };
+    if constexpr (!LATE_BN) load_bn();
 
     floatx4 acc[NT][NCO];
 #pragma unroll
@@ -239,7 +254,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     stage_load(0);
     if constexpr (WREG) {
 #pragma unroll
-        for (int i = 0; i < 36; ++i) wreg_load(i, 0);
+        for (int i = 0; i < NWA; ++i) wreg_load(i, 0);
     }
     stage_store(0);
     __syncthreads();
@@ -267,7 +282,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
                     }
                 }
         } else {
-            const float* wp = &ws[buf][g * WCS + n];
+            const float* wp = &ws[WREG ? 0 : buf][g * WCS + n];
 #pragma unroll
             for (int dz = 0; dz < G::KD; ++dz)
 #pragma unroll
@@ -277,15 +292,19 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
                     for (int r = 0; r < NR; ++r) br[r] = xw[(zw * S + dz) * PLANE + r * IX + dx];
 #pragma unroll
                     for (int dy = 0; dy < K; ++dy) {
+                        const int tap = (dz * K + dy) * K + dx;
                         float av[MT];
 #pragma unroll
-                        for (int mt = 0; mt < MT; ++mt) av[mt] = wp[((dz * K + dy) * K + dx) * 4 * WCS + mt * 16];
+                        for (int mt = 0; mt < MT; ++mt)
+                            av[mt] = WREG ? wa[WREG ? tap * MT + mt : 0] : wp[tap * 4 * WCS + mt * 16];
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
                             for (int mt = 0; mt < MT; ++mt)
                                 acc[nt][mt] =
                                     __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], br[nt * S + dy], acc[nt][mt], 0, 0, 0);
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) wreg_load(tap * MT + mt, 4 * (ch + 1));
                     }
                 }
         }
@@ -294,6 +313,7 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
     }
 
     // ---- epilogue: lane (g, n) holds rows 4g + j of each tile, column n
+    if constexpr (LATE_BN) load_bn();
     const int x = xo0 + n;
     const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0),
@@ -345,9 +365,12 @@ __global__ void __launch_bounds__(kT3Threads) tconv3_kernel(const esm_conv_desc 
 // lane, reloaded for the next k-step after their last use, as WREG), the full tiles' weights are staged in LDS.
 // Per output the products and their order (dz, dx, dy within a k-step, k-steps in channel order) are the MT
 // form's, so the result is bit-identical to it.  Plain BasicConv epilogue only (BN + GELU).
-template <int MF, int NT>
+// WZ: waves along z (plane pairs per workgroup; 4 / WZ waves along y): 2 where Do is not a multiple of 8 (the
+// 12-plane conv2.1 / agg_0.1 at L-K: 16 planes computed for 12 with 4)
+template <int MF, int NT, int WZ = 4>
 struct HzGeo {
-    static constexpr int ZB = 8, IZ = ZB + 2, IY = NT + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
+    static constexpr int WY = 4 / WZ, ZB = 2 * WZ, YB = WY * NT;
+    static constexpr int IZ = ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
     static constexpr int CS = CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;  // channel stride = 16 mod 32 banks
     static constexpr int XE = 4 * CS0, XL = 4 * CS, XR = (XE + kT3Threads - 1) / kT3Threads;
     static constexpr int WCS = MF % 2 ? 16 * MF : 16 * MF + 16;      // weight row stride = 16 mod 32
@@ -355,18 +378,19 @@ struct HzGeo {
     static constexpr int NR = NT + 2;
 };
 
-template <int MF, int NT>
+template <int MF, int NT, int WZ>
 __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_desc a) {
-    using G = HzGeo<MF, NT>;
+    using G = HzGeo<MF, NT, WZ>;
     constexpr int IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS, XR = G::XR, WR = G::WR, NR = G::NR;
     __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
     __shared__ __attribute__((aligned(16))) float ws[2][G::WL];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, g = lane >> 4, n = lane & 15;
-    const int zw = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int zw = wave % WZ, yw = wave / WZ;
     const Blk3 bk_ = xcd_block((a.hint & kHintXcd) != 0);
-    const int xo0 = bk_.x * 16, yo0 = bk_.y * NT;
+    const int xo0 = bk_.x * 16, yo0 = bk_.y * G::YB;
     const int nzb = (a.Do + G::ZB - 1) / G::ZB;
     const int b = bk_.z / nzb;
     const int zo0 = (bk_.z - b * nzb) * G::ZB;
@@ -449,7 +473,7 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
     for (int ch = 0; ch < nchunk; ++ch) {
         const int buf = ch & 1;
         if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
-        const float* xw = &xs[buf][g * CS + n];
+        const float* xw = &xs[buf][g * CS + yw * NT * IX + n];
         const float* wp = &ws[buf][g * WCS + n];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -511,7 +535,7 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
     };
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const int y = yo0 + nt;
+        const int y = yo0 + yw * NT + nt;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -530,13 +554,14 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
     }
 }
 
-template <int MF, int NT>
+template <int MF, int NT, int WZ = 4>
 int launch_hz(const esm_conv_desc& a, hipStream_t s) {
-    const long long z = static_cast<long long>(a.B) * ((a.Do + 7) / 8);
-    const long long gy = ceil_div(a.Ho, NT);
+    using G = HzGeo<MF, NT, WZ>;
+    const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB);
+    const long long gy = ceil_div(a.Ho, G::YB);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3 hz): grid too large");
     const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
-    hipLaunchKernelGGL((tconv3hz_kernel<MF, NT>), grid, dim3(kT3Threads), 0, s, a);
+    hipLaunchKernelGGL((tconv3hz_kernel<MF, NT, WZ>), grid, dim3(kT3Threads), 0, s, a);
     return check_launch("conv(tile3 hz)");
 }
 
@@ -909,6 +934,15 @@ int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
     return arg_error("conv(tile3): at most 96 output channels");
 }
 
+// stride 2, register weights: one cout group of 1..3 tiles
+template <int NT, int WZ>
+int launch_t3_mtw(const esm_conv_desc& a, hipStream_t s) {
+    const int tiles = (a.Cout + 15) / 16;
+    if (tiles == 1) return launch_t3<2, 3, 1, NT, WZ, false, 1, false, true>(a, s, 1);
+    if (tiles == 2) return launch_t3<2, 3, 2, NT, WZ, false, 1, false, true>(a, s, 1);
+    return launch_t3<2, 3, 3, NT, WZ, false, 1, false, true>(a, s, 1);
+}
+
 // 1x1x1 over 1..3 sources
 template <int NT>
 int launch_t3_k1(const esm_conv_desc& a, hipStream_t s) {
@@ -1026,6 +1060,12 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
         return launch_t3_k1<4>(a, s);
     }
     if (a.stride == 2) {  // one row per wave unless asked (r04 probe, L-K B = 4: conv1.0 274 -> 226 us, conv2.0 92 -> 86)
+        // round 6: the weights as register operands (<= 3 cout tiles per workgroup, one source); hint bit 29: LDS
+        if (!((a.hint >> 29) & 1) && a.nsrc == 1 && a.Cout <= 32) {  // (3 tiles: 150 VGPRs, conv2.0 84 -> 88 us)
+            if (rsel == 2) return launch_t3_mtw<2, 2>(a, s);
+            if (rsel == 3) return launch_t3_mtw<4, 2>(a, s);
+            return launch_t3_mtw<1, 2>(a, s);
+        }
         if (rsel == 2) return launch_t3_mt<2, 3, 2, 2>(a, s);
         if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
         return launch_t3_mt<2, 3, 1, 2>(a, s);
@@ -1044,11 +1084,19 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
                                               static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain && !((a.hint >> 29) & 1) && (a.Cout == 24 || a.Cout == 40)) {
         const int nt = rsel == 1 ? 2 : rsel >= 2 ? 4 : (vox < (1LL << 19) ? 2 : 4);
-        if (a.Cout == 24) return nt == 2 ? launch_hz<1, 2>(a, s) : launch_hz<1, 4>(a, s);  // (8 rows spill)
-        return launch_hz<2, 2>(a, s);  // 40 couts: 2 rows per wave (4 and 8 exceed the register file)
+        const bool z2 = (a.Do % 8) != 0 && (a.Do % 4) == 0;  // 2 plane pairs x 2 row groups: no idle planes
+        if (a.Cout == 24) {
+            if (z2) return nt == 2 ? launch_hz<1, 2, 2>(a, s) : launch_hz<1, 4, 2>(a, s);
+            return nt == 2 ? launch_hz<1, 2>(a, s) : launch_hz<1, 4>(a, s);  // (8 rows spill)
+        }
+        return z2 ? launch_hz<2, 2, 2>(a, s) : launch_hz<2, 2>(a, s);  // 40 couts: 2 rows (4, 8 exceed the registers)
     }
-    if (rsel == 1) return launch_t3_mt<1, 3, 1, 4>(a, s);
-    if (rsel == 2 || (rsel == 0 && vox < (1LL << 19))) return launch_t3_mt<1, 3, 2, 4>(a, s);
+    // depth not a multiple of 4 (conv3.1 at L-K: 6 planes): 2 planes x 2 row groups per workgroup, no idle planes
+    const bool z2 = (a.Do % 4) != 0 && (a.Do % 2) == 0;
+    if (rsel == 1) return z2 ? launch_t3_mt<1, 3, 1, 2>(a, s) : launch_t3_mt<1, 3, 1, 4>(a, s);
+    if (rsel == 2 || (rsel == 0 && vox < (1LL << 19)))
+        return z2 ? launch_t3_mt<1, 3, 2, 2>(a, s) : launch_t3_mt<1, 3, 2, 4>(a, s);
+    if (z2 && rsel == 3 && !(a.hint & (1 << 28))) return launch_t3_mt<1, 3, 4, 2>(a, s);
     // 8 rows per wave on the largest volumes (L-K B = 4 aggregation_out.conv1.1, 24 -> 24 on 24x48x156: 277 vs 301
     // us for 4 rows, r04 probe); hint bit 28 with rows 4 asks for it explicitly
     if ((rsel == 3 && (a.hint & (1 << 28))) || rsel == 0) return launch_t3_mt<1, 3, 8, 4>(a, s);

@@ -41,7 +41,10 @@ CANDIDATES = [0, 0x11, 0x12, 0x14, 0x41, 0x42, 0x211, 0x212, 0x241, 0x242, 0x121
               (1 << 25) | (2 << 26), (1 << 22) | (1 << 28), (1 << 22) | (2 << 26) | (1 << 28),
               (1 << 22) | (3 << 26) | (1 << 28), (1 << 21) | (1 << 29),
               # round 4: the LDS-tiled form (rows per wave automatic / 1 / 2 / 4) and the rules without it
-              1 << 23, (1 << 23) | (1 << 26), (1 << 23) | (2 << 26), (1 << 23) | (3 << 26), 1 << 19]
+              1 << 23, (1 << 23) | (1 << 26), (1 << 23) | (2 << 26), (1 << 23) | (3 << 26), 1 << 19,
+              # round 6: bit 29 with the LDS-tiled form = its LDS-staged weights / padded MT (A/B of the register forms)
+              (1 << 23) | (1 << 29), (1 << 23) | (1 << 26) | (1 << 29), (1 << 23) | (2 << 26) | (1 << 29),
+              (1 << 23) | (3 << 26) | (1 << 29)]
 
 
 def op_time(hp, i: int, reps: int) -> float:

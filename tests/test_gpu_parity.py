@@ -308,6 +308,11 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
             hz = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows)
             mt = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 29)
             assert torch.equal(hz, mt), hex(rows)
+    if k == 3 and s == 2 and cout <= 32:
+        # round 6: the stride-2 MT form with register weights (default) is bitwise its LDS-weight form (bit 29)
+        for rows in (0, 1 << 26, 2 << 26, 3 << 26):
+            lw = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 29)
+            assert torch.equal(lw, outs[rows]), hex(rows)
     res = torch.randn(ref.shape)
     mul = torch.rand(B, cout, ref.shape[3], ref.shape[4]) + 0.5
     want = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res)
@@ -419,6 +424,51 @@ def test_conv_tile3_multisource_crop(cins, cout, shape):
     for rsel in (0, 1, 2, 3):
         y = run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), xd, hint=HINT_TILE3 | (rsel << 26))
         assert rel(y, ref) < 1e-5, rsel
+
+
+HINT_PW = HINT_TILE3 | 1 << 29  # on a 1x1: the pointwise streaming form (conv_pw.hip, round 6)
+PW_CASES = [  # (nd, cins, cout, shape, B, act, bn)
+    (2, (32, 32, 32), 32, (1, 48, 156), 2, ACT_GELU, True),   # up_refinement agg_1.0 (ref4x at L)
+    (2, (32, 32, 48), 32, (1, 23, 36), 1, ACT_GELU, True),    # agg_0.0, ragged last pixel group
+    (2, (32, 128), 32, (1, 12, 40), 2, ACT_GELU, True),       # 160 input channels
+    (3, (24, 24), 24, (6, 12, 40), 2, ACT_GELU, True),        # hourglass agg_1.0 (two cout tiles, padded)
+    (3, (40, 40), 40, (4, 6, 20), 1, ACT_GELU, True),         # agg_0.0 (three cout tiles)
+    (3, (8,), 48, (3, 5, 12), 2, ACT_NONE, False),            # one source, bias, no BN, no activation
+    (2, (16,), 8, (1, 10, 30), 1, ACT_SILU, True),            # one cout tile, 8 couts
+    (3, (12, 12, 12), 16, (2, 9, 14), 1, ACT_GELU, True),     # three sources
+]
+
+
+@pytest.mark.parametrize("nd,cins,cout,shape,B,act,bn", PW_CASES)
+def test_conv_pointwise_form(nd, cins, cout, shape, B, act, bn):
+    """The pointwise streaming form for 1x1 BasicConvs over a channel concat (conv_pw.hip) vs fp64 torch
+    (relative 1e-5); the LDS-tiled k1 form (TILE3 alone) for comparison."""
+    conv, b = _mk(nd, sum(cins), cout, 1, 1, 0, bias=not bn, bn=bn, seed=sum(cins) + cout)
+    sh = shape if nd == 3 else shape[1:]
+    xs = [torch.randn(B, c, *sh) for c in cins]
+    ref = _ref_conv(xs, conv, b, act)
+    p = pk(conv, b, act)
+    xd = [x.to(DEV) for x in xs]
+    y = run_conv(Ctx(DEV), p, xd, hint=HINT_PW)
+    assert rel(y, ref) < 1e-5
+    assert rel(run_conv(Ctx(DEV), p, xd, hint=HINT_TILE3), ref) < 1e-5
+    assert torch.equal(run_conv(Ctx(DEV), p, xd, hint=HINT_PW), y)  # deterministic
+
+
+def test_conv_pointwise_form_fallback():
+    """Layouts the pointwise form cannot stream (a cropped source view, P % 4 != 0) take the other forms
+    when the hint asks for it, with the same results."""
+    conv, bn = _mk(3, 48, 24, 1, 1, 0, seed=5)
+    big = torch.randn(1, 24, 5, 8, 13)
+    xs = [big[:, :, :4, :6, :10], torch.randn(1, 24, 4, 6, 10)]
+    ref = _ref_conv(xs, conv, bn, ACT_GELU)
+    bigd = big.to(DEV)
+    xd = [bigd[:, :, :4, :6, :10], xs[1].to(DEV)]
+    assert rel(run_conv(Ctx(DEV), pk(conv, bn, ACT_GELU), xd, hint=HINT_PW), ref) < 1e-5
+    conv2, bn2 = _mk(2, 16, 16, 1, 1, 0, seed=6)
+    x = torch.randn(1, 16, 7, 9)
+    assert rel(run_conv(Ctx(DEV), pk(conv2, bn2, ACT_GELU), [x.to(DEV)], hint=HINT_PW),
+               _ref_conv([x], conv2, bn2, ACT_GELU)) < 1e-5
 
 
 HINT_SMALL = 1 << 21
