@@ -10,10 +10,15 @@
 //     t = 0..3 with column n <-> pixel 4n + t: lane (q, n) reads channel 4k + q, pixels 4n .. 4n + 3 as
 //     ONE 16-byte load per k-step (a wave-instruction covers 4 channels x 64 pixels, 256-byte rows), and
 //     after the epilogue holds 4 consecutive pixels of each of its couts: 16-byte stores;
-//   * the weights (<= 192 x 48) sit in LDS once per workgroup (row stride = 16 mod 32 banks: conflict-
-//     free ds_read_b32 of the A operand, one per cout tile and k-step, shared by the 4 column tiles);
-//   * k-steps are unrolled by 4 with their loads issued together (4 x 1 KB in flight per wave);
-//   * the workgroup's 4 waves walk the pixel groups grid-stride, so the weight staging is amortised.
+//   * the weights (<= 192 x 48) sit in LDS once per workgroup, sized to Cin (row stride = 16 mod 32 banks:
+//     conflict-free ds_read_b32 of the A operand, one per cout tile and k-step, shared by the 4 column tiles);
+//   * per source, k-steps go in batches of 4, double-buffered: batch i + 1's loads (4 KB per wave) are in
+//     flight while batch i's 16 MT MFMAs run;
+//   * small launches with 3 cout tiles put one tile per workgroup (grid z) for occupancy.
+// (Round 6 measured two alternatives slower at L-K B = 4: no double buffering, 63 /
+//     56 us for ref4x.agg_1.0 / agg_1.0; A operands loaded from global per k-step with one flat k loop over
+//     the sources, ~79 us: the per-k-step source select put the buffer descriptor in vector registers, i.e.
+//     a waterfall loop around every load.)
 // Each output is one fixed-order sum (channel order, 4 per MFMA): deterministic, within fp32 reassociation
 // of the other forms (tests: 1e-5 relative).  Plain BasicConv epilogue (BN + activation) only.
 #include "conv_direct.h"
@@ -29,26 +34,27 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 template <int MT, int ACT>
 __global__ void __launch_bounds__(kPwThreads) pw_kernel(const esm_conv_desc a, int P, int ngroups) {
-    constexpr int WCS = MT % 2 ? MT * 16 : MT * 16 + 16;  // weight row stride, = 16 mod 32
+    constexpr int WCS = MT % 2 ? MT * 16 : MT * 16 + 16;        // weight row stride, = 16 mod 32
     extern __shared__ __attribute__((aligned(16))) float ws[];  // [round_up(Cin, 4)][WCS] (launcher's size)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, q = lane >> 4, n = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y;
+    const int m0 = blockIdx.z * MT * 16;  // first cout of this workgroup (cout-split launches: one tile per z)
 
     // weights: row = input channel (zero past Cin, up to the next multiple of 4), column = output channel
     const int cin4 = (a.Cin + 3) & ~3;
     for (int e = tid; e < cin4 * MT * 16; e += kPwThreads) {
         const int c = e / (MT * 16), m = e - c * (MT * 16);
-        ws[c * WCS + m] = (c < a.Cin && m < a.cout_pad) ? a.w[static_cast<long long>(c) * a.cout_pad + m] : 0.f;
+        ws[c * WCS + m] = (c < a.Cin && m0 + m < a.cout_pad) ? a.w[static_cast<long long>(c) * a.cout_pad + m0 + m] : 0.f;
     }
     float scl[MT][4], shf[MT][4];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int cc = min(16 * mt + 4 * q + r, a.Cout - 1);
+            const int cc = min(m0 + 16 * mt + 4 * q + r, a.Cout - 1);
             scl[mt][r] = a.scale ? a.scale[cc] : 1.f;
             shf[mt][r] = a.shift ? a.shift[cc] : 0.f;
         }
@@ -56,10 +62,6 @@ __global__ void __launch_bounds__(kPwThreads) pw_kernel(const esm_conv_desc a, i
 
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         a.out + b * a.ob, static_cast<short>(0), 4 * ((a.Cout - 1) * static_cast<int>(a.oc) + P), 0x00020000);
-    auto src_rsrc = [&](const esm_src& s) __attribute__((always_inline)) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(s.ptr + b * s.sb), static_cast<short>(0),
-                                                 4 * ((s.C - 1) * static_cast<int>(s.sc) + P), 0x00020000);
-    };
 
     for (int gi = blockIdx.x * 4 + wave; gi < ngroups; gi += gridDim.x * 4) {
         const int pp = gi * 64 + 4 * n;  // this lane's first pixel (P % 4 == 0: all four valid or none)
@@ -72,23 +74,29 @@ __global__ void __launch_bounds__(kPwThreads) pw_kernel(const esm_conv_desc a, i
 
         int c0 = 0;  // first (global) channel of the source
 #pragma unroll
-        for (int k = 0; k < ESM_MAX_SRC; ++k) {
-            if (k >= a.nsrc) break;
-            const esm_src& sk = a.src[k];
-            const __amdgpu_buffer_rsrc_t rs = src_rsrc(sk);
-            const int sc = static_cast<int>(sk.sc);
+        for (int j = 0; j < ESM_MAX_SRC; ++j) {
+            if (j >= a.nsrc) break;
+            const esm_src& sj = a.src[j];  // (compile-time index: the descriptor stays in scalar registers)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(sj.ptr + b * sj.sb), static_cast<short>(0),
+                4 * ((sj.C - 1) * static_cast<int>(sj.sc) + P), 0x00020000);
+            const int sc = static_cast<int>(sj.sc);
             const unsigned vo = pok ? 4u * static_cast<unsigned>(q * sc + pp) : kOOB;
-            const int ns = sk.C >> 2;
-            // U k-steps from s: loads first (in flight together), then 4 MT MFMAs per k-step
-            auto steps = [&](auto uc, int s) __attribute__((always_inline)) {
-                constexpr int U = decltype(uc)::value;
-                u32x4 bv[U];
+            const int ns = sj.C >> 2;
+            // batch i = k-steps 4i .. 4i + 3 (the last one partial: cnt = its k-steps, a wave-uniform count)
+            auto load_b = [&](u32x4 (&bv)[4], int i) __attribute__((always_inline)) {
+                const int cnt = min(4, ns - 4 * i);
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    bv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(vo), 16 * (s + u) * sc, 0);
+                for (int u = 0; u < 4; ++u)  // (past the source: range-checked zeros, which no MFMA reads)
+                    bv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(u < cnt ? vo : kOOB),
+                                                                  16 * (4 * i + u) * sc, 0);
+            };
+            auto mfma_b = [&](const u32x4 (&bv)[4], int i) __attribute__((always_inline)) {
+                const int cnt = min(4, ns - 4 * i);
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const float* wr = &ws[(c0 + 4 * (s + u) + q) * WCS + n];
+                for (int u = 0; u < 4; ++u) {
+                    if (u >= cnt) break;
+                    const float* wr = &ws[(c0 + 4 * (4 * i + u) + q) * WCS + n];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
                         const float av = wr[16 * mt];
@@ -99,18 +107,27 @@ __global__ void __launch_bounds__(kPwThreads) pw_kernel(const esm_conv_desc a, i
                     }
                 }
             };
-            int s = 0;
-            for (; s + 4 <= ns; s += 4) steps(std::integral_constant<int, 4>{}, s);
-            for (; s < ns; ++s) steps(std::integral_constant<int, 1>{}, s);
-            c0 += sk.C;
+            // double-buffered: batch i + 1's loads (up to 4 KB per wave) in flight during batch i's MFMAs
+            const int nb = (ns + 3) >> 2;
+            u32x4 b0[4], b1[4];
+            load_b(b0, 0);
+            int i = 0;
+            for (; i + 2 <= nb; i += 2) {
+                load_b(b1, i + 1);
+                mfma_b(b0, i);
+                if (i + 2 < nb) load_b(b0, i + 2);
+                mfma_b(b1, i + 1);
+            }
+            if (i < nb) mfma_b(b0, i);
+            c0 += sj.C;
         }
 
-        // epilogue: lane (n, q) holds couts 16 mt + 4 q + r at pixels 4n + t (t = 0..3): one 16-byte store each
+        // epilogue: lane (n, q) holds couts m0 + 16 mt + 4 q + r at pixels 4n + t (t = 0..3): one 16-byte store each
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int co = 16 * mt + 4 * q + r;
+                const int co = m0 + 16 * mt + 4 * q + r;
                 u32x4 o;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -160,22 +177,26 @@ int launch_pw(const esm_conv_desc& a, hipStream_t s) {
     if (!pw_ok(a)) return arg_error("conv: pointwise-form hint not applicable");
     const int P = a.Di * a.Hi * a.Wi;
     const int ngroups = (P + 63) / 64;
-    // one pixel group per wave up to 2^14 groups (latency hiding by occupancy: the weights' LDS is sized to
-    // Cin, 9-37 KB), then up to 8 per wave
     const long long total = static_cast<long long>(ngroups) * a.B;
+    const int tiles = (a.Cout + 15) / 16;
+    // launches of fewer than 4096 pixel groups with 3 cout tiles (agg_0.0 at L-K B = 4: 1404 groups, 40 couts; 23.6 ->
+    // 20.8 us): one cout tile per workgroup (grid z), tiles x the waves; else every tile in one wave, the B operands
+    // loaded once (2 tiles split measured slower: ref4x.agg_0.0, 112 -> 32 at 96 x 312, 24.7 -> 30.0 us)
+    const bool split = total < 4096 && tiles > 2;
+    // one pixel group per wave up to 2^14 groups (latency hiding by occupancy), then up to 8 per wave
     const int per_wave = static_cast<int>(std::max<long long>(1, std::min<long long>(8, total / 16384)));
     const int gx = std::max(1, (ngroups + 4 * per_wave - 1) / (4 * per_wave));
     if (a.B > 65535) return arg_error("conv(pointwise): batch too large");
-    const dim3 grid(gx, a.B);
-    const int mt = (a.Cout + 15) / 16;
+    const dim3 grid(gx, a.B, split ? tiles : 1);
+    const int mt = split ? 1 : tiles;
     const bool gelu = a.act == ESM_ACT_GELU;
     const size_t lds = 4u * static_cast<size_t>((a.Cin + 3) & ~3) * (mt % 2 ? mt * 16 : mt * 16 + 16);
-#define ESM_PW(M)                                                                                            \
-    do {                                                                                                     \
-        if (gelu)                                                                                            \
-            hipLaunchKernelGGL((pw_kernel<M, ESM_ACT_GELU>), grid, dim3(kPwThreads), lds, s, a, P, ngroups);   \
-        else                                                                                                 \
-            hipLaunchKernelGGL((pw_kernel<M, -1>), grid, dim3(kPwThreads), lds, s, a, P, ngroups);             \
+#define ESM_PW(M)                                                                                             \
+    do {                                                                                                      \
+        if (gelu)                                                                                             \
+            hipLaunchKernelGGL((pw_kernel<M, ESM_ACT_GELU>), grid, dim3(kPwThreads), lds, s, a, P, ngroups);  \
+        else                                                                                                  \
+            hipLaunchKernelGGL((pw_kernel<M, -1>), grid, dim3(kPwThreads), lds, s, a, P, ngroups);            \
     } while (0)
     if (mt == 1) ESM_PW(1);
     else if (mt == 2) ESM_PW(2);

@@ -26,8 +26,9 @@ struct StGeo {
     static constexpr int LRW = kTW / R + 2;
     // nf = 8, r = 4 (ESMStereo-S) builds the shuffled tile with MFMA: each low-res pixel's 4x4
     // sub-pixels land as 4 aligned columns, so its tile spans the whole low-res window (origin X0 - 4)
-    static constexpr bool MF = NF == 8 && R == 4;
-    static constexpr int MX0 = MF ? 4 : 1;  // tile column 0 = output column X0 - MX0
+    // (round 6: nf = 16, r = 2, ESMStereo-L, likewise: each low-res pixel's 2x2 sub-pixels as 2 aligned columns)
+    static constexpr bool MF = (NF == 8 && R == 4) || (NF == 16 && R == 2);
+    static constexpr int MX0 = MF ? R : 1;  // tile column 0 = output column X0 - MX0
     static constexpr int MH = TH + 2, MW = MF ? LRW * R : kTW + 2, MWP = MF ? MW : MW + 2;  // 16-B aligned rows
     static constexpr int NUP = NF * R * R;
     static constexpr int WN = NUP * NF + NUP + NF * 9 + 1;  // up_w, up_b, tail_w, tail_b
@@ -94,7 +95,47 @@ __global__ void __launch_bounds__(kThreads) shuffle_tail_kernel(const esm_shuffl
     const float* upb = wsh + NUP * NF;
     const float* tw = wsh + NUP * NF + NUP;
     const float tb = a.tail_b ? wsh[WN - 1] : 0.f;
-    if constexpr (G::MF) {
+    if constexpr (G::MF && R == 2) {
+        // nf = 16, r = 2 (ESMStereo-L's heads, round 6): the 1x1 as MFMA, M = the 64 up-channels (wave w: tile
+        // 16 w .. 16 w + 15 = channels 4w .. 4w + 3 x their 2x2 sub-pixels), N = 16 low-res pixels, K = the 16
+        // input channels (4 k-steps).  Lane (g, n) receives up-channels 16 w + 4 g + j, i.e. channel 4 w + g,
+        // sub-pixel (j / 2, j % 2) of low-res pixel n: two 8-byte LDS stores.  (The VALU loop it replaces did
+        // 64 FMAs per item with wave-uniform LDS weight reads: 110 us of the L-K B = 4 step's 4x head.)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+        float av[4], bias[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) av[kk] = upw[(wave * 16 + n) * NF + 4 * kk + g];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bias[j] = upb[wave * 16 + 4 * g + j];
+        const int c = 4 * wave + g;
+        const float* lrf = &lr[0][0][0];
+#pragma unroll 1
+        for (int nt = 0; nt < (PIX + 15) / 16; ++nt) {
+            const int p = nt * 16 + n;
+            const bool pin = p < PIX;
+            const int py = p / LRW, px = p - (p / LRW) * LRW;
+            conv::floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], lrf[(4 * kk + g) * PIX + (pin ? p : 0)], acc, 0, 0, 0);
+            const int X = (lx0 + px) * R;  // sub-pixel column 0
+#pragma unroll
+            for (int sy = 0; sy < 2; ++sy) {
+                const int Y = (ly0 + py) * R + sy;
+                const int my = Y - (Y0 - 1);
+                const bool yok = Y >= 0 && Y < HO;
+                f32x2 o;
+#pragma unroll
+                for (int sx = 0; sx < 2; ++sx) {
+                    const float v = silu_fast(acc[2 * sy + sx] + bias[2 * sy + sx]);
+                    o[sx] = (yok && X + sx >= 0 && X + sx < WO) ? v : 0.f;  // zero padding of the 3x3 tail
+                }
+                if (pin && my >= 0 && my < MH) *reinterpret_cast<f32x2*>(&mid[c][my][px * R]) = o;
+            }
+        }
+    } else if constexpr (G::MF) {
         // 1x1 conv as MFMA: M = the 16 sub-pixels (sy, sx) of one channel c, N = 16 low-res pixels,
         // K = the 8 input channels (2 k-steps).  Lane (g, n) gets sub-pixel row sy = g, columns
         // sx = 0..3 of low-res pixel n: one 16-byte LDS store per lane.  Wave w: channels 2w, 2w+1.

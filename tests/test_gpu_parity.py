@@ -745,7 +745,7 @@ def test_convt_c1_form(nd, cin):
         run_conv(Ctx(DEV), pk(c2, b2, ACT_GELU), [x.to(DEV)], hint=1 << 16)
 
 
-@pytest.mark.parametrize("nf,r,H,W", [(8, 4, 24, 78), (8, 4, 7, 21), (8, 2, 13, 29), (16, 2, 24, 78), (16, 2, 5, 9),
+@pytest.mark.parametrize("nf,r,H,W", [(8, 4, 24, 78), (8, 4, 7, 21), (8, 2, 13, 29), (16, 2, 24, 78), (16, 2, 5, 9), (16, 2, 37, 61),
                                       (16, 4, 6, 17), (8, 4, 96, 312), (8, 2, 130, 301), (8, 4, 1, 1),
                                       (8, 4, 9, 17), (8, 4, 33, 50)])
 def test_shuffle_tail(nf, r, H, W):
