@@ -669,8 +669,7 @@ __device__ __forceinline__ void tconvt3_body(const esm_conv_desc& a, int ncg, co
     // fused 1x1: weights, BN and the extra sources at this lane's output pixels, in flight during the K loop
     Up1Ops<(XB > 0 ? XB : 1)> u1;
     float bx1[2][NT][(XB > 0 ? XB : 1)];
-    if constexpr (XB > 0) {
-        static_assert(MT == 1, "fused 1x1: one cout tile");
+    if constexpr (XB > 0 && MT == 1) {  // (two tiles: loaded in the epilogue, the K loop needs the registers)
         const esm_conv_desc& bb = *bp;
         up1_weights(u1, bb, a.Cout, lane);
         const Up1Src us = up1_src(bb, b, !D2);
@@ -739,7 +738,64 @@ __device__ __forceinline__ void tconvt3_body(const esm_conv_desc& a, int ncg, co
     // ---- epilogue: lane (g, n) holds output columns 2m, 2m + 1 (m = xm0 + n) of rows 4g + j
     const int x = 2 * (xm0 + n);
     const int z = D2 ? 0 : 2 * (zm0 + zw) + qd;
-    if constexpr (XB > 0) {
+    static_assert(XB == 0 || MT <= 2, "fused 1x1: one or two cout tiles");
+    if constexpr (XB > 0 && MT == 2) {
+        // two tiles (round 6, conv_up1.h Up1Ops2): the 1x1's operands and the extra sources, loaded here
+        const esm_conv_desc& bb = *bp;
+        Up1Ops2<XB> u2;
+        up1_weights2(u2, bb, a.Cout, lane);
+        const Up1Src us = up1_src(bb, b, !D2);
+        const __amdgpu_buffer_rsrc_t rb_ = __builtin_amdgcn_make_buffer_rsrc(
+            bb.out + b * bb.ob, static_cast<short>(0),
+            4 * ((bb.Cout - 1) * static_cast<int>(bb.oc) + (D2 ? 0 : (bb.Do - 1) * static_cast<int>(bb.od)) +
+                 (bb.Ho - 1) * static_cast<int>(bb.oh) + bb.Wo),
+            0x00020000);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int y = 2 * (ym0 + yw * NT + nt) + qh;
+            const int orow = 4 * ((D2 ? 0 : z * static_cast<int>(bb.od)) + y * static_cast<int>(bb.oh));
+            const bool rok = y < bb.Ho && z < bb.Do;
+            float bx[2][XB];
+            if constexpr (PAIR) {
+                up1_extra2(bx[0], bx[1], us, bb, a.Cout, lane, z, y, x);
+            } else {
+#pragma unroll
+                for (int qw = 0; qw < 2; ++qw) up1_extra(bx[qw], us, bb, a.Cout, lane, z, y, x + qw);
+            }
+            floatx4 o[2][2];  // [qw][mb]
+#pragma unroll
+            for (int qw = 0; qw < 2; ++qw) {
+                float yv[2][4];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) yv[mt][j] = gelu_erf(acc[qw][nt][mt][j] * scl[mt][j] + shf[mt][j]);
+                up1_finish2(o[qw], u2, yv, bx[qw]);
+            }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 16 * mb + 4 * g + j;
+                    if constexpr (PAIR) {
+                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                        const unsigned vo = (rok && x < bb.Wo && co < bb.Cout)
+                                                ? 4u * static_cast<unsigned>(co * static_cast<int>(bb.oc) + x) : kOOB;
+                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(o[0][mb][j]), __float_as_uint(o[1][mb][j])},
+                                                              rb_, static_cast<int>(vo), rok ? orow : 0, kStoreAux);
+                    } else {
+#pragma unroll
+                        for (int qw = 0; qw < 2; ++qw) {
+                            const unsigned vo = (rok && x + qw < bb.Wo && co < bb.Cout)
+                                                    ? 4u * static_cast<unsigned>(co * static_cast<int>(bb.oc) + x + qw) : kOOB;
+                            store_b32(__float_as_uint(o[qw][mb][j]), rb_, static_cast<int>(vo), rok ? orow : 0);
+                        }
+                    }
+                }
+        }
+        return;
+    }
+    if constexpr (XB > 0 && MT == 1) {
         const esm_conv_desc& bb = *bp;
         const __amdgpu_buffer_rsrc_t rb_ = __builtin_amdgcn_make_buffer_rsrc(
             bb.out + b * bb.ob, static_cast<short>(0),
@@ -839,13 +895,14 @@ __global__ void __launch_bounds__(kT3Threads) tconvt3_kernel(const esm_conv_desc
     tconvt3_body<MT, NT, ACT, PLAIN, D2, 0>(a, ncg, nullptr);
 }
 
-// ConvTranspose + crop + cat + 1x1 (conv_up1.h); PAIR: 8-byte extra-source loads and output stores
-template <int NT, bool D2, int XB, bool PAIR>
+// ConvTranspose + crop + cat + 1x1 (conv_up1.h); PAIR: 8-byte extra-source loads and output stores; MT: cout tiles of
+// both convs (2: 17-32 couts, round 6)
+template <int MT, int NT, bool D2, int XB, bool PAIR>
 __global__ void __launch_bounds__(kT3Threads) tconvt3_up1_kernel(const esm_conv_desc a, const esm_conv_desc b) {
-    tconvt3_body<1, NT, ESM_ACT_GELU, true, D2, XB, PAIR>(a, 1, &b);
+    tconvt3_body<MT, NT, ESM_ACT_GELU, true, D2, XB, PAIR>(a, 1, &b);
 }
 
-template <int NT, bool D2>
+template <int NT, bool D2, int MT = 1>
 int launch_tt3_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     const long long z = D2 ? static_cast<long long>(a.B) * 2 : static_cast<long long>(a.B) * ((a.Di + 3) / 4) * 4;
     const long long gy = ceil_div(a.Hi, D2 ? 4 * NT : NT);
@@ -858,14 +915,20 @@ int launch_tt3_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s
 #define ESM_UP1(X)                                                                                   \
     do {                                                                                             \
         if (pair)                                                                                    \
-            hipLaunchKernelGGL((tconvt3_up1_kernel<NT, D2, X, true>), grid, dim3(kT3Threads), 0, s, a, b); \
+            hipLaunchKernelGGL((tconvt3_up1_kernel<MT, NT, D2, X, true>), grid, dim3(kT3Threads), 0, s, a, b); \
         else                                                                                         \
-            hipLaunchKernelGGL((tconvt3_up1_kernel<NT, D2, X, false>), grid, dim3(kT3Threads), 0, s, a, b); \
+            hipLaunchKernelGGL((tconvt3_up1_kernel<MT, NT, D2, X, false>), grid, dim3(kT3Threads), 0, s, a, b); \
     } while (0)
-    if (xb <= 4) ESM_UP1(4);
-    else if (xb <= 8) ESM_UP1(8);
-    else if (xb <= 10) ESM_UP1(10);
-    else ESM_UP1(12);
+    if constexpr (MT == 2) {  // (<= 32 extra channels: conv_up1.hip)
+        if (xb <= 4) ESM_UP1(4);
+        else if (xb <= 6) ESM_UP1(6);
+        else ESM_UP1(8);
+    } else {
+        if (xb <= 4) ESM_UP1(4);
+        else if (xb <= 8) ESM_UP1(8);
+        else if (xb <= 10) ESM_UP1(10);
+        else ESM_UP1(12);
+    }
 #undef ESM_UP1
     return check_launch("conv(tile3 transposed + 1x1)");
 }
@@ -1013,6 +1076,10 @@ int launch_tile_up1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t 
     const bool d3 = a.kd == 4;
     if (!(d3 ? tile3_ok(a) : tile2_ok(a))) return arg_error("convt_1x1: the tiled form cannot run this transposed conv");
     const int rsel = (a.hint >> 26) & 3;
+    if (a.Cout > 16 || b.Cout > 16) {  // two cout tiles (3-D only: conv_up1.hip)
+        if (!d3) return arg_error("convt_1x1: two cout tiles for the 3-D form only");
+        return rsel == 1 ? launch_tt3_up1<1, false, 2>(a, b, s) : launch_tt3_up1<2, false, 2>(a, b, s);
+    }
     if (d3) return rsel == 1 ? launch_tt3_up1<1, false>(a, b, s) : launch_tt3_up1<2, false>(a, b, s);
     return rsel == 1 ? launch_tt3_up1<1, true>(a, b, s) : launch_tt3_up1<2, true>(a, b, s);
 }

@@ -140,22 +140,82 @@ __device__ __forceinline__ floatx4 up1_finish(const Up1Ops<XB>& u, const float (
     return o;
 }
 
+// Two cout tiles on both sides (round 6: the L hourglass's conv2_up 40 -> 24 + agg_1.0 48 -> 24): the transposed
+// conv's channels 16 mt + 4q + r (tile mt, accumulator row r) feed the 1x1's k-step (mt, r); the 1x1's outputs run
+// as two tiles mb.  A operands wy[mb][mt][r] = W_b[16 mb + i][16 mt + 4 q + r], wx[mb][cb] = W_b[16 mb + i][Cy + 4 cb + q].
+template <int XB>
+struct Up1Ops2 {
+    float wy[2][2][4];
+    float wx[2][XB];
+    float s2[2][4], h2[2][4];
+};
+
+template <int XB>
+__device__ __forceinline__ void up1_weights2(Up1Ops2<XB>& u, const esm_conv_desc& b, int Cy, int lane) {
+    const int i = lane & 15, q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b.w), static_cast<short>(0),
+                                                                         4 * b.cin_pad * b.cout_pad, 0x00020000);
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int co = 16 * mb + i;
+        const bool iok = co < b.Cout;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * mt + 4 * q + r;
+                u.wy[mb][mt][r] = buf_load_s(wrs, (iok && c < Cy) ? 4u * static_cast<unsigned>(c * b.cout_pad + co) : kOOB, 0);
+            }
+#pragma unroll
+        for (int cb = 0; cb < XB; ++cb) {
+            const int c = Cy + 4 * cb + q;
+            u.wx[mb][cb] = buf_load_s(wrs, (iok && c < b.Cin) ? 4u * static_cast<unsigned>(c * b.cout_pad + co) : kOOB, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int cc = min(16 * mb + 4 * q + r, b.Cout - 1);
+            u.s2[mb][r] = b.scale[cc];
+            u.h2[mb][r] = b.shift[cc];
+        }
+    }
+}
+
+// o[mb][r] = GELU(BN_b(sum_k W[16 mb + 4q + r][k] x[k][pixel n])) for lane (n, q); y[mt][r]: the transposed conv's
+// channel 16 mt + 4q + r after its BN + GELU
+template <int XB>
+__device__ __forceinline__ void up1_finish2(floatx4 (&o)[2], const Up1Ops2<XB>& u, const float (&y)[2][4],
+                                            const float (&bx)[XB]) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        floatx4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d = __builtin_amdgcn_mfma_f32_16x16x4f32(u.wy[mb][mt][r], y[mt][r], d, 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < XB; ++cb) d = __builtin_amdgcn_mfma_f32_16x16x4f32(u.wx[mb][cb], bx[cb], d, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[mb][r] = gelu_erf(d[r] * u.s2[mb][r] + u.h2[mb][r]);
+    }
+}
+
 // Host-side validation of a (transposed conv) + b (1x1 over [a's cropped output, extra sources]); xb_max:
 // the extra k-steps the chosen kernel holds.  ESM_OK or ESM_ERR_ARG with the message set.
-inline int up1_check(const esm_conv_desc& a, const esm_conv_desc& b, int xb_max) {
+inline int up1_check(const esm_conv_desc& a, const esm_conv_desc& b, int xb_max, int cout_max = 16) {
     const bool d3 = a.kd > 1 || a.Di > 1 || a.Do > 1 || (a.transposed && a.kd == 4);
     if (!a.transposed || a.kh != 4 || a.stride != 2 || a.nsrc != 1) return arg_error("convt_1x1: a must be a k4 s2 transposed conv");
     if (a.act != ESM_ACT_GELU || !a.scale || !a.shift || a.mul || a.res || a.up || a.out2 || a.post_scale != 1.f)
         return arg_error("convt_1x1: a must be a BasicConv (BN + GELU, plain epilogue)");
-    if (a.Cout < 1 || a.Cout > 16 || (a.Cout & 3)) return arg_error("convt_1x1: a.Cout must be 4, 8, 12 or 16");
+    if (a.Cout < 1 || a.Cout > cout_max || (a.Cout & 3))
+        return arg_error("convt_1x1: a.Cout must be a multiple of 4, <= 16 (<= 32: the tiled form, 3-D, <= 32 extra channels)");
     if (b.transposed || b.kh != 1 || b.kw != 1 || b.kd != 1 || b.stride != 1 || b.ph || b.pw || b.pd)
         return arg_error("convt_1x1: b must be a 1x1 stride-1 conv");
     if (b.act != ESM_ACT_GELU || !b.out || !b.scale || !b.shift || b.mul || b.res || b.up || b.out2 ||
         b.post_scale != 1.f || b.shuffle > 1)
         return arg_error("convt_1x1: b must be a BasicConv (BN + GELU, plain epilogue)");
     if (b.pre && d3) return arg_error("convt_1x1: a partial sum (pre) for the 2-D form only");
-    if (b.nsrc < 2 || b.src[0].C != a.Cout || b.Cout < 1 || b.Cout > 16 || b.B != a.B)
-        return arg_error("convt_1x1: b.src[0] must be a's output, b.Cout <= 16");
+    if (b.nsrc < 2 || b.src[0].C != a.Cout || b.Cout < 1 || b.Cout > cout_max || b.B != a.B)
+        return arg_error("convt_1x1: b.src[0] must be a's output, b.Cout <= 16 (<= 32: the tiled form)");
     if (b.Hi > a.Ho || b.Wi > a.Wo || b.Di > a.Do || b.Ho != b.Hi || b.Wo != b.Wi || b.Do != b.Di ||
         (d3 ? (b.Di < 1) : (b.Di != 1)))
         return arg_error("convt_1x1: b's extent must be a crop of a's output");

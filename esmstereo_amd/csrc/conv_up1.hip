@@ -21,14 +21,20 @@ int up1_validate(const esm_conv_desc& a, const esm_conv_desc& b) {
     if (!ac.out) ac.out = b.out;  // a's output is never written; conv_check wants a pointer
     int rc = conv_check(ac);
     if (rc == ESM_OK) rc = conv_check(b);
-    if (rc == ESM_OK) rc = up1_check(a, b, kUp1MaxXB);
-    return rc;
+    if (rc != ESM_OK) return rc;
+    // 17-32 couts on either side: the two-tile tiled form only (3-D, <= 32 extra channels)
+    const bool wide = a.Cout > 16 || b.Cout > 16;
+    const bool d3 = a.kd == 4;
+    if (wide && (!d3 || b.Cin - a.Cout > 32))
+        return arg_error("convt_1x1: more than 16 couts only for the 3-D tiled form with <= 32 extra channels");
+    return up1_check(a, b, wide ? 8 : kUp1MaxXB, wide ? 32 : 16);
 }
 
 int launch_convt_1x1(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
     const int rc = up1_validate(a, b);
     if (rc != ESM_OK) return rc;
-    const bool tile = (a.hint & (1 << 23)) || (!(a.hint & (1 << 21)) && !small_auto(a));
+    const bool wide = a.Cout > 16 || b.Cout > 16;
+    const bool tile = wide || (a.hint & (1 << 23)) || (!(a.hint & (1 << 21)) && !small_auto(a));
     return tile ? launch_tile_up1(a, b, s) : launch_small_up1(a, b, s);
 }
 

@@ -810,12 +810,17 @@ def convt_1x1_supported(pa: PackedConv, pb: PackedConv, extra: Sequence[torch.Te
     """Python mirror of conv_up1.h up1_check (plus the on/off switch)."""
     if not CONVT1X1_ENABLED or not pa.transposed or pb.transposed or (pa.k, pa.stride, pa.pad) != (4, 2, 1):
         return False
-    if pa.act != ACT_GELU or pa.scale is None or pa.shift is None or pa.cout > 16 or pa.cout % 4:
+    # 17-32 couts on either side: the two-tile 3-D tiled form, <= 32 extra channels (round 6: L's conv2_up + agg_1.0)
+    wide = pa.cout > 16 or pb.cout > 16
+    if pa.act != ACT_GELU or pa.scale is None or pa.shift is None or pa.cout > 32 or pa.cout % 4:
         return False
-    if (pb.k, pb.stride, pb.pad) != (1, 1, 0) or pb.act != ACT_GELU or pb.cout > 16 or pb.nd != pa.nd:
+    if (pb.k, pb.stride, pb.pad) != (1, 1, 0) or pb.act != ACT_GELU or pb.cout > 32 or pb.nd != pa.nd:
+        return False
+    if wide and (pa.nd != 3 or pa.cout < 2):
         return False
     cx = sum(int(t.shape[1]) for t in extra)
-    return 1 <= len(extra) <= 2 and all(int(t.shape[1]) % 4 == 0 for t in extra) and 4 <= cx <= CONVT1X1_MAX_EXTRA
+    return 1 <= len(extra) <= 2 and all(int(t.shape[1]) % 4 == 0 for t in extra) and \
+        4 <= cx <= (32 if wide else CONVT1X1_MAX_EXTRA)
 
 
 def run_convt_1x1(ctx: Ctx, pa: PackedConv, srcs: Sequence[torch.Tensor], pb: PackedConv, extra: Sequence[torch.Tensor],

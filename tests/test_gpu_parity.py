@@ -910,6 +910,11 @@ UP1_CASES = [  # (nd, cin, cy, extra channels, coutb, input grid, crop, B, hint 
     (3, 20, 16, (8, 4), 8, (3, 5, 10), (6, 9, 20), 2, 0x4800000),      # 3-D tiled rows 1, three sources
     (2, 12, 12, (16, 32), 16, (11, 19), (21, 37), 2, 0x8800000),       # 2-D tiled, odd crop, batch 2
     (2, 12, 4, (48,), 5, (11, 19), (22, 37), 2, 0),                    # 4 couts, 48 extra channels
+    # round 6: two cout tiles (3-D tiled form): L aggregation conv2_up 40 -> 24 + agg_1.0 (48 -> 24)
+    (3, 40, 24, (24,), 24, (3, 6, 20), (6, 12, 40), 2, 0),
+    (3, 40, 24, (24,), 24, (3, 6, 20), (6, 12, 40), 1, 0x4800000),     # rows 1
+    (3, 32, 20, (8, 4), 28, (3, 5, 9), (5, 9, 17), 2, 0),              # ragged crop, 20 / 28 couts, three sources
+    (3, 24, 32, (32,), 32, (2, 4, 11), (4, 8, 22), 1, 0),              # 32 couts, 32 extra channels
 ]
 
 
