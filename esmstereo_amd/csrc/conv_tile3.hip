@@ -29,9 +29,13 @@ namespace conv {
 namespace {
 
 constexpr int kT3Threads = 256;
+constexpr bool kT3Dma = true;  // buffer-to-LDS staging where a form has it (hint bit 28 turns it off per launch)
 
 // D2: a 2-D conv (one plane, kd = 1): the same pipeline with the depth dimension of extent 1
-template <int S, int K, int NT, int WZ, bool PZ, int MT, bool D2 = false>
+// DMA (round 6): the input window is staged by buffer_load ... lds (global -> LDS, no staging registers): per
+// channel NCH chunks of 64 consecutive window elements, one wave-instruction each, so a channel's LDS stride is
+// NCH * 64 + CMOD (the chunk tail lanes write zeros into the padding)
+template <int S, int K, int NT, int WZ, bool PZ, int MT, bool D2 = false, bool DMA = false>
 struct T3Geo {
     static constexpr int WY = 4 / WZ;                     // waves along y
     static constexpr int ZB = PZ ? 2 * WZ : WZ;           // output planes per workgroup
@@ -41,7 +45,8 @@ struct T3Geo {
     static constexpr int PLANE = IY * IX;
     static constexpr int CS0 = IZ * PLANE;
     static constexpr int CMOD = S == 1 ? 16 : 1;          // channel stride mod 32 (bank offset of lanes 16..31)
-    static constexpr int CS = CS0 + ((CMOD - CS0 % 32) % 32 + 32) % 32;
+    static constexpr int NCH = (CS0 + 63) / 64;
+    static constexpr int CS = DMA ? NCH * 64 + CMOD : CS0 + ((CMOD - CS0 % 32) % 32 + 32) % 32;
     static constexpr int XE = 4 * CS0;                    // staged input elements per k-step
     static constexpr int XL = 4 * CS;                     // LDS floats per input buffer
     static constexpr int TAPS = KD * K * K;
@@ -59,14 +64,20 @@ struct T3Geo {
 // straight into registers (36, or 27 MT, per k-step, reloaded for the next k-step right after their last MFMA)
 // instead of the workgroup staging them in LDS: 18 KB less LDS per workgroup (agg at L-K: 2 -> 4 workgroups per
 // CU), no weight stores
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false, bool WREG = false>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int ACT, bool PLAIN, int NS = 1, bool D2 = false, bool WREG = false,
+          bool DMA = false>
 __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) tconv3_kernel(const esm_conv_desc a, int ncg) {
-    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
+    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2, DMA>;
+    static_assert(!DMA || (WREG && NS == 1), "DMA staging: register weights, one source");
     static_assert(!WREG || PZ || (K == 3 && !D2 && NS == 1), "register weights: plane pairs or 3x3x3 MT");
     constexpr int NWA = PZ ? 36 : G::TAPS * MT;  // register A operands per k-step (WREG)
     constexpr int IY = G::IY, IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS;
-    constexpr int XR = G::XR, WR = WREG ? 1 : G::WR, NR = G::NR;
-    __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
+    constexpr int XR = DMA ? 1 : G::XR, WR = WREG ? 1 : G::WR, NR = G::NR;
+    // (two arrays, not one [2][..]: with DMA staging the waitcnt pass can then tell the buffer being filled from
+    // the one being read)
+    __shared__ __attribute__((aligned(16))) float xs0[G::XL];
+    __shared__ __attribute__((aligned(16))) float xs1[G::XL];
+    auto xsb = [&](int buf) __attribute__((always_inline)) { return buf ? xs1 : xs0; };
     __shared__ __attribute__((aligned(16))) float ws[WREG ? 1 : 2][WREG ? 1 : G::WL];
 
     const int tid = threadIdx.x;
@@ -122,7 +133,7 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
     // from e where used: only the global offset is kept in a register)
     unsigned xoff[NS][XR];
 #pragma unroll
-    for (int k = 0; k < XR; ++k) {
+    for (int k = 0; k < (DMA ? 0 : XR); ++k) {
         const int e = tid + k * kT3Threads;
         const int ix = e % IX, iy = (e / IX) % IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
         const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
@@ -159,6 +170,35 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
         wdst[k] = dst;
     }
     float xv[XR], wv[WR];
+    // DMA: wave w issues the chunks i = w + 4 k (k < NCH) of the 4 x NCH per k-step: channel i / NCH, window elements
+    // 64 (i % NCH) + lane (past the window: zeros into the channel's padding)
+    constexpr int NCH = G::NCH;
+    unsigned doff[DMA ? NCH : 1];
+    if constexpr (DMA) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            const int i = wave + 4 * k, c = i / NCH, e = (i - c * NCH) * 64 + lane;
+            const int ix = e % IX, iy = (e / IX) % IY, iz = e / PLANE;
+            const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
+            const bool ok = e < G::CS0 && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+            doff[k] = ok ? 4u * static_cast<unsigned>(c * sc0 + zi * sd0 + yi * sh0 + xi) : kOOB;
+        }
+    }
+    auto stage_dma = [&](int c0, int buf) __attribute__((always_inline)) {
+        if constexpr (DMA) {
+#pragma unroll
+            for (int k = 0; k < NCH; ++k) {
+                const int i = wave + 4 * k, c = i / NCH;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs0, (__attribute__((address_space(3))) void*)(xsb(buf) + c * CS + (i - c * NCH) * 64), 4,
+                    c0 + c < a.Cin ? doff[k] : kOOB, 4 * c0 * sc0, 0, 0);
+            }
+        }
+    };
+    // DMA: the LDS writes of the buffer-to-LDS loads land before the barrier that publishes them
+    auto dma_wait = [&]() __attribute__((always_inline)) {
+        if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    };
     // the k-step's loads from source Q (compile-time: every array index stays constant; a run-time select
     // between xoff[0][k] and xoff[1][k] becomes a dynamic index of a private array, i.e. scratch)
     auto load_src = [&](auto qc, int c0) __attribute__((always_inline)) {
@@ -168,7 +208,7 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
         const int cq = c0 - (Q == 0 ? 0 : (Q == 1 ? lo1 : lo2));
         const int scq = Q == 0 ? sc0 : (Q == 1 ? sc1 : sc2);
 #pragma unroll
-        for (int k = 0; k < XR; ++k) {
+        for (int k = 0; k < (DMA ? 0 : XR); ++k) {
             const int ci = (tid + k * kT3Threads) / G::CS0;
             xv[k] = buf_load_s(rq, c0 + ci < a.Cin ? xoff[Q][k] : kOOB, 4 * cq * scq);
         }
@@ -189,9 +229,9 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
     };
     auto stage_store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < XR; ++k) {
+        for (int k = 0; k < (DMA ? 0 : XR); ++k) {
             const int e = tid + k * kT3Threads;
-            if (e < G::XE) xs[buf][e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
+            if (e < G::XE) xsb(buf)[e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
         }
         if constexpr (!WREG) {
 #pragma unroll
@@ -256,12 +296,17 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
 #pragma unroll
         for (int i = 0; i < NWA; ++i) wreg_load(i, 0);
     }
+    stage_dma(0, 0);
     stage_store(0);
+    dma_wait();
     __syncthreads();
     for (int ch = 0; ch < nchunk; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
-        const float* xw = &xs[buf][g * CS + (yw * NT * S) * IX + n * S];
+        if (ch + 1 < nchunk) {  // next k-step's loads in flight during the MFMAs
+            stage_load(4 * (ch + 1));
+            stage_dma(4 * (ch + 1), buf ^ 1);
+        }
+        const float* xw = xsb(buf) + g * CS + (yw * NT * S) * IX + n * S;
         if constexpr (PZ) {
             const float* wp = &ws[WREG ? 0 : buf][g * 16 + n];
 #pragma unroll
@@ -309,6 +354,7 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
                 }
         }
         if (ch + 1 < nchunk) stage_store(buf ^ 1);
+        dma_wait();
         __syncthreads();
     }
 
@@ -367,22 +413,27 @@ __global__ void __launch_bounds__(kT3Threads, (WREG && !PZ && MT <= 2) ? 4 : 1) 
 // form's, so the result is bit-identical to it.  Plain BasicConv epilogue only (BN + GELU).
 // WZ: waves along z (plane pairs per workgroup; 4 / WZ waves along y): 2 where Do is not a multiple of 8 (the
 // 12-plane conv2.1 / agg_0.1 at L-K: 16 planes computed for 12 with 4)
-template <int MF, int NT, int WZ = 4>
+// DMA: the input window staged global -> LDS directly (as T3Geo's DMA)
+template <int MF, int NT, int WZ = 4, bool DMA = false>
 struct HzGeo {
     static constexpr int WY = 4 / WZ, ZB = 2 * WZ, YB = WY * NT;
     static constexpr int IZ = ZB + 2, IY = YB + 2, IX = 18, PLANE = IY * IX, CS0 = IZ * PLANE;
-    static constexpr int CS = CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;  // channel stride = 16 mod 32 banks
+    static constexpr int NCH = (CS0 + 63) / 64;
+    static constexpr int CS = DMA ? NCH * 64 + 16 : CS0 + ((16 - CS0 % 32) % 32 + 32) % 32;  // = 16 mod 32 banks
     static constexpr int XE = 4 * CS0, XL = 4 * CS, XR = (XE + kT3Threads - 1) / kT3Threads;
     static constexpr int WCS = MF % 2 ? 16 * MF : 16 * MF + 16;      // weight row stride = 16 mod 32
     static constexpr int WE = 27 * 4 * 16 * MF, WL = 27 * 4 * WCS, WR = (WE + kT3Threads - 1) / kT3Threads;
     static constexpr int NR = NT + 2;
 };
 
-template <int MF, int NT, int WZ>
+template <int MF, int NT, int WZ, bool DMA>
 __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_desc a) {
-    using G = HzGeo<MF, NT, WZ>;
-    constexpr int IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS, XR = G::XR, WR = G::WR, NR = G::NR;
-    __shared__ __attribute__((aligned(16))) float xs[2][G::XL];
+    using G = HzGeo<MF, NT, WZ, DMA>;
+    constexpr int IX = G::IX, PLANE = G::PLANE, CS = G::CS, WCS = G::WCS, WR = G::WR, NR = G::NR;
+    constexpr int XR = DMA ? 1 : G::XR, NCH = G::NCH;
+    __shared__ __attribute__((aligned(16))) float xs0[G::XL];
+    __shared__ __attribute__((aligned(16))) float xs1[G::XL];
+    auto xsb = [&](int buf) __attribute__((always_inline)) { return buf ? xs1 : xs0; };
     __shared__ __attribute__((aligned(16))) float ws[2][G::WL];
 
     const int tid = threadIdx.x;
@@ -406,7 +457,7 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
 
     unsigned xoff[XR];
 #pragma unroll
-    for (int k = 0; k < XR; ++k) {
+    for (int k = 0; k < (DMA ? 0 : XR); ++k) {
         const int e = tid + k * kT3Threads;
         const int ix = e % IX, iy = (e / IX) % G::IY, iz = (e / PLANE) % G::IZ, ci = e / G::CS0;
         const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
@@ -434,10 +485,35 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
     auto wreg_load = [&](int i, int c0) __attribute__((always_inline)) {
         wa[i] = buf_load_s(wrs, wpo[i / 9], 4 * ((i % 9) * a.cin_pad + c0) * a.cout_pad);
     };
+    unsigned doff[DMA ? NCH : 1];  // DMA: wave w's chunks i = w + 4 k: channel i / NCH, elements 64 (i % NCH) + lane
+    if constexpr (DMA) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            const int i = wave + 4 * k, c = i / NCH, e = (i - c * NCH) * 64 + lane;
+            const int ix = e % IX, iy = (e / IX) % G::IY, iz = e / PLANE;
+            const int zi = zi0 + iz, yi = yi0 + iy, xi = xi0 + ix;
+            const bool ok = e < G::CS0 && zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi && xi >= 0 && xi < a.Wi;
+            doff[k] = ok ? 4u * static_cast<unsigned>(c * sc + zi * sd + yi * sh + xi) : kOOB;
+        }
+    }
+    auto stage_dma = [&](int c0, int buf) __attribute__((always_inline)) {
+        if constexpr (DMA) {
+#pragma unroll
+            for (int k = 0; k < NCH; ++k) {
+                const int i = wave + 4 * k, c = i / NCH;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(xsb(buf) + c * CS + (i - c * NCH) * 64), 4,
+                    c0 + c < a.Cin ? doff[k] : kOOB, 4 * c0 * sc, 0, 0);
+            }
+        }
+    };
+    auto dma_wait = [&]() __attribute__((always_inline)) {
+        if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA's LDS writes landed
+    };
     float xv[XR], wv[WR];
     auto stage_load = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < XR; ++k) {
+        for (int k = 0; k < (DMA ? 0 : XR); ++k) {
             const int ci = (tid + k * kT3Threads) / G::CS0;
             xv[k] = buf_load_s(rs, c0 + ci < a.Cin ? xoff[k] : kOOB, 4 * c0 * sc);
         }
@@ -446,9 +522,9 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
     };
     auto stage_store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < XR; ++k) {
+        for (int k = 0; k < (DMA ? 0 : XR); ++k) {
             const int e = tid + k * kT3Threads;
-            if (e < G::XE) xs[buf][e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
+            if (e < G::XE) xsb(buf)[e + (e / G::CS0) * (CS - G::CS0)] = xv[k];
         }
 #pragma unroll
         for (int k = 0; k < WR; ++k)
@@ -466,14 +542,19 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
 
     const int nchunk = (a.Cin + 3) >> 2;
     stage_load(0);
+    stage_dma(0, 0);
 #pragma unroll
     for (int i = 0; i < 36; ++i) wreg_load(i, 0);
     stage_store(0);
+    dma_wait();
     __syncthreads();
     for (int ch = 0; ch < nchunk; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < nchunk) stage_load(4 * (ch + 1));  // next k-step's loads in flight during the MFMAs
-        const float* xw = &xs[buf][g * CS + yw * NT * IX + n];
+        if (ch + 1 < nchunk) {  // next k-step's loads in flight during the MFMAs
+            stage_load(4 * (ch + 1));
+            stage_dma(4 * (ch + 1), buf ^ 1);
+        }
+        const float* xw = xsb(buf) + g * CS + yw * NT * IX + n;
         const float* wp = &ws[buf][g * WCS + n];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -506,6 +587,7 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
                 }
             }
         if (ch + 1 < nchunk) stage_store(buf ^ 1);
+        dma_wait();
         __syncthreads();
     }
 
@@ -557,11 +639,18 @@ __global__ void __launch_bounds__(kT3Threads, 2) tconv3hz_kernel(const esm_conv_
 template <int MF, int NT, int WZ = 4>
 int launch_hz(const esm_conv_desc& a, hipStream_t s) {
     using G = HzGeo<MF, NT, WZ>;
+    // the input window by DMA for the 40-cout layers (conv2.1 / agg_0.1 at L-K B = 4: 101.7 -> 99.7 us in the graph),
+    // through registers for 24 couts (conv1.1: 229.4 vs 232.1 us with DMA; scripts/probes/op_hint_probe.py); hint bit
+    // 28 flips the choice (A/B)
+    const bool dma = ((a.hint >> 28) & 1) ? MF != 2 : (MF == 2 && kT3Dma);
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB);
     const long long gy = ceil_div(a.Ho, G::YB);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3 hz): grid too large");
     const dim3 grid(ceil_div(a.Wo, 16), static_cast<unsigned>(gy), static_cast<unsigned>(z));
-    hipLaunchKernelGGL((tconv3hz_kernel<MF, NT, WZ>), grid, dim3(kT3Threads), 0, s, a);
+    if (dma)
+        hipLaunchKernelGGL((tconv3hz_kernel<MF, NT, WZ, true>), grid, dim3(kT3Threads), 0, s, a);
+    else
+        hipLaunchKernelGGL((tconv3hz_kernel<MF, NT, WZ, false>), grid, dim3(kT3Threads), 0, s, a);
     return check_launch("conv(tile3 hz)");
 }
 
@@ -963,9 +1052,9 @@ int launch_tt3_mt(const esm_conv_desc& a, hipStream_t s) {
     return arg_error("conv(tile3 transposed): at most 96 output channels");
 }
 
-template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false, bool WREG = false>
+template <int S, int K, int MT, int NT, int WZ, bool PZ, int NS = 1, bool D2 = false, bool WREG = false, bool DMA = false>
 int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
-    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2>;
+    using G = T3Geo<S, K, NT, WZ, PZ, MT, D2, DMA>;
     const long long z = static_cast<long long>(a.B) * ((a.Do + G::ZB - 1) / G::ZB) * ncg;
     const long long gy = ceil_div(a.Ho, G::YB);
     if (z > 65535 || gy > 65535) return arg_error("conv(tile3): grid too large");
@@ -974,11 +1063,11 @@ int launch_t3(const esm_conv_desc& a, hipStream_t s, int ncg) {
                        static_cast<long long>(a.Cout) * a.oc + static_cast<long long>(a.Do) * a.od +
                                static_cast<long long>(a.Ho) * a.oh < (kOOB >> 2);
     if (plain)
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2, WREG>), grid, dim3(kT3Threads), 0,
-                           s, a, ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, ESM_ACT_GELU, true, NS, D2, WREG, DMA>), grid, dim3(kT3Threads),
+                           0, s, a, ncg);
     else
-        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2, WREG>), grid, dim3(kT3Threads), 0, s, a,
-                           ncg);
+        hipLaunchKernelGGL((tconv3_kernel<S, K, MT, NT, WZ, PZ, -1, false, NS, D2, WREG, DMA>), grid, dim3(kT3Threads), 0, s,
+                           a, ncg);
     return check_launch("conv(tile3)");
 }
 
@@ -998,12 +1087,11 @@ int launch_t3_mt(const esm_conv_desc& a, hipStream_t s) {
 }
 
 // stride 2, register weights: one cout group of 1..3 tiles
-template <int NT, int WZ>
+template <int NT, int WZ, bool DMA = false>
 int launch_t3_mtw(const esm_conv_desc& a, hipStream_t s) {
     const int tiles = (a.Cout + 15) / 16;
-    if (tiles == 1) return launch_t3<2, 3, 1, NT, WZ, false, 1, false, true>(a, s, 1);
-    if (tiles == 2) return launch_t3<2, 3, 2, NT, WZ, false, 1, false, true>(a, s, 1);
-    return launch_t3<2, 3, 3, NT, WZ, false, 1, false, true>(a, s, 1);
+    if (tiles == 1) return launch_t3<2, 3, 1, NT, WZ, false, 1, false, true, DMA>(a, s, 1);
+    return launch_t3<2, 3, 2, NT, WZ, false, 1, false, true, DMA>(a, s, 1);
 }
 
 // 1x1x1 over 1..3 sources
@@ -1129,9 +1217,13 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     if (a.stride == 2) {  // one row per wave unless asked (r04 probe, L-K B = 4: conv1.0 274 -> 226 us, conv2.0 92 -> 86)
         // round 6: the weights as register operands (<= 3 cout tiles per workgroup, one source); hint bit 29: LDS
         if (!((a.hint >> 29) & 1) && a.nsrc == 1 && a.Cout <= 32) {  // (3 tiles: 150 VGPRs, conv2.0 84 -> 88 us)
-            if (rsel == 2) return launch_t3_mtw<2, 2>(a, s);
+            // the input window staged global -> LDS directly (bit 28: through registers, A/B)
+            // (4 rows: the DMA window's channel padding would exceed 64 KB of LDS; measured at L-K B = 4 in the
+            // graph, scripts/probes/op_hint_probe.py: conv1.0 168.6 us with it at 2 rows, 161.2 without)
+            const bool dma = !((a.hint >> 28) & 1) && kT3Dma;
+            if (rsel == 2) return dma ? launch_t3_mtw<2, 2, true>(a, s) : launch_t3_mtw<2, 2>(a, s);
             if (rsel == 3) return launch_t3_mtw<4, 2>(a, s);
-            return launch_t3_mtw<1, 2>(a, s);
+            return dma ? launch_t3_mtw<1, 2, true>(a, s) : launch_t3_mtw<1, 2>(a, s);
         }
         if (rsel == 2) return launch_t3_mt<2, 3, 2, 2>(a, s);
         if (rsel == 3) return launch_t3_mt<2, 3, 4, 2>(a, s);
@@ -1139,10 +1231,19 @@ int launch_tile3(const esm_conv_desc& a, hipStream_t s) {
     }
     if (a.Cout <= 8) {  // plane pairs; hint bit 29: weights staged in LDS (round 5), else in registers (round 6)
         const bool lw = (a.hint >> 29) & 1;
-        if (rsel == 1) return lw ? launch_t3<1, 3, 1, 1, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 1, 4, true, 1, false, true>(a, s, 1);
+        // register weights: the input window staged global -> LDS directly (round 6), bit 28: through registers
+        const bool dma = !((a.hint >> 28) & 1) && kT3Dma;
+        if (rsel == 1)
+            return lw ? launch_t3<1, 3, 1, 1, 4, true>(a, s, 1)
+                      : (dma ? launch_t3<1, 3, 1, 1, 4, true, 1, false, true, true>(a, s, 1)
+                             : launch_t3<1, 3, 1, 1, 4, true, 1, false, true>(a, s, 1));
         if (rsel == 2 || (rsel == 0 && vox < (1LL << 20)))
-            return lw ? launch_t3<1, 3, 1, 2, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 2, 4, true, 1, false, true>(a, s, 1);
-        return lw ? launch_t3<1, 3, 1, 4, 4, true>(a, s, 1) : launch_t3<1, 3, 1, 4, 4, true, 1, false, true>(a, s, 1);
+            return lw ? launch_t3<1, 3, 1, 2, 4, true>(a, s, 1)
+                      : (dma ? launch_t3<1, 3, 1, 2, 4, true, 1, false, true, true>(a, s, 1)
+                             : launch_t3<1, 3, 1, 2, 4, true, 1, false, true>(a, s, 1));
+        return lw ? launch_t3<1, 3, 1, 4, 4, true>(a, s, 1)
+                  : (dma ? launch_t3<1, 3, 1, 4, 4, true, 1, false, true, true>(a, s, 1)
+                         : launch_t3<1, 3, 1, 4, 4, true, 1, false, true>(a, s, 1));
     }
     // 24 / 40 couts, plain BasicConv: the plane-pair hybrid (hint bit 29: the padded MT form, A/B); rows per wave
     // 2 / 4 for rsel 1 / 2-3, automatic 4 (2 on small volumes)

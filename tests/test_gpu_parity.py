@@ -302,6 +302,9 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
         outs[hint] = y
     if cout <= 8 and k == 3 and s == 1:
         assert torch.equal(outs[1 << 29], outs[0]) and torch.equal(outs[2 << 26 | 1 << 29], outs[2 << 26])
+        # round 6: buffer-to-LDS staging (default) bitwise the register staging (bit 28)
+        for rows in (1 << 26, 2 << 26):
+            assert torch.equal(run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 28), outs[rows]), hex(rows)
     if cout in (24, 40) and k == 3 and s == 1:
         # round 6: the plane-pair hybrid for 16 MF + 8 couts (default) is bitwise the padded MT form (bit 29)
         for rows in (1 << 26, 2 << 26):
@@ -310,9 +313,13 @@ def test_conv_tile3_form(cin, cout, k, s, shape, B):
             assert torch.equal(hz, mt), hex(rows)
     if k == 3 and s == 2 and cout <= 32:
         # round 6: the stride-2 MT form with register weights (default) is bitwise its LDS-weight form (bit 29)
+        # and its buffer-to-LDS staging (default) bitwise the register staging (bit 28)
         for rows in (0, 1 << 26, 2 << 26, 3 << 26):
             lw = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 29)
             assert torch.equal(lw, outs[rows]), hex(rows)
+            if rows != 3 << 26:
+                rg = run_conv(Ctx(DEV), p, [x.to(DEV)], hint=HINT_TILE3 | rows | 1 << 28)
+                assert torch.equal(rg, outs[rows]), hex(rows)
     res = torch.randn(ref.shape)
     mul = torch.rand(B, cout, ref.shape[3], ref.shape[4]) + 0.5
     want = _ref_conv([x], conv, bn, ACT_GELU, mul=mul, res=res)
