@@ -136,6 +136,10 @@ typedef struct {
                      split over two waves (partial rows summed once through LDS; R >= 4).  Bit 29 with SMALL:
                      8 waves per workgroup splitting K (layers with more than 4 channel groups); bit 29 on
                      the first desc of esm_conv_pair2_f32: regression source (see there).
+                     With TILE3 (round 6): bit 29 on a 1x1 = the pointwise streaming form (conv_pw.hip, chosen
+                     automatically for dense 1x1 BasicConvs over >= 2^16 pixels), on a 3x3x3 layer = its
+                     LDS-staged-weight / padded-MT variant (A/B); bit 28 on the register-weight 3-D forms flips
+                     the buffer-to-LDS (DMA) staging of the input window.
                      Bit 30 (any value of the other bits, including 0 = automatic): XCD-slab tile order for
                      the small / wide / wide3 / wideT / pair / single-output ConvT forms: each XCD runs a
                      contiguous band of tiles, so halo rows are fetched once per band instead of once per
