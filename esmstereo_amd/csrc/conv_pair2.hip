@@ -334,12 +334,7 @@ bool pair2_ok(const esm_conv_desc& a, const esm_conv_desc& b) {
     return 4 * last < static_cast<long long>(kOOB) && b.oc < (1 << 28) && b.oh < (1 << 28);
 }
 
-bool tiny3_ok(const esm_conv_desc& a, const esm_conv_desc& b);                       // conv_tiny3.hip
-int launch_tiny3(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s);  // conv_tiny3.hip
-
 int launch_pair2(const esm_conv_desc& a, const esm_conv_desc& b, hipStream_t s) {
-    // two 3x3x3 convs on a tiny volume (round 6: the hourglass's conv3 at S / M)
-    if (a.kd == 3 || b.kd == 3) return tiny3_ok(a, b) ? launch_tiny3(a, b, s) : arg_error("conv pair (3-D): unsupported pair");
     if (!pair2_ok(a, b)) return arg_error("conv pair: unsupported pair");
     if (a.kh == 5) return b.kh == 3 ? launch_p2_k<5, 1, 3>(a, b, s) : launch_p2_k<5, 1, 1>(a, b, s);
     if (a.kh == 1) return b.kh == 3 ? launch_p2_k<1, 1, 3>(a, b, s) : launch_p2_k<1, 1, 1>(a, b, s);

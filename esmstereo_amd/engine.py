@@ -756,31 +756,8 @@ def run_gwc_stem(ctx: Ctx, pc: PackedConv, L: torch.Tensor, R: torch.Tensor, G: 
 PAIR2_ENABLED = _ab("ESM_PAIR2", "1") != "0"
 
 
-# Two 3x3x3 BasicConvs on a tiny volume as one launch (conv_tiny3.hip, round 6: the hourglass's conv3 at S / M,
-# 60 output voxels at S-K); ESM_TINY3=0 keeps two launches (A/B)
-TINY3_ENABLED = _ab("ESM_TINY3", "0") != "0"
-TINY3_MAX_VOX = 128
-
-
-def tiny3_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
-    """Python mirror of conv_tiny3.hip tiny3_ok (plus the on/off switch)."""
-    if not TINY3_ENABLED or pa.nd != 3 or pb.nd != 3 or pa.transposed or pb.transposed or len(srcs) != 1:
-        return False
-    if (pa.k, pa.pad) != (3, 1) or (pb.k, pb.stride, pb.pad) != (3, 1, 1) or pa.stride not in (1, 2):
-        return False
-    if pa.act != ACT_GELU or pb.act != ACT_GELU or pa.shift is None or pb.shift is None:
-        return False
-    if pa.cout > 32 or pb.cout > 32 or pb.cin != pa.cout:
-        return False
-    D, H, W = (int(v) for v in srcs[0].shape[2:])
-    Do, Ho, Wo = ((v + 2 - 3) // pa.stride + 1 for v in (D, H, W))
-    return Do * Ho * Wo <= TINY3_MAX_VOX
-
-
 def pair2_supported(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> bool:
     """Python mirror of conv_pair2.hip pair2_ok (plus the on/off switch)."""
-    if pa.nd == 3:
-        return tiny3_supported(pa, pb, srcs)
     if not PAIR2_ENABLED or pa.nd != 2 or pb.nd != 2 or pa.transposed or pb.transposed:
         return False
     if pa.cout != 16 or pb.cin != 16 or pb.cout > 16 or pa.cin > (64 if pa.k == 1 else 48):
@@ -802,8 +779,6 @@ def pair2_auto(pa: PackedConv, pb: PackedConv, srcs: Sequence[torch.Tensor]) -> 
     stride-2 head + conv1.1 at 192x624: 23.6 vs 19.0)."""
     if not pair2_supported(pa, pb, srcs):
         return False
-    if pa.nd == 3:
-        return True  # (the tiny volumes: tiny3_supported)
     B = int(srcs[0].shape[0])
     Ho = (int(srcs[0].shape[2]) + 2 * pa.pad - pa.k) // pa.stride + 1
     Wo = (int(srcs[0].shape[3]) + 2 * pa.pad - pa.k) // pa.stride + 1

@@ -478,37 +478,6 @@ def test_conv_pointwise_form_fallback():
                _ref_conv([x], conv2, bn2, ACT_GELU)) < 1e-5
 
 
-TINY3_CASES = [  # (cin, c1, c2, stride of convA, input extent, B): two 3x3x3 BasicConvs on a tiny volume
-    (16, 24, 24, 2, (3, 6, 20), 1),   # S aggregation conv3 (60 output voxels)
-    (16, 24, 24, 2, (3, 6, 20), 2),   # batch 2
-    (12, 16, 16, 2, (3, 5, 9), 1),    # odd extents
-    (8, 32, 12, 1, (2, 4, 15), 2),    # stride 1, 120 voxels, two cout tiles then one
-    (20, 4, 28, 2, (4, 4, 4), 1),     # ragged channel counts
-]
-
-
-@pytest.mark.parametrize("cin,c1,c2,s,shape,B", TINY3_CASES)
-def test_conv_tiny3_pair(cin, c1, c2, s, shape, B):
-    """Two 3x3x3 BasicConvs on a tiny volume in one launch (conv_tiny3.hip, through esm_conv_pair2_f32) vs fp64 torch
-    of the two layers and vs two separate launches (relative 1e-5)."""
-    from esmstereo_amd.engine import pair2_supported, run_pair2
-    ca, ba = _mk(3, cin, c1, 3, s, 1, seed=61 + cin)
-    cb, bb = _mk(3, c1, c2, 3, 1, 1, seed=62 + c2)
-    x = torch.randn(B, cin, *shape)
-    ref = _ref_conv([_ref_conv([x], ca, ba, ACT_GELU)], cb, bb, ACT_GELU)
-    pa_, pb_ = pk(ca, ba, ACT_GELU), pk(cb, bb, ACT_GELU)
-    xd = [x.to(DEV)]
-    assert pair2_supported(pa_, pb_, xd)
-    ctx = Ctx(DEV)
-    y = run_pair2(ctx, pa_, xd, pb_, force=True)
-    torch.cuda.synchronize()
-    assert ctx.meta[-1]["kind"] == "conv_pair"
-    assert rel(y, ref) < 1e-5
-    two = run_conv(ctx, pb_, [run_conv(ctx, pa_, xd)])
-    assert rel(y, two) < 1e-5
-    assert torch.equal(run_pair2(Ctx(DEV), pa_, xd, pb_, force=True), y)  # deterministic
-
-
 HINT_SMALL = 1 << 21
 SMALL_CASES = [(3, [16], 16, 3, 1, False, (3, 6, 20)), (3, [24], 24, 3, 1, False, (2, 3, 10)),
                (3, [16], 24, 3, 2, False, (3, 6, 20)), (3, [12], 16, 3, 2, False, (6, 12, 39)),
