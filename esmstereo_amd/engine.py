@@ -949,6 +949,10 @@ def run_dwconv(ctx: Ctx, x: torch.Tensor, w: torch.Tensor, scale: Optional[torch
                k: int, stride: int, pad: int, act: int, tag: str = "dwconv") -> torch.Tensor:
     """Depthwise KxK conv (groups = C) + folded BN + activation (``esm_dwconv_f32``): timm's ``conv_dw -> bn``
     (+ act) of the backbone blocks.  ``w``: [C, K*K] contiguous."""
+    if stride <= 0 or k <= 0 or not 0 <= pad < k:
+        raise ValueError("dwconv: stride and K must be positive, 0 <= pad < K")
+    if x.dim() != 4 or x.stride(3) != 1:
+        raise ValueError("dwconv: a [B, C, H, W] input with unit W stride")
     require_device(x, "dwconv input")
     B, C, H, W = (int(v) for v in x.shape)
     Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1

@@ -178,3 +178,17 @@ def test_trt_signature_and_state_dict():
     assert list(inspect.signature(b.forward).parameters) == ["left", "right"]
     with pytest.raises(RuntimeError, match="ROCm"):
         b.eval()(torch.randn(1, 3, 64, 128), torch.randn(1, 3, 64, 128))
+
+
+def test_run_dwconv_rejects_bad_arguments():
+    """run_dwconv refuses a W-strided view and non-positive stride / K or bad padding on the host,
+    before any descriptor reaches the library."""
+    import torch as _t
+    from esmstereo_amd.engine import run_dwconv
+    x = _t.zeros(1, 4, 8, 16)
+    w = _t.zeros(4, 9)
+    for kw in (dict(k=3, stride=0, pad=1), dict(k=0, stride=1, pad=0), dict(k=3, stride=1, pad=3)):
+        with pytest.raises(ValueError):
+            run_dwconv(None, x, w, None, None, act=0, **kw)
+    with pytest.raises(ValueError):
+        run_dwconv(None, x[..., ::2], w, None, None, 3, 1, 1, 0)
