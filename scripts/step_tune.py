@@ -36,14 +36,15 @@ from autotune import CANDIDATES  # noqa: E402
 
 
 BATCH = 1  # --batch: pairs per plan (the L-K per-rank slice of configs[3] is B = 4)
+HW = (384, 1248, 192)  # --height / --width / --maxdisp (configs[2]: 544 x 960; configs[4]: 1024 x 1504 md256)
 
 
 def build(variant: str, dev):
     backbone, cvs = bench.VARIANTS[variant]
-    model = E.ESMStereo(192, True, False, backbone, cvs)
+    model = E.ESMStereo(HW[2], True, False, backbone, cvs)
     bench.seeded_init(model, 1234)
     model = model.eval().to(dev)
-    left, right = bench.synthetic_pair(BATCH, 384, 1248, 192, 100, dev)
+    left, right = bench.synthetic_pair(BATCH, HW[0], HW[1], HW[2], 100, dev)
     with torch.no_grad():
         ml, mr, att, up = model.prefix(left, right)
     B, C, h, w = (int(v) for v in ml.shape)
@@ -170,10 +171,14 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--only", default="", help="tune: comma-separated substrings of the op names to tune")
     ap.add_argument("--batch", type=int, default=1, help="pairs per plan (hint keys carry B)")
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--width", type=int, default=1248)
+    ap.add_argument("--maxdisp", type=int, default=192)
     ap.add_argument("--report", default=os.path.join(ROOT, "gpurun_out", "step_tune_report.json"))
     args = ap.parse_args()
-    global BATCH
+    global BATCH, HW
     BATCH = args.batch
+    HW = (args.height, args.width, args.maxdisp)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     variants = args.variants.split(",")
