@@ -23,9 +23,12 @@ __global__ void __launch_bounds__(kDwThreads) dwconv_kernel(const esm_dwconv_des
     constexpr int IWP = IW + 1;
     __shared__ float tile[IH * IWP];
     const int tid = threadIdx.x;
-    const int plane = blockIdx.z;  // b * C + c
+    // grid x = (b * C + c) * tiles_x + tile x (planes on x: the z grid's 65535 limit is below B * C of the
+    // backbone's [left; right] batch at configs[3]'s 32 pairs)
+    const int ntx = (a.Wo + kDwTX - 1) / kDwTX;
+    const int plane = blockIdx.x / ntx;
     const int b = plane / a.C, c = plane - (plane / a.C) * a.C;
-    const int oy0 = blockIdx.y * kDwTY, ox0 = blockIdx.x * kDwTX;
+    const int oy0 = blockIdx.y * kDwTY, ox0 = (blockIdx.x - plane * ntx) * kDwTX;
     const int iy0 = oy0 * S - a.pad, ix0 = ox0 * S - a.pad;
     const float* xp = a.x + b * a.xb + c * a.xc;
     for (int i = tid; i < IH * IW; i += kDwThreads) {
@@ -65,7 +68,7 @@ __global__ void __launch_bounds__(kDwThreads) dwconv_kernel(const esm_dwconv_des
 
 template <int K, int S>
 int launch_dw(const esm_dwconv_desc& a, hipStream_t s) {
-    const dim3 grid(ceil_div(a.Wo, kDwTX), ceil_div(a.Ho, kDwTY), static_cast<unsigned>(a.B * a.C));
+    const dim3 grid(static_cast<unsigned>(ceil_div(a.Wo, kDwTX) * a.B * a.C), ceil_div(a.Ho, kDwTY), 1);
     hipLaunchKernelGGL((dwconv_kernel<K, S>), grid, dim3(kDwThreads), 0, s, a);
     return check_launch("dwconv");
 }
@@ -84,8 +87,8 @@ int launch_dwconv(const esm_dwconv_desc* d, hipStream_t s) {
         return arg_error("dwconv: output extent inconsistent with K / stride / pad");
     if (a.xh < a.W || a.xc < static_cast<long long>(a.H) * a.xh || a.oh < a.Wo || a.oc < static_cast<long long>(a.Ho) * a.oh)
         return arg_error("dwconv: strides inconsistent with the extents");
-    if (static_cast<long long>(a.B) * a.C > 65535 || ceil_div(a.Ho, kDwTY) > 65535u)  // grid z / y limits
-        return arg_error("dwconv: grid too large");
+    if (static_cast<long long>(ceil_div(a.Wo, kDwTX)) * a.B * a.C > 0x7fffffffLL || ceil_div(a.Ho, kDwTY) > 65535u)
+        return arg_error("dwconv: grid too large");  // (grid x / y limits)
     if (a.K == 3 && a.stride == 1) return launch_dw<3, 1>(a, s);
     if (a.K == 3 && a.stride == 2) return launch_dw<3, 2>(a, s);
     if (a.K == 5 && a.stride == 1) return launch_dw<5, 1>(a, s);

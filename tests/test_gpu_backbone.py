@@ -82,3 +82,16 @@ def test_model_prefix_fast_vs_modules():
     flat = lambda o: [o[0], o[1], o[2]] + list(o[3])  # noqa: E731
     for i, (g, r) in enumerate(zip(flat(got), flat(ref))):
         assert rel(g, r.detach()) < 1e-4, (i, rel(g, r.detach()))
+
+
+def test_dwconv_many_planes():
+    """B * C above the 65535 z-grid limit (the backbone over [left; right] at configs[3]'s 32 pairs): the planes ride
+    on grid x."""
+    torch.manual_seed(7)
+    B, C, H, W, k = 72, 1000, 5, 6, 3
+    x = torch.randn(B, C, H, W)
+    w = torch.randn(C, 1, k, k) * 0.3
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    ref = F.conv2d(x.double(), w.double(), None, 1, 1, 1, C) * sc.double().view(1, C, 1, 1) + sh.double().view(1, C, 1, 1)
+    y = run_dwconv(Ctx(DEV), x.to(DEV), w.reshape(C, k * k).contiguous().to(DEV), sc.to(DEV), sh.to(DEV), k, 1, 1, ACT_NONE)
+    assert rel(y, ref) < 1e-5
